@@ -1,0 +1,166 @@
+/*
+ * llfe.h -- C ABI of libllfe.so, the MI355X (gfx950) batched image-feature backend.
+ *
+ * This is the drop-in boundary behind the reference's Python call sites
+ * (Kira7dn/Low_Level_Feature_Extraction @ 2025-05-23).  The reference has no FFI of
+ * its own -- its "plugin" surface is a set of static Python methods bound by direct
+ * import in app/api/v1/endpoints/analyze.py:15-26 -- so each entry point below names
+ * the reference function whose native work it replaces.  The Python mirror of those
+ * methods lives in low_level_feature_extraction_amd/ and reaches this ABI via ctypes
+ * (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *   - plain pointers and sizes only; no torch / numpy types.
+ *   - images are BGR, 8-bit, H x W x 3, rows contiguous (stride W*3), batches are
+ *     packed N x H x W x 3 (NHWC) with one shared H, W.
+ *   - "device" pointers live on the ctx's device (e.g. a torch tensor's data_ptr());
+ *     "host" pointers are ordinary CPU memory.
+ *   - every call returns LLFE_OK (0) or a negative LLFE_ERR_* code; no exception
+ *     crosses the ABI; llfe_last_error(ctx) returns a message for the last failure.
+ *   - a ctx is bound to one device and is not thread-safe; use one ctx per host
+ *     thread per GPU.  `stream` is a hipStream_t (NULL = the legacy default stream).
+ *   - calls are synchronous with respect to their host outputs: when a function
+ *     returns, every host output it wrote is valid.
+ */
+#ifndef LLFE_H
+#define LLFE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LLFE_ABI_VERSION 1
+
+#define LLFE_OK 0
+#define LLFE_ERR_INVALID (-1)
+#define LLFE_ERR_HIP (-2)
+#define LLFE_ERR_CAPACITY (-3)
+#define LLFE_ERR_OOM (-4)
+#define LLFE_ERR_UNSUPPORTED (-5)
+
+/* feature mask bits (FeatureType colors / shapes / shadows) */
+#define LLFE_FEATURE_COLORS 1u
+#define LLFE_FEATURE_SHAPES 2u
+#define LLFE_FEATURE_SHADOWS 4u
+
+/* shape type codes (ShapeAnalyzer.analyze_shapes @L159-172 type strings) */
+#define LLFE_SHAPE_UNKNOWN 0
+#define LLFE_SHAPE_TRIANGLE 1
+#define LLFE_SHAPE_RECTANGLE 2
+#define LLFE_SHAPE_CIRCLE 3
+#define LLFE_SHAPE_POLYGON 4
+
+/* validate_and_preprocess_image modes (app/services/analyze/utils.py:22-28) */
+#define LLFE_PRE_NONE 0
+#define LLFE_PRE_AUTO 1
+#define LLFE_PRE_HIGH_QUALITY 2
+#define LLFE_PRE_PERFORMANCE 3
+
+typedef struct llfe_ctx llfe_ctx;
+typedef void *llfe_stream; /* hipStream_t */
+
+typedef struct {
+    const uint8_t *data;   /* N x H x W x 3 BGR u8 */
+    int32_t n, height, width;
+    int32_t on_device;     /* 1: device pointer, 0: host pointer */
+    /* optional "parity mode" noise: N x H x W x 3 int8 in RGB channel order, i.e.
+     * exactly np.random.normal(0, 0.5, (H*W, 3)).astype(np.int8) per image
+     * (color_extractor.py:224).  NULL -> on-device Philox4x32-10 noise of the same
+     * distribution. */
+    const int8_t *noise;
+    int32_t noise_on_device;
+    int32_t reserved;
+    int64_t index_base;    /* global index of image 0 (seeds are per global index) */
+} llfe_batch;
+
+typedef struct {
+    /* colors: _get_dominant_colors + bincount (color_extractor.py:174-236) */
+    int32_t n_colors;          /* K = min(n_colors, U) centres (U when U <= 1) */
+    int32_t counts[5];         /* np.bincount(labels) per centre, k-means order */
+    uint8_t centers_rgb[5][3]; /* centers.astype(np.uint8), k-means order */
+    uint8_t pad_[1];
+    int64_t n_unique;          /* len(np.unique(pixels, axis=0)) */
+    double compactness;        /* best cv2.kmeans compactness */
+    /* shadows: processed[thresh == 255] sum / size (shadow pyc @L21-24) */
+    uint64_t shadow_sum;
+    uint64_t shadow_count;
+    /* shapes: slice [shape_offset, shape_offset + n_shapes) of the shapes array */
+    int64_t shape_offset;
+    int32_t n_shapes;
+    int32_t n_contours;        /* external contours before the area >= 100 filter */
+} llfe_image_result;
+
+typedef struct {
+    int32_t type; /* LLFE_SHAPE_* */
+    int32_t x, y, width, height;
+    int32_t pad_;
+    double border_radius;
+    double area;
+} llfe_shape;
+
+/* ---- context ---------------------------------------------------------- */
+int llfe_init(int device, llfe_ctx **out);
+int llfe_destroy(llfe_ctx *ctx);
+const char *llfe_last_error(llfe_ctx *ctx);
+int llfe_abi_version(void);
+
+/* ---- whole hot path ----------------------------------------------------
+ * Replaces, per image of the batch:
+ *   ColorExtractor.extract_colors native work  (color_extractor.py:217-236)
+ *   ShapeAnalyzer.analyze_shapes               (shape pyc @L125-189)
+ *   ShadowAnalyzer.analyze_shadow_level stats  (shadow pyc @L12-24)
+ * results[n] host; shapes[shape_capacity] host; *shapes_needed = total shapes
+ * (LLFE_ERR_CAPACITY when it exceeds shape_capacity; results are still valid). */
+int llfe_process_batch(llfe_ctx *ctx, const llfe_batch *batch, uint32_t features, uint64_t seed,
+                       llfe_image_result *results, llfe_shape *shapes, int64_t shape_capacity,
+                       int64_t *shapes_needed, llfe_stream stream);
+
+/* ---- stage entry points (parity tests; device in/out unless noted) ------ */
+/* gray = cvtColor(BGR2GRAY); out = GaussianBlur(gray, (5,5), 0)
+ * (shape pyc @L18-21, shadow pyc @L8-9) */
+int llfe_gray_blur5(llfe_ctx *ctx, const uint8_t *bgr, uint8_t *blurred, int32_t n, int32_t h, int32_t w,
+                    llfe_stream stream);
+/* dilate(Canny(blur5(gray), 50, 150), ones(3,3)) as 0/255 u8 (shape pyc @L6-30) */
+int llfe_shape_mask(llfe_ctx *ctx, const uint8_t *bgr, uint8_t *mask, int32_t n, int32_t h, int32_t w,
+                    llfe_stream stream);
+/* Canny NMS classes before hysteresis: 0 weak, 1 suppressed, 2 strong */
+int llfe_edge_classes(llfe_ctx *ctx, const uint8_t *bgr, uint8_t *classes, int32_t n, int32_t h, int32_t w,
+                      llfe_stream stream);
+/* sums[n], counts[n] host: adaptive-threshold shadow statistics (shadow pyc @L15-21) */
+int llfe_shadow_stats(llfe_ctx *ctx, const uint8_t *bgr, uint64_t *sums, uint64_t *counts, int32_t n, int32_t h,
+                      int32_t w, llfe_stream stream);
+/* noise + np.unique(axis=0) (color_extractor.py:220-225,177).  keys: device
+ * n x (h*w) u32 (R<<16|G<<8|B ascending, first n_unique[i] valid); n_unique host. */
+int llfe_color_unique(llfe_ctx *ctx, const llfe_batch *batch, uint64_t seed, uint32_t *keys, int64_t *n_unique,
+                      llfe_stream stream);
+/* cv2.kmeans(float32(keys->RGB), K=min(n_colors,U), None, (EPS+MAX_ITER,200,0.2), 10,
+ * KMEANS_PP_CENTERS) per image (color_extractor.py:189-197).  keys device
+ * (n x key_stride), n_points host; results host (colour fields only). */
+int llfe_kmeans(llfe_ctx *ctx, const uint32_t *keys, int64_t key_stride, const int64_t *n_points, int32_t n,
+                int32_t n_colors, uint64_t seed, int64_t index_base, llfe_image_result *results,
+                llfe_stream stream);
+/* Pillow Image.resize(size, LANCZOS, box) on u8 HWC (image_processor.py:221-224).
+ * box may be NULL (whole image). src/dst device. */
+int llfe_resize_lanczos_pil(llfe_ctx *ctx, const uint8_t *src, int32_t h, int32_t w, int32_t ch, uint8_t *dst,
+                            int32_t out_h, int32_t out_w, const double *box, llfe_stream stream);
+/* host-side external contours (findContours RETR_EXTERNAL/CHAIN_APPROX_SIMPLE,
+ * shape pyc @L140) on a host u8 mask; points x,y pairs; offsets[n_contours+1].
+ * Returns the number of contours, or LLFE_ERR_CAPACITY with *needed_points set. */
+int llfe_find_contours(const uint8_t *mask, int32_t h, int32_t w, int32_t *points, int64_t points_capacity,
+                       int32_t *offsets, int32_t offsets_capacity, int64_t *needed_points);
+/* ShapeAnalyzer.detect_border_radius(contour, epsilon_factor) (shape pyc @L32-61)
+ * on one contour (x,y int32 pairs). */
+double llfe_border_radius(const int32_t *points, int32_t n, double epsilon_factor);
+/* one iteration of the analyze_shapes loop (shape pyc @L146-181): returns 1 and fills
+ * *out when contourArea >= 100, 0 when the contour is dropped. */
+int llfe_classify_contour(const int32_t *points, int32_t n, llfe_shape *out);
+/* host-side shape records from a host u8 mask (the analyze_shapes loop). */
+int llfe_shapes_from_mask(const uint8_t *mask, int32_t h, int32_t w, llfe_shape *shapes, int32_t capacity,
+                          int32_t *n_contours);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LLFE_H */

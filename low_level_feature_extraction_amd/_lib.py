@@ -1,0 +1,130 @@
+"""ctypes binding of libllfe.so (the C ABI declared in include/llfe.h).
+
+This is the same binding a non-Python caller would write; nothing
+here depends on torch.  Importing it never falls back to a CPU implementation: if the
+shared library is missing or cannot be loaded, ``lib()`` raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "libllfe.so")
+
+LLFE_OK = 0
+LLFE_ERR_INVALID = -1
+LLFE_ERR_HIP = -2
+LLFE_ERR_CAPACITY = -3
+LLFE_ERR_OOM = -4
+LLFE_ERR_UNSUPPORTED = -5
+
+FEATURE_COLORS = 1
+FEATURE_SHAPES = 2
+FEATURE_SHADOWS = 4
+
+SHAPE_TYPES = {0: "unknown", 1: "triangle", 2: "rectangle", 3: "circle", 4: "polygon"}
+
+
+class LlfeBatch(C.Structure):
+    _fields_ = [
+        ("data", C.c_void_p),
+        ("n", C.c_int32),
+        ("height", C.c_int32),
+        ("width", C.c_int32),
+        ("on_device", C.c_int32),
+        ("noise", C.c_void_p),
+        ("noise_on_device", C.c_int32),
+        ("reserved", C.c_int32),
+        ("index_base", C.c_int64),
+    ]
+
+
+class LlfeImageResult(C.Structure):
+    _fields_ = [
+        ("n_colors", C.c_int32),
+        ("counts", C.c_int32 * 5),
+        ("centers_rgb", (C.c_uint8 * 3) * 5),
+        ("pad_", C.c_uint8),
+        ("n_unique", C.c_int64),
+        ("compactness", C.c_double),
+        ("shadow_sum", C.c_uint64),
+        ("shadow_count", C.c_uint64),
+        ("shape_offset", C.c_int64),
+        ("n_shapes", C.c_int32),
+        ("n_contours", C.c_int32),
+    ]
+
+
+class LlfeShape(C.Structure):
+    _fields_ = [
+        ("type", C.c_int32),
+        ("x", C.c_int32),
+        ("y", C.c_int32),
+        ("width", C.c_int32),
+        ("height", C.c_int32),
+        ("pad_", C.c_int32),
+        ("border_radius", C.c_double),
+        ("area", C.c_double),
+    ]
+
+
+# every symbol declared in include/llfe.h, with its ctypes signature
+_vp, _i32, _i64, _u32, _u64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint32, C.c_uint64
+SIGNATURES = {
+    "llfe_init": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
+    "llfe_destroy": (C.c_int, [_vp]),
+    "llfe_last_error": (C.c_char_p, [_vp]),
+    "llfe_abi_version": (C.c_int, []),
+    "llfe_process_batch": (C.c_int, [_vp, C.POINTER(LlfeBatch), _u32, _u64, _vp, _vp, _i64, C.POINTER(C.c_int64), _vp]),
+    "llfe_gray_blur5": (C.c_int, [_vp, _vp, _vp, _i32, _i32, _i32, _vp]),
+    "llfe_shape_mask": (C.c_int, [_vp, _vp, _vp, _i32, _i32, _i32, _vp]),
+    "llfe_edge_classes": (C.c_int, [_vp, _vp, _vp, _i32, _i32, _i32, _vp]),
+    "llfe_shadow_stats": (C.c_int, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _vp]),
+    "llfe_color_unique": (C.c_int, [_vp, C.POINTER(LlfeBatch), _u64, _vp, _vp, _vp]),
+    "llfe_kmeans": (C.c_int, [_vp, _vp, _i64, _vp, _i32, _i32, _u64, _i64, _vp, _vp]),
+    "llfe_resize_lanczos_pil": (C.c_int, [_vp, _vp, _i32, _i32, _i32, _vp, _i32, _i32, _vp, _vp]),
+    "llfe_find_contours": (C.c_int, [_vp, _i32, _i32, _vp, _i64, _vp, _i32, C.POINTER(C.c_int64)]),
+    "llfe_border_radius": (C.c_double, [_vp, _i32, C.c_double]),
+    "llfe_classify_contour": (C.c_int, [_vp, _i32, C.POINTER(LlfeShape)]),
+    "llfe_shapes_from_mask": (C.c_int, [_vp, _i32, _i32, _vp, _i32, C.POINTER(C.c_int32)]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class LlfeError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"llfe error {code}: {msg}")
+        self.code = code
+
+
+def lib():
+    """Load libllfe.so (building it from source if it is absent or stale)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            from . import _build
+
+            if _build._stale():
+                try:
+                    _build.build()
+                except Exception as e:  # pragma: no cover - surfaced to caller
+                    if not os.path.exists(LIB_PATH):
+                        raise RuntimeError(f"libllfe.so is missing and could not be built: {e}") from e
+            L = C.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                f = getattr(L, name)
+                f.restype = res
+                f.argtypes = args
+            _lib = L
+    return _lib
+
+
+def check(ctx, rc):
+    if rc < 0:
+        msg = lib().llfe_last_error(ctx)
+        raise LlfeError(rc, msg.decode() if msg else "")
+    return rc

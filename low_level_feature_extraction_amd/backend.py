@@ -1,0 +1,339 @@
+"""Device-side entry points over the C ABI (one context per GPU per host thread).
+
+``Backend`` owns an ``llfe_ctx`` for one device and exposes the batch pipeline and the
+stage functions with numpy / torch arguments.  Device memory for host inputs is
+handled by the library itself (``on_device = 0``); torch tensors already on the GPU are
+passed by pointer together with torch's current HIP stream, so no copy is made.
+
+Nothing in this module computes features on the CPU: a missing ``libllfe.so`` or a
+missing GPU raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib as L
+
+FEATURE_BITS = {"colors": L.FEATURE_COLORS, "shapes": L.FEATURE_SHAPES, "shadows": L.FEATURE_SHADOWS}
+
+
+def feature_mask(features) -> int:
+    m = 0
+    for f in features:
+        f = getattr(f, "value", f)
+        if f not in FEATURE_BITS:
+            raise ValueError(f"unknown feature {f!r}")
+        m |= FEATURE_BITS[f]
+    return m
+
+
+@dataclass
+class ImageFeatures:
+    """Per-image output of the batched hot path (pre-assembly)."""
+
+    centers_rgb: np.ndarray  # (K, 3) uint8, k-means order
+    counts: np.ndarray       # (K,) unique colours per centre
+    n_unique: int
+    compactness: float
+    shadow_sum: int
+    shadow_count: int
+    shapes: list = field(default_factory=list)
+    n_contours: int = 0
+    width: int = 0
+    height: int = 0
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+def _is_torch(x) -> bool:
+    try:
+        import torch
+    except ImportError:  # pragma: no cover
+        return False
+    return isinstance(x, torch.Tensor)
+
+
+class Backend:
+    _instances: dict = {}
+    _ilock = threading.Lock()
+
+    def __init__(self, device: int | None = None):
+        if device is None:
+            device = int(os.environ.get("LLFE_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+        self.device = device
+        self._lib = L.lib()
+        ctx = C.c_void_p()
+        rc = self._lib.llfe_init(device, C.byref(ctx))
+        if rc != L.LLFE_OK:
+            raise L.LlfeError(rc, f"llfe_init(device={device}) failed (no HIP device available?)")
+        self.ctx = ctx
+        self._lock = threading.Lock()
+
+    @classmethod
+    def get(cls, device: int | None = None) -> "Backend":
+        if device is None:
+            device = int(os.environ.get("LLFE_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+        key = (device, threading.get_ident())
+        with cls._ilock:
+            b = cls._instances.get(key)
+            if b is None:
+                b = cls._instances[key] = Backend(device)
+            return b
+
+    def close(self):
+        if self.ctx:
+            self._lib.llfe_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ helpers
+    def _chk(self, rc):
+        return L.check(self.ctx, rc)
+
+    def _stream(self, t=None):
+        if t is not None and _is_torch(t) and t.is_cuda:
+            torch = _torch()
+            return C.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+        return C.c_void_p(0)
+
+    @staticmethod
+    def _batch_view(images):
+        """-> (pointer, n, h, w, on_device, keepalive)"""
+        if _is_torch(images):
+            t = images
+            if t.dtype != _torch().uint8 or t.dim() != 4 or t.shape[-1] != 3:
+                raise ValueError(f"expected N x H x W x 3 uint8 tensor, got {tuple(t.shape)} {t.dtype}")
+            t = t.contiguous()
+            return t.data_ptr(), t.shape[0], t.shape[1], t.shape[2], int(t.is_cuda), t
+        a = np.ascontiguousarray(images, dtype=np.uint8)
+        if a.ndim == 3:
+            a = a[None]
+        if a.ndim != 4 or a.shape[-1] != 3:
+            raise ValueError(f"expected N x H x W x 3 uint8 array, got {a.shape}")
+        return a.ctypes.data, a.shape[0], a.shape[1], a.shape[2], 0, a
+
+    @staticmethod
+    def _noise_view(noise, n, h, w):
+        if noise is None:
+            return None, 0, None
+        if _is_torch(noise):
+            t = noise.contiguous()
+            if t.numel() != n * h * w * 3:
+                raise ValueError("noise must hold N*H*W*3 int8 values")
+            return t.data_ptr(), int(t.is_cuda), t
+        a = np.ascontiguousarray(noise, dtype=np.int8)
+        if a.size != n * h * w * 3:
+            raise ValueError("noise must hold N*H*W*3 int8 values")
+        return a.ctypes.data, 0, a
+
+    # ------------------------------------------------------------------ hot path
+    def process(self, images, features=("colors", "shapes", "shadows"), seed: int = 0, noise=None,
+                index_base: int = 0) -> list:
+        """Run the batched hot path. ``images``: N x H x W x 3 BGR uint8 (numpy host
+        array or torch tensor, host or GPU).  Returns a list of ImageFeatures."""
+        ptr, n, h, w, on_dev, keep = self._batch_view(images)
+        nptr, n_on_dev, nkeep = self._noise_view(noise, n, h, w)
+        mask = feature_mask(features)
+        b = L.LlfeBatch(C.c_void_p(ptr), n, h, w, on_dev, C.c_void_p(nptr) if nptr else None, n_on_dev, 0,
+                        index_base)
+        results = (L.LlfeImageResult * max(n, 1))()
+        cap = max(64 * n, 64)
+        needed = C.c_int64(0)
+        stream = self._stream(keep)
+        with self._lock:
+            while True:
+                shapes = (L.LlfeShape * cap)()
+                rc = self._lib.llfe_process_batch(self.ctx, C.byref(b), mask, C.c_uint64(seed & (2**64 - 1)), results,
+                                                  shapes, cap, C.byref(needed), stream)
+                if rc == L.LLFE_ERR_CAPACITY and needed.value > cap:
+                    cap = int(needed.value)
+                    continue
+                self._chk(rc)
+                break
+        out = []
+        for i in range(n):
+            r = results[i]
+            k = r.n_colors
+            centers = np.array([[r.centers_rgb[j][c] for c in range(3)] for j in range(k)], np.uint8).reshape(-1, 3)
+            counts = np.array([r.counts[j] for j in range(k)], np.int64)
+            shp = []
+            if mask & L.FEATURE_SHAPES:
+                for j in range(r.shape_offset, r.shape_offset + r.n_shapes):
+                    s = shapes[j]
+                    shp.append({
+                        "type": L.SHAPE_TYPES[s.type],
+                        "x": int(s.x),
+                        "y": int(s.y),
+                        "width": int(s.width),
+                        "height": int(s.height),
+                        "border_radius": float(s.border_radius),
+                        "area": float(s.area),
+                    })
+            out.append(ImageFeatures(centers, counts, int(r.n_unique), float(r.compactness), int(r.shadow_sum),
+                                     int(r.shadow_count), shp, int(r.n_contours), w, h))
+        del keep, nkeep
+        return out
+
+    # ------------------------------------------------------------------ stages (device tensors)
+    def _dev_batch(self, images):
+        torch = _torch()
+        if not _is_torch(images):
+            images = torch.from_numpy(np.ascontiguousarray(images, np.uint8))
+        if images.dim() == 3:
+            images = images[None]
+        return images.to(f"cuda:{self.device}").contiguous()
+
+    def gray_blur5(self, images):
+        torch = _torch()
+        x = self._dev_batch(images)
+        n, h, w, _ = x.shape
+        out = torch.empty((n, h, w), dtype=torch.uint8, device=x.device)
+        self._chk(self._lib.llfe_gray_blur5(self.ctx, x.data_ptr(), out.data_ptr(), n, h, w, self._stream(x)))
+        return out
+
+    def edge_classes(self, images):
+        torch = _torch()
+        x = self._dev_batch(images)
+        n, h, w, _ = x.shape
+        out = torch.empty((n, h, w), dtype=torch.uint8, device=x.device)
+        self._chk(self._lib.llfe_edge_classes(self.ctx, x.data_ptr(), out.data_ptr(), n, h, w, self._stream(x)))
+        return out
+
+    def shape_mask(self, images):
+        torch = _torch()
+        x = self._dev_batch(images)
+        n, h, w, _ = x.shape
+        out = torch.empty((n, h, w), dtype=torch.uint8, device=x.device)
+        self._chk(self._lib.llfe_shape_mask(self.ctx, x.data_ptr(), out.data_ptr(), n, h, w, self._stream(x)))
+        return out
+
+    def shadow_stats(self, images):
+        x = self._dev_batch(images)
+        n, h, w, _ = x.shape
+        sums = np.zeros(n, np.uint64)
+        cnts = np.zeros(n, np.uint64)
+        self._chk(self._lib.llfe_shadow_stats(self.ctx, x.data_ptr(), sums.ctypes.data, cnts.ctypes.data, n, h, w,
+                                              self._stream(x)))
+        return sums, cnts
+
+    def color_unique(self, images, seed=0, noise=None, index_base=0):
+        """-> (keys device tensor n x h*w int32 view of u32, n_unique np.int64[n])"""
+        torch = _torch()
+        x = self._dev_batch(images)
+        n, h, w, _ = x.shape
+        nz = None
+        if noise is not None:
+            nz = torch.as_tensor(np.ascontiguousarray(noise, np.int8)).to(x.device).contiguous()
+        keys = torch.empty((n, h * w), dtype=torch.int32, device=x.device)
+        nu = np.zeros(n, np.int64)
+        b = L.LlfeBatch(C.c_void_p(x.data_ptr()), n, h, w, 1, C.c_void_p(nz.data_ptr()) if nz is not None else None,
+                        1, 0, index_base)
+        self._chk(self._lib.llfe_color_unique(self.ctx, C.byref(b), C.c_uint64(seed), keys.data_ptr(),
+                                              nu.ctypes.data, self._stream(x)))
+        return keys, nu
+
+    def kmeans(self, keys, n_points, n_colors=5, seed=0, index_base=0):
+        """keys: device int32 tensor (n, stride) of packed RGB keys; n_points np.int64[n]."""
+        n = keys.shape[0]
+        n_points = np.ascontiguousarray(n_points, np.int64)
+        res = (L.LlfeImageResult * max(n, 1))()
+        self._chk(self._lib.llfe_kmeans(self.ctx, keys.data_ptr(), keys.shape[1], n_points.ctypes.data, n, n_colors,
+                                        C.c_uint64(seed), index_base, res, self._stream(keys)))
+        out = []
+        for i in range(n):
+            r = res[i]
+            k = r.n_colors
+            centers = np.array([[r.centers_rgb[j][c] for c in range(3)] for j in range(k)], np.uint8).reshape(-1, 3)
+            out.append((centers, np.array([r.counts[j] for j in range(k)], np.int64), float(r.compactness)))
+        return out
+
+    def resize_lanczos_pil(self, image, out_w, out_h, box=None):
+        """Pillow LANCZOS resize of one H x W x C uint8 image (torch GPU tensor or numpy)."""
+        torch = _torch()
+        x = image if _is_torch(image) else torch.from_numpy(np.ascontiguousarray(image, np.uint8))
+        x = x.to(f"cuda:{self.device}").contiguous()
+        if x.dim() == 2:
+            x = x[:, :, None]
+        h, w, ch = x.shape
+        out = torch.empty((out_h, out_w, ch), dtype=torch.uint8, device=x.device)
+        bx = None
+        if box is not None:
+            bx = (C.c_double * 4)(*[float(v) for v in box])
+        self._chk(self._lib.llfe_resize_lanczos_pil(self.ctx, x.data_ptr(), h, w, ch, out.data_ptr(), out_h, out_w,
+                                                    bx, self._stream(x)))
+        return out
+
+
+# ---------------------------------------------------------------------- host-only geometry
+def find_contours(mask: np.ndarray) -> list:
+    """findContours(mask, RETR_EXTERNAL, CHAIN_APPROX_SIMPLE) -> list of (n,2) int32."""
+    lib = L.lib()
+    m = np.ascontiguousarray(mask, np.uint8)
+    h, w = m.shape
+    cap = 1 << 16
+    while True:
+        pts = np.empty((cap, 2), np.int32)
+        offs = np.empty(cap + 1, np.int32)
+        need = C.c_int64(0)
+        nc = lib.llfe_find_contours(m.ctypes.data, h, w, pts.ctypes.data, cap, offs.ctypes.data, cap + 1,
+                                    C.byref(need))
+        if nc == L.LLFE_ERR_CAPACITY:
+            cap = max(int(need.value), cap * 2)
+            continue
+        if nc < 0:
+            raise L.LlfeError(nc, "llfe_find_contours failed")
+        return [pts[offs[i]:offs[i + 1]].copy() for i in range(nc)]
+
+
+def _contour_xy(contour) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(contour).reshape(-1, 2), np.int32)
+
+
+def border_radius(contour, epsilon_factor=0.02) -> float:
+    p = _contour_xy(contour)
+    return float(L.lib().llfe_border_radius(p.ctypes.data, len(p), epsilon_factor))
+
+
+def classify_contour(contour):
+    p = _contour_xy(contour)
+    s = L.LlfeShape()
+    rc = L.lib().llfe_classify_contour(p.ctypes.data, len(p), C.byref(s))
+    if rc < 0:
+        raise L.LlfeError(rc, "llfe_classify_contour failed")
+    if rc == 0:
+        return None
+    return {"type": L.SHAPE_TYPES[s.type], "x": int(s.x), "y": int(s.y), "width": int(s.width),
+            "height": int(s.height), "border_radius": float(s.border_radius), "area": float(s.area)}
+
+
+def shapes_from_mask(mask: np.ndarray) -> list:
+    lib = L.lib()
+    m = np.ascontiguousarray(mask, np.uint8)
+    h, w = m.shape
+    cap = 1024
+    while True:
+        arr = (L.LlfeShape * cap)()
+        nc = C.c_int32(0)
+        n = lib.llfe_shapes_from_mask(m.ctypes.data, h, w, arr, cap, C.byref(nc))
+        if n == L.LLFE_ERR_CAPACITY:
+            cap *= 4
+            continue
+        if n < 0:
+            raise L.LlfeError(n, "llfe_shapes_from_mask failed")
+        return [{"type": L.SHAPE_TYPES[s.type], "x": int(s.x), "y": int(s.y), "width": int(s.width),
+                 "height": int(s.height), "border_radius": float(s.border_radius), "area": float(s.area)}
+                for s in arr[:n]]

@@ -1,0 +1,672 @@
+// C ABI of libllfe.so (include/llfe.h): context, workspace and the batch pipeline
+// that replaces the native work behind ColorExtractor.extract_colors,
+// ShapeAnalyzer.analyze_shapes and ShadowAnalyzer.analyze_shadow_level.
+//
+// Per chunk of images (all on the caller's stream):
+//   stencil (gray/blur5/Canny-NMS/adaptive mean)  -> class map + shadow sums
+//   hysteresis relaunches until no tile border changes
+//   dilate + bit-pack -> D2H (1 bit / pixel)
+//   colour bitmap -> compaction -> k-means (10 attempts / image) -> D2H 64 B / image
+//   host thread pool: external contours + shape geometry from the packed masks
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <condition_variable>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/llfe.h"
+#include "contours.h"
+#include "llfe_internal.h"
+
+using namespace llfe;
+
+namespace {
+
+// ------------------------------------------------------------------ thread pool
+class Pool {
+  public:
+    explicit Pool(int n) {
+        for (int i = 0; i < n; i++) th_.emplace_back([this] { run(); });
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+    }
+    int size() const { return (int)th_.size(); }
+    // run f(i) for i in [0, n) on the pool (+ calling thread), wait for all
+    void parallel_for(int n, const std::function<void(int, int)> &f) {
+        if (n <= 0) return;
+        std::atomic<int> next{0};
+        std::atomic<int> done{0};
+        int workers = std::min((int)th_.size(), n);
+        auto job = [&](int wid) {
+            for (int i; (i = next.fetch_add(1)) < n;) f(i, wid);
+        };
+        {
+            std::lock_guard<std::mutex> g(m_);
+            for (int w = 0; w < workers; w++)
+                q_.push_back([&, w] {
+                    job(w + 1);
+                    done.fetch_add(1);
+                    cv_done_.notify_all();
+                });
+        }
+        cv_.notify_all();
+        job(0);
+        std::unique_lock<std::mutex> lk(m_);
+        cv_done_.wait(lk, [&] { return done.load() == workers; });
+    }
+
+  private:
+    void run() {
+        for (;;) {
+            std::function<void()> f;
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [this] { return stop_ || !q_.empty(); });
+                if (stop_ && q_.empty()) return;
+                f = std::move(q_.back());
+                q_.pop_back();
+            }
+            f();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::vector<std::function<void()>> q_;
+    std::mutex m_;
+    std::condition_variable cv_, cv_done_;
+    bool stop_ = false;
+};
+
+template <typename T>
+struct DevBuf {
+    T *p = nullptr;
+    size_t n = 0;
+    hipError_t ensure(size_t count, bool zero = false) {
+        if (count <= n) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        hipError_t e = hipMalloc((void **)&p, count * sizeof(T));
+        if (e != hipSuccess) return e;
+        n = count;
+        if (zero) e = hipMemset(p, 0, count * sizeof(T));
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+template <typename T>
+struct HostBuf {
+    T *p = nullptr;
+    size_t n = 0;
+    hipError_t ensure(size_t count) {
+        if (count <= n) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+        hipError_t e = hipHostMalloc((void **)&p, count * sizeof(T), hipHostMallocDefault);
+        if (e == hipSuccess) n = count;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    uint64_t z = x;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// CV_32F Gaussian kernel of getGaussianKernel(n, sigma<=0): bit-exact softdouble
+// construction (sigma = 0.15 n + 0.35, normalised, centre = 1/sum) cast to float.
+void gauss_kernel_f32(int n, float *out) {
+    double sigma = (double)n * 0.15 + 0.35;
+    double scale2 = -0.125 / (sigma * sigma);
+    int n2 = (n - 1) / 2;
+    double vals[32], sum = 0.0;
+    for (int i = 0, x = 1 - n; i < n2; i++, x += 2) {
+        vals[i] = std::exp((double)(x * x) * scale2);
+        sum += vals[i];
+    }
+    sum = sum * 2.0 + 1.0;
+    double mul = 1.0 / sum;
+    for (int i = 0; i < n2; i++) out[i] = out[n - 1 - i] = (float)(vals[i] * mul);
+    out[n2] = (float)(1.0 * mul);
+}
+
+// Pillow precompute_coeffs (LANCZOS, support 3) -> 22-bit fixed point
+int pil_coeffs(int in_size, double in0, double in1, int out_size, std::vector<int32_t> &bounds,
+               std::vector<int32_t> &kk) {
+    double scale = (in1 - in0) / out_size;
+    double filterscale = scale < 1.0 ? 1.0 : scale;
+    double support = 3.0 * filterscale;
+    int ksize = (int)std::ceil(support) * 2 + 1;
+    bounds.assign((size_t)out_size * 2, 0);
+    kk.assign((size_t)out_size * ksize, 0);
+    std::vector<double> k(ksize);
+    auto sinc = [](double x) {
+        if (x == 0.0) return 1.0;
+        x = x * M_PI;
+        return std::sin(x) / x;
+    };
+    auto lanczos = [&](double x) { return (-3.0 <= x && x < 3.0) ? sinc(x) * sinc(x / 3) : 0.0; };
+    for (int xx = 0; xx < out_size; xx++) {
+        double center = in0 + (xx + 0.5) * scale;
+        double ww = 0.0, ss = 1.0 / filterscale;
+        int xmin = (int)(center - support + 0.5);
+        if (xmin < 0) xmin = 0;
+        int xmax = (int)(center + support + 0.5);
+        if (xmax > in_size) xmax = in_size;
+        xmax -= xmin;
+        int x = 0;
+        for (; x < xmax; x++) {
+            double wv = lanczos((x + xmin - center + 0.5) * ss);
+            k[x] = wv;
+            ww += wv;
+        }
+        for (x = 0; x < xmax; x++)
+            if (ww != 0.0) k[x] /= ww;
+        for (; x < ksize; x++) k[x] = 0;
+        for (x = 0; x < ksize; x++) {
+            double v = k[x] * (1 << 22);
+            kk[(size_t)xx * ksize + x] = v < 0 ? (int32_t)(-0.5 + v) : (int32_t)(0.5 + v);
+        }
+        bounds[2 * xx] = xmin;
+        bounds[2 * xx + 1] = xmax;
+    }
+    return ksize;
+}
+
+int default_threads() {
+    const char *e = getenv("LLFE_HOST_THREADS");
+    if (e && atoi(e) > 0) return atoi(e);
+    unsigned hc = std::thread::hardware_concurrency();
+    return (int)std::max(1u, std::min(hc ? hc : 4u, 16u));
+}
+
+}  // namespace
+
+struct llfe_ctx {
+    int device = 0;
+    std::string err;
+    Pool *pool = nullptr;
+    StencilParams sp{};
+    // device workspace
+    DevBuf<uint8_t> d_in, d_cls, d_dirty, d_rsz_tmp;
+    DevBuf<int8_t> d_noise;
+    DevBuf<uint64_t> d_bits, d_rng;
+    DevBuf<unsigned long long> d_shadow;
+    DevBuf<int> d_changed, d_order;
+    DevBuf<uint32_t> d_bitmap, d_occ, d_keys, d_kscratch;
+    DevBuf<int64_t> d_nuniq;
+    DevBuf<KmeansAttemptOut> d_att;
+    DevBuf<KmeansImageOut> d_kout;
+    DevBuf<int32_t> d_coef;
+    // pinned host staging
+    HostBuf<uint64_t> h_bits;
+    HostBuf<unsigned long long> h_shadow;
+    HostBuf<KmeansImageOut> h_kout;
+    HostBuf<int> h_changed;
+    HostBuf<uint64_t> h_rng;
+    HostBuf<int64_t> h_nuniq;
+    // per-thread host scratch
+    std::vector<std::vector<int8_t>> work;
+    std::vector<Contours> cont;
+    std::vector<ShapeScratch> shs;
+    std::vector<std::vector<llfe_shape>> img_shapes;
+    std::vector<int32_t> img_ncont;
+
+    int fail(int code, const char *fmt, ...) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        err = buf;
+        return code;
+    }
+};
+
+#define HIPCHK(ctx, expr)                                                                                   \
+    do {                                                                                                    \
+        hipError_t e_ = (expr);                                                                             \
+        if (e_ != hipSuccess) return (ctx)->fail(LLFE_ERR_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                                                 __FILE__, __LINE__);                                       \
+    } while (0)
+
+namespace {
+
+constexpr int kChunk = 256;  // images per device pass (bounds workspace: ~15 MB / 1080p image)
+
+int stage_input(llfe_ctx *ctx, const llfe_batch *b, int i0, int n, const uint8_t **d_img, const int8_t **d_noise,
+                hipStream_t s) {
+    size_t P3 = (size_t)b->height * b->width * 3;
+    if (b->on_device) {
+        *d_img = b->data + (size_t)i0 * P3;
+    } else {
+        HIPCHK(ctx, ctx->d_in.ensure(P3 * n));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->d_in.p, b->data + (size_t)i0 * P3, P3 * n, hipMemcpyHostToDevice, s));
+        *d_img = ctx->d_in.p;
+    }
+    *d_noise = nullptr;
+    if (b->noise) {
+        if (b->noise_on_device) {
+            *d_noise = b->noise + (size_t)i0 * P3;
+        } else {
+            HIPCHK(ctx, ctx->d_noise.ensure(P3 * n));
+            HIPCHK(ctx, hipMemcpyAsync(ctx->d_noise.p, b->noise + (size_t)i0 * P3, P3 * n, hipMemcpyHostToDevice, s));
+            *d_noise = ctx->d_noise.p;
+        }
+    }
+    return LLFE_OK;
+}
+
+int run_hysteresis(llfe_ctx *ctx, int n, int h, int w, hipStream_t s, int *launches) {
+    const size_t tiles = (size_t)tiles_x(w) * tiles_y(h) * n;
+    HIPCHK(ctx, ctx->d_dirty.ensure(2 * tiles));
+    HIPCHK(ctx, ctx->d_changed.ensure(1));
+    HIPCHK(ctx, ctx->h_changed.ensure(1));
+    uint8_t *din = nullptr, *dout = ctx->d_dirty.p, *dspare = ctx->d_dirty.p + tiles;
+    int it = 0;
+    for (;; it++) {
+        HIPCHK(ctx, hipMemsetAsync(dout, 0, tiles, s));
+        HIPCHK(ctx, hipMemsetAsync(ctx->d_changed.p, 0, sizeof(int), s));
+        HIPCHK(ctx, launch_hysteresis(ctx->d_cls.p, n, h, w, din, dout, ctx->d_changed.p, s));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->h_changed.p, ctx->d_changed.p, sizeof(int), hipMemcpyDeviceToHost, s));
+        HIPCHK(ctx, hipStreamSynchronize(s));
+        if (*ctx->h_changed.p == 0) break;
+        if (it > 100000) return ctx->fail(LLFE_ERR_INVALID, "hysteresis did not converge");
+        uint8_t *t = din ? din : dspare;
+        din = dout;
+        dout = t;
+    }
+    if (launches) *launches = it + 1;
+    return LLFE_OK;
+}
+
+int color_stage(llfe_ctx *ctx, const uint8_t *img, const int8_t *noise, int n, int h, int w, uint64_t seed,
+                int64_t index_base, hipStream_t s) {
+    const int64_t P = (int64_t)h * w;
+    const int64_t key_stride = (std::max<int64_t>(P, 1) + 3) & ~int64_t(3);
+    HIPCHK(ctx, ctx->d_bitmap.ensure((size_t)n * kBitmapWords, true));
+    HIPCHK(ctx, ctx->d_occ.ensure((size_t)n * kOccWords, true));
+    HIPCHK(ctx, ctx->d_keys.ensure((size_t)n * key_stride));
+    HIPCHK(ctx, ctx->d_nuniq.ensure(n));
+    HIPCHK(ctx, launch_color_bitmap(img, noise, n, h, w, seed, index_base, ctx->d_bitmap.p, ctx->d_occ.p, s));
+    HIPCHK(ctx, launch_color_compact(ctx->d_bitmap.p, ctx->d_occ.p, n, ctx->d_keys.p, key_stride, ctx->d_nuniq.p, s));
+    return LLFE_OK;
+}
+
+int kmeans_stage(llfe_ctx *ctx, const uint32_t *keys, int64_t key_stride, const int64_t *d_nuniq, int n,
+                 int n_colors, uint64_t seed, int64_t index_base, hipStream_t s) {
+    if (n_colors < 1 || n_colors > kMaxK) return ctx->fail(LLFE_ERR_UNSUPPORTED, "n_colors must be in [1, 5]");
+    const int64_t sstride = kmeans_scratch_stride(key_stride);
+    HIPCHK(ctx, ctx->d_rng.ensure(n));
+    HIPCHK(ctx, ctx->h_rng.ensure(n));
+    HIPCHK(ctx, ctx->d_order.ensure(n));
+    HIPCHK(ctx, ctx->d_kscratch.ensure((size_t)n * kAttempts * sstride));
+    HIPCHK(ctx, ctx->d_att.ensure((size_t)n * kAttempts));
+    HIPCHK(ctx, ctx->d_kout.ensure(n));
+    for (int i = 0; i < n; i++) {
+        uint64_t st = splitmix64(seed + (uint64_t)(index_base + i));
+        ctx->h_rng.p[i] = st ? st : 0xFFFFFFFFull;
+    }
+    HIPCHK(ctx, hipMemcpyAsync(ctx->d_rng.p, ctx->h_rng.p, sizeof(uint64_t) * n, hipMemcpyHostToDevice, s));
+    HIPCHK(ctx, launch_kmeans(keys, key_stride, d_nuniq, n, n_colors, ctx->d_rng.p, ctx->d_order.p, ctx->d_kscratch.p,
+                              sstride, ctx->d_att.p, ctx->d_kout.p, s));
+    return LLFE_OK;
+}
+
+void fill_color_result(const KmeansImageOut &k, llfe_image_result &r) {
+    r.n_colors = k.k;
+    for (int c = 0; c < 5; c++) {
+        r.counts[c] = k.counts[c];
+        for (int j = 0; j < 3; j++) r.centers_rgb[c][j] = k.centers_rgb[c][j];
+    }
+    r.n_unique = k.n_unique;
+    r.compactness = k.compactness;
+}
+
+bool valid_dims(int n, int h, int w) { return n >= 0 && h > 0 && w > 0 && (int64_t)h * w < (1LL << 31); }
+
+}  // namespace
+
+extern "C" {
+
+int llfe_abi_version(void) { return LLFE_ABI_VERSION; }
+
+int llfe_init(int device, llfe_ctx **out) {
+    if (!out) return LLFE_ERR_INVALID;
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return LLFE_ERR_HIP;
+    if (device < 0 || device >= count) return LLFE_ERR_INVALID;
+    if (hipSetDevice(device) != hipSuccess) return LLFE_ERR_HIP;
+    llfe_ctx *c = new llfe_ctx();
+    c->device = device;
+    gauss_kernel_f32(11, c->sp.k11);
+    c->pool = new Pool(default_threads() - 1);
+    int nt = c->pool->size() + 1;
+    c->work.resize(nt);
+    c->cont.resize(nt);
+    c->shs.resize(nt);
+    *out = c;
+    return LLFE_OK;
+}
+
+int llfe_destroy(llfe_ctx *ctx) {
+    if (!ctx) return LLFE_OK;
+    (void)hipSetDevice(ctx->device);
+    ctx->d_in.release(); ctx->d_cls.release(); ctx->d_dirty.release(); ctx->d_rsz_tmp.release();
+    ctx->d_noise.release(); ctx->d_bits.release(); ctx->d_rng.release(); ctx->d_shadow.release();
+    ctx->d_changed.release(); ctx->d_order.release(); ctx->d_bitmap.release(); ctx->d_occ.release();
+    ctx->d_keys.release(); ctx->d_kscratch.release(); ctx->d_nuniq.release(); ctx->d_att.release();
+    ctx->d_kout.release(); ctx->d_coef.release();
+    ctx->h_bits.release(); ctx->h_shadow.release(); ctx->h_kout.release(); ctx->h_changed.release();
+    ctx->h_rng.release(); ctx->h_nuniq.release();
+    delete ctx->pool;
+    delete ctx;
+    return LLFE_OK;
+}
+
+const char *llfe_last_error(llfe_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int llfe_process_batch(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_t seed,
+                       llfe_image_result *results, llfe_shape *shapes, int64_t shape_capacity,
+                       int64_t *shapes_needed, llfe_stream stream) {
+    if (!ctx || !b || !results) return LLFE_ERR_INVALID;
+    if (!valid_dims(b->n, b->height, b->width) || (b->n > 0 && !b->data))
+        return ctx->fail(LLFE_ERR_INVALID, "invalid batch n=%d h=%d w=%d", b->n, b->height, b->width);
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = (hipStream_t)stream;
+    const int h = b->height, w = b->width, wpr = words_per_row(w);
+    const bool want_col = features & LLFE_FEATURE_COLORS, want_shp = features & LLFE_FEATURE_SHAPES,
+               want_shd = features & LLFE_FEATURE_SHADOWS;
+    const int64_t P = (int64_t)h * w;
+    const int64_t key_stride = (std::max<int64_t>(P, 1) + 3) & ~int64_t(3);
+    int64_t total_shapes = 0;
+    for (int i0 = 0; i0 < b->n; i0 += kChunk) {
+        const int n = std::min(kChunk, b->n - i0);
+        const uint8_t *img;
+        const int8_t *noise;
+        int rc = stage_input(ctx, b, i0, n, &img, &noise, s);
+        if (rc) return rc;
+        if (want_shp || want_shd) {
+            HIPCHK(ctx, ctx->d_shadow.ensure(2 * (size_t)n));
+            HIPCHK(ctx, ctx->h_shadow.ensure(2 * (size_t)n));
+            if (want_shp) HIPCHK(ctx, ctx->d_cls.ensure((size_t)n * P));
+            if (want_shd) HIPCHK(ctx, hipMemsetAsync(ctx->d_shadow.p, 0, sizeof(unsigned long long) * 2 * n, s));
+            HIPCHK(ctx, launch_stencil(img, n, h, w, want_shp ? ctx->d_cls.p : nullptr, nullptr,
+                                       want_shd ? ctx->d_shadow.p : nullptr, want_shd ? ctx->d_shadow.p + n : nullptr,
+                                       ctx->sp, s));
+        }
+        if (want_col) {
+            rc = color_stage(ctx, img, noise, n, h, w, seed, b->index_base + i0, s);
+            if (rc) return rc;
+            rc = kmeans_stage(ctx, ctx->d_keys.p, key_stride, ctx->d_nuniq.p, n, 5, seed, b->index_base + i0, s);
+            if (rc) return rc;
+            HIPCHK(ctx, ctx->h_kout.ensure(n));
+            HIPCHK(ctx, hipMemcpyAsync(ctx->h_kout.p, ctx->d_kout.p, sizeof(KmeansImageOut) * n, hipMemcpyDeviceToHost, s));
+        }
+        if (want_shp) {
+            rc = run_hysteresis(ctx, n, h, w, s, nullptr);
+            if (rc) return rc;
+            HIPCHK(ctx, ctx->d_bits.ensure((size_t)n * h * wpr));
+            HIPCHK(ctx, ctx->h_bits.ensure((size_t)n * h * wpr));
+            HIPCHK(ctx, launch_dilate_pack(ctx->d_cls.p, n, h, w, ctx->d_bits.p, nullptr, s));
+            HIPCHK(ctx, hipMemcpyAsync(ctx->h_bits.p, ctx->d_bits.p, sizeof(uint64_t) * n * h * wpr,
+                                       hipMemcpyDeviceToHost, s));
+        }
+        if (want_shd)
+            HIPCHK(ctx, hipMemcpyAsync(ctx->h_shadow.p, ctx->d_shadow.p, sizeof(unsigned long long) * 2 * n,
+                                       hipMemcpyDeviceToHost, s));
+        HIPCHK(ctx, hipStreamSynchronize(s));
+
+        for (int i = 0; i < n; i++) {
+            llfe_image_result &r = results[i0 + i];
+            std::memset(&r, 0, sizeof r);
+            if (want_col) fill_color_result(ctx->h_kout.p[i], r);
+            if (want_shd) {
+                r.shadow_sum = ctx->h_shadow.p[i];
+                r.shadow_count = ctx->h_shadow.p[n + i];
+            }
+        }
+        if (want_shp) {
+            ctx->img_shapes.resize(n);
+            ctx->img_ncont.assign(n, 0);
+            const uint64_t *hb = ctx->h_bits.p;
+            ctx->pool->parallel_for(n, [&](int i, int wid) {
+                external_contours_bits(hb + (size_t)i * h * wpr, h, w, wpr, ctx->work[wid], ctx->cont[wid]);
+                ctx->img_ncont[i] = shapes_from_contours(ctx->cont[wid], ctx->shs[wid], ctx->img_shapes[i]);
+            });
+            for (int i = 0; i < n; i++) {
+                llfe_image_result &r = results[i0 + i];
+                r.shape_offset = total_shapes;
+                r.n_shapes = (int32_t)ctx->img_shapes[i].size();
+                r.n_contours = ctx->img_ncont[i];
+                for (size_t k = 0; k < ctx->img_shapes[i].size(); k++) {
+                    if (shapes && total_shapes + (int64_t)k < shape_capacity)
+                        shapes[total_shapes + k] = ctx->img_shapes[i][k];
+                }
+                total_shapes += r.n_shapes;
+            }
+        }
+    }
+    if (shapes_needed) *shapes_needed = total_shapes;
+    if (want_shp && total_shapes > shape_capacity)
+        return ctx->fail(LLFE_ERR_CAPACITY, "shape capacity %lld < %lld", (long long)shape_capacity,
+                         (long long)total_shapes);
+    return LLFE_OK;
+}
+
+int llfe_gray_blur5(llfe_ctx *ctx, const uint8_t *bgr, uint8_t *blurred, int32_t n, int32_t h, int32_t w,
+                    llfe_stream stream) {
+    if (!ctx || !valid_dims(n, h, w) || !bgr || !blurred) return LLFE_ERR_INVALID;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    HIPCHK(ctx, launch_stencil(bgr, n, h, w, nullptr, blurred, nullptr, nullptr, ctx->sp, (hipStream_t)stream));
+    HIPCHK(ctx, hipStreamSynchronize((hipStream_t)stream));
+    return LLFE_OK;
+}
+
+int llfe_edge_classes(llfe_ctx *ctx, const uint8_t *bgr, uint8_t *classes, int32_t n, int32_t h, int32_t w,
+                      llfe_stream stream) {
+    if (!ctx || !valid_dims(n, h, w) || !bgr || !classes) return LLFE_ERR_INVALID;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    HIPCHK(ctx, launch_stencil(bgr, n, h, w, classes, nullptr, nullptr, nullptr, ctx->sp, (hipStream_t)stream));
+    HIPCHK(ctx, hipStreamSynchronize((hipStream_t)stream));
+    return LLFE_OK;
+}
+
+int llfe_shape_mask(llfe_ctx *ctx, const uint8_t *bgr, uint8_t *mask, int32_t n, int32_t h, int32_t w,
+                    llfe_stream stream) {
+    if (!ctx || !valid_dims(n, h, w) || !bgr || !mask) return LLFE_ERR_INVALID;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(ctx, ctx->d_cls.ensure((size_t)n * h * w));
+    HIPCHK(ctx, launch_stencil(bgr, n, h, w, ctx->d_cls.p, nullptr, nullptr, nullptr, ctx->sp, s));
+    int rc = run_hysteresis(ctx, n, h, w, s, nullptr);
+    if (rc) return rc;
+    HIPCHK(ctx, launch_dilate_pack(ctx->d_cls.p, n, h, w, nullptr, mask, s));
+    HIPCHK(ctx, hipStreamSynchronize(s));
+    return LLFE_OK;
+}
+
+int llfe_shadow_stats(llfe_ctx *ctx, const uint8_t *bgr, uint64_t *sums, uint64_t *counts, int32_t n, int32_t h,
+                      int32_t w, llfe_stream stream) {
+    if (!ctx || !valid_dims(n, h, w) || !bgr || !sums || !counts) return LLFE_ERR_INVALID;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(ctx, ctx->d_shadow.ensure(2 * (size_t)n));
+    HIPCHK(ctx, hipMemsetAsync(ctx->d_shadow.p, 0, sizeof(unsigned long long) * 2 * n, s));
+    HIPCHK(ctx, launch_stencil(bgr, n, h, w, nullptr, nullptr, ctx->d_shadow.p, ctx->d_shadow.p + n, ctx->sp, s));
+    HIPCHK(ctx, hipMemcpyAsync(sums, ctx->d_shadow.p, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, s));
+    HIPCHK(ctx, hipMemcpyAsync(counts, ctx->d_shadow.p + n, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, s));
+    HIPCHK(ctx, hipStreamSynchronize(s));
+    return LLFE_OK;
+}
+
+int llfe_color_unique(llfe_ctx *ctx, const llfe_batch *b, uint64_t seed, uint32_t *keys, int64_t *n_unique,
+                      llfe_stream stream) {
+    if (!ctx || !b || !keys || !n_unique || !valid_dims(b->n, b->height, b->width)) return LLFE_ERR_INVALID;
+    if (b->n > kChunk) return ctx->fail(LLFE_ERR_UNSUPPORTED, "llfe_color_unique: n > %d", kChunk);
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = (hipStream_t)stream;
+    const int h = b->height, w = b->width, n = b->n;
+    const int64_t P = (int64_t)h * w;
+    const uint8_t *img;
+    const int8_t *noise;
+    int rc = stage_input(ctx, b, 0, n, &img, &noise, s);
+    if (rc) return rc;
+    HIPCHK(ctx, ctx->d_bitmap.ensure((size_t)n * kBitmapWords, true));
+    HIPCHK(ctx, ctx->d_occ.ensure((size_t)n * kOccWords, true));
+    HIPCHK(ctx, ctx->d_nuniq.ensure(n));
+    HIPCHK(ctx, ctx->h_nuniq.ensure(n));
+    HIPCHK(ctx, launch_color_bitmap(img, noise, n, h, w, seed, b->index_base, ctx->d_bitmap.p, ctx->d_occ.p, s));
+    HIPCHK(ctx, launch_color_compact(ctx->d_bitmap.p, ctx->d_occ.p, n, keys, P, ctx->d_nuniq.p, s));
+    HIPCHK(ctx, hipMemcpyAsync(n_unique, ctx->d_nuniq.p, sizeof(int64_t) * n, hipMemcpyDeviceToHost, s));
+    HIPCHK(ctx, hipStreamSynchronize(s));
+    return LLFE_OK;
+}
+
+int llfe_kmeans(llfe_ctx *ctx, const uint32_t *keys, int64_t key_stride, const int64_t *n_points, int32_t n,
+                int32_t n_colors, uint64_t seed, int64_t index_base, llfe_image_result *results,
+                llfe_stream stream) {
+    if (!ctx || !keys || !n_points || !results || n < 0) return LLFE_ERR_INVALID;
+    if (key_stride % 4 || ((uintptr_t)keys & 15))
+        return ctx->fail(LLFE_ERR_INVALID, "keys must be 16-byte aligned with key_stride % 4 == 0");
+    if (n > kMaxKmeansBatch) return ctx->fail(LLFE_ERR_UNSUPPORTED, "llfe_kmeans: n > %d", kMaxKmeansBatch);
+    for (int i = 0; i < n; i++)
+        if (n_points[i] < 0 || n_points[i] > key_stride) return ctx->fail(LLFE_ERR_INVALID, "n_points out of range");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(ctx, ctx->d_nuniq.ensure(n));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->d_nuniq.p, n_points, sizeof(int64_t) * n, hipMemcpyHostToDevice, s));
+    int rc = kmeans_stage(ctx, keys, key_stride, ctx->d_nuniq.p, n, n_colors, seed, index_base, s);
+    if (rc) return rc;
+    HIPCHK(ctx, ctx->h_kout.ensure(n));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->h_kout.p, ctx->d_kout.p, sizeof(KmeansImageOut) * n, hipMemcpyDeviceToHost, s));
+    HIPCHK(ctx, hipStreamSynchronize(s));
+    for (int i = 0; i < n; i++) {
+        std::memset(&results[i], 0, sizeof(llfe_image_result));
+        fill_color_result(ctx->h_kout.p[i], results[i]);
+    }
+    return LLFE_OK;
+}
+
+int llfe_resize_lanczos_pil(llfe_ctx *ctx, const uint8_t *src, int32_t h, int32_t w, int32_t ch, uint8_t *dst,
+                            int32_t out_h, int32_t out_w, const double *box, llfe_stream stream) {
+    if (!ctx || !src || !dst || h <= 0 || w <= 0 || ch <= 0 || out_h <= 0 || out_w <= 0) return LLFE_ERR_INVALID;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = (hipStream_t)stream;
+    double bx0 = box ? box[0] : 0, by0 = box ? box[1] : 0, bx1 = box ? box[2] : w, by1 = box ? box[3] : h;
+    bool need_h = out_w != w || bx0 != 0 || bx1 != out_w;
+    bool need_v = out_h != h || by0 != 0 || by1 != out_h;
+    std::vector<int32_t> bh, kh, bv, kv;
+    int ksh = pil_coeffs(w, bx0, bx1, out_w, bh, kh);
+    int ksv = pil_coeffs(h, by0, by1, out_h, bv, kv);
+    int yfirst = bv[0], ylast = bv[2 * out_h - 2] + bv[2 * out_h - 1];
+    // coefficient block: [bh | kh | bv | kv]
+    size_t nb = bh.size() + kh.size() + bv.size() + kv.size();
+    HIPCHK(ctx, ctx->d_coef.ensure(nb));
+    std::vector<int32_t> all;
+    all.reserve(nb);
+    if (need_h)
+        for (int i = 0; i < out_h; i++) bv[2 * i] -= yfirst;
+    all.insert(all.end(), bh.begin(), bh.end());
+    all.insert(all.end(), kh.begin(), kh.end());
+    all.insert(all.end(), bv.begin(), bv.end());
+    all.insert(all.end(), kv.begin(), kv.end());
+    HIPCHK(ctx, hipMemcpyAsync(ctx->d_coef.p, all.data(), nb * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    const int32_t *dbh = ctx->d_coef.p, *dkh = dbh + bh.size(), *dbv = dkh + kh.size(), *dkv = dbv + bv.size();
+    if (!need_h && !need_v) {
+        HIPCHK(ctx, hipMemcpyAsync(dst, src, (size_t)h * w * ch, hipMemcpyDeviceToDevice, s));
+    } else if (need_h && !need_v) {
+        HIPCHK(ctx, launch_resize_h(src, h, w, ch, yfirst, ylast - yfirst, dst, out_w, dbh, dkh, ksh, s));
+    } else if (!need_h) {
+        HIPCHK(ctx, launch_resize_v(src, w, ch, dst, out_h, dbv, dkv, ksv, s));
+    } else {
+        const int rows = ylast - yfirst;
+        HIPCHK(ctx, ctx->d_rsz_tmp.ensure((size_t)rows * out_w * ch));
+        HIPCHK(ctx, launch_resize_h(src, h, w, ch, yfirst, rows, ctx->d_rsz_tmp.p, out_w, dbh, dkh, ksh, s));
+        HIPCHK(ctx, launch_resize_v(ctx->d_rsz_tmp.p, out_w, ch, dst, out_h, dbv, dkv, ksv, s));
+    }
+    HIPCHK(ctx, hipStreamSynchronize(s));  // host coefficient vectors die here
+    return LLFE_OK;
+}
+
+int llfe_find_contours(const uint8_t *mask, int32_t h, int32_t w, int32_t *points, int64_t points_capacity,
+                       int32_t *offsets, int32_t offsets_capacity, int64_t *needed_points) {
+    if (!mask || h <= 0 || w <= 0) return LLFE_ERR_INVALID;
+    std::vector<int8_t> work;
+    Contours c;
+    external_contours_u8(mask, h, w, work, c);
+    const int nc = (int)c.start.size() - 1;
+    const int64_t npts = (int64_t)c.xy.size() / 2;
+    if (needed_points) *needed_points = npts;
+    if (npts > points_capacity || nc + 1 > offsets_capacity) return LLFE_ERR_CAPACITY;
+    // output in cv2 order (newest first)
+    int64_t wpos = 0;
+    offsets[0] = 0;
+    for (int k = 0; k < nc; k++) {
+        int src = nc - 1 - k;
+        int64_t a = c.start[src], b2 = c.start[src + 1];
+        std::memcpy(points + 2 * wpos, c.xy.data() + 2 * a, sizeof(int32_t) * 2 * (b2 - a));
+        wpos += b2 - a;
+        offsets[k + 1] = (int32_t)wpos;
+    }
+    return nc;
+}
+
+double llfe_border_radius(const int32_t *points, int32_t n, double epsilon_factor) {
+    if (!points || n <= 0) return 0.0;
+    ShapeScratch sc;
+    return border_radius(points, n, epsilon_factor, sc);
+}
+
+int llfe_classify_contour(const int32_t *points, int32_t n, llfe_shape *out) {
+    if (!points || n <= 0 || !out) return n == 0 ? 0 : LLFE_ERR_INVALID;
+    ShapeScratch sc;
+    return classify_contour(points, n, sc, *out) ? 1 : 0;
+}
+
+int llfe_shapes_from_mask(const uint8_t *mask, int32_t h, int32_t w, llfe_shape *shapes, int32_t capacity,
+                          int32_t *n_contours) {
+    if (!mask || h <= 0 || w <= 0) return LLFE_ERR_INVALID;
+    std::vector<int8_t> work;
+    Contours c;
+    ShapeScratch sc;
+    std::vector<llfe_shape> out;
+    external_contours_u8(mask, h, w, work, c);
+    int nc = shapes_from_contours(c, sc, out);
+    if (n_contours) *n_contours = nc;
+    if ((int64_t)out.size() > capacity) return LLFE_ERR_CAPACITY;
+    for (size_t i = 0; i < out.size(); i++) shapes[i] = out[i];
+    return (int)out.size();
+}
+
+}  // extern "C"

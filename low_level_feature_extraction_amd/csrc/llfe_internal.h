@@ -1,0 +1,86 @@
+// Internal declarations shared by the HIP kernel files and the C-ABI layer.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace llfe {
+
+// ---------------------------------------------------------------- stencils
+// Output tile of the fused stencil front-end (gray -> blur5 -> {Canny NMS,
+// adaptive Gaussian mean}); 256 threads per tile.
+constexpr int kTileW = 64;
+constexpr int kTileH = 32;
+
+struct StencilParams {
+    float k11[11];  // CV_32F GaussianBlur 11x11 sigma 0 kernel (adaptiveThreshold)
+};
+
+// shape pyc @L18-24 + shadow pyc @L8-21 for a packed NHWC batch.
+//   cls (may be null): n x h x w u8, 0 weak / 1 suppressed / 2 strong
+//   blurred (may be null): n x h x w u8 (parity of GaussianBlur 5x5)
+//   shadow_sum/shadow_cnt (may be null): per image u64 accumulators (zeroed by caller)
+hipError_t launch_stencil(const uint8_t *bgr, int n, int h, int w, uint8_t *cls, uint8_t *blurred,
+                          unsigned long long *shadow_sum, unsigned long long *shadow_cnt, const StencilParams &p,
+                          hipStream_t s);
+
+// Canny hysteresis on the class map (in place): one launch = tile-local flood +
+// cross-tile propagation through changed tile borders.  dirty_in/out: per-tile flags
+// (n * tiles) ; *changed (device) set when any tile border changed.
+hipError_t launch_hysteresis(uint8_t *cls, int n, int h, int w, const uint8_t *dirty_in, uint8_t *dirty_out,
+                             int *changed, hipStream_t s);
+
+// dilate(edges(cls==2), 3x3) -> bit-packed mask: n x h x words_per_row u64, bit
+// (x & 63) of word x>>6 ; and optional u8 0/255 mask.
+hipError_t launch_dilate_pack(const uint8_t *cls, int n, int h, int w, uint64_t *bits, uint8_t *mask_u8,
+                              hipStream_t s);
+
+inline int words_per_row(int w) { return (w + 63) / 64; }
+inline int tiles_x(int w) { return (w + kTileW - 1) / kTileW; }
+inline int tiles_y(int h) { return (h + kTileH - 1) / kTileH; }
+
+// ---------------------------------------------------------------- colours
+constexpr int kBitmapWords = 1 << 19;  // 2^24 bits as u32 words (2 MiB per image)
+constexpr int kOccWords = 1 << 10;     // 1 bit per 512-bit block -> 32768 bits
+constexpr int kMaxK = 5;
+constexpr int kAttempts = 10;
+
+// BGR->RGB, noise (host int8 RGB stream or Philox), presence bitmap + occupancy.
+hipError_t launch_color_bitmap(const uint8_t *bgr, const int8_t *noise, int n, int h, int w, uint64_t seed,
+                               int64_t index_base, uint32_t *bitmap, uint32_t *occ, hipStream_t s);
+// bitmap -> ascending keys (np.unique order), clears bitmap+occ for reuse.
+hipError_t launch_color_compact(uint32_t *bitmap, uint32_t *occ, int n, uint32_t *keys, int64_t key_stride,
+                                int64_t *n_unique, hipStream_t s);
+
+struct KmeansAttemptOut {
+    double compactness;
+    float centers[kMaxK][3];
+    int32_t counts[kMaxK];
+    int32_t iters;
+    int32_t pad;
+};
+
+struct KmeansImageOut {
+    int32_t k;
+    int32_t counts[kMaxK];
+    uint8_t centers_rgb[kMaxK][3];
+    uint8_t pad[1];
+    int64_t n_unique;
+    double compactness;
+};
+
+// per image: K = min(n_colors, U); attempts run as separate workgroups
+// (ordered largest U first), then a finalize kernel picks the best attempt.
+hipError_t launch_kmeans(const uint32_t *keys, int64_t key_stride, const int64_t *n_unique, int n, int n_colors,
+                         const uint64_t *rng_states, int32_t *order, uint32_t *scratch, int64_t scratch_stride,
+                         KmeansAttemptOut *attempts, KmeansImageOut *out, hipStream_t s);
+// u32 scratch per (image, attempt) for k-means++ step sums
+int64_t kmeans_scratch_stride(int64_t key_stride);
+constexpr int kMaxKmeansBatch = 4096;
+
+// ---------------------------------------------------------------- resize
+hipError_t launch_resize_h(const uint8_t *src, int src_h, int src_w, int ch, int row0, int rows, uint8_t *dst,
+                           int out_w, const int32_t *bounds, const int32_t *coeffs, int ksize, hipStream_t s);
+hipError_t launch_resize_v(const uint8_t *src, int src_w, int ch, uint8_t *dst, int out_h, const int32_t *bounds,
+                           const int32_t *coeffs, int ksize, hipStream_t s);
+
+}  // namespace llfe
