@@ -100,11 +100,24 @@ typedef struct {
     double area;
 } llfe_shape;
 
+/* per-kernel timing collected with hipEvents on the launch stream while profiling
+ * is enabled (bench.py's roofline numbers) */
+typedef struct {
+    char name[32];
+    int64_t launches;
+    double total_ms;
+    double bytes;  /* algorithmic HBM bytes attributed to those launches */
+} llfe_kernel_stat;
+
 /* ---- context ---------------------------------------------------------- */
 int llfe_init(int device, llfe_ctx **out);
 int llfe_destroy(llfe_ctx *ctx);
 const char *llfe_last_error(llfe_ctx *ctx);
 int llfe_abi_version(void);
+/* enable (1) / disable (0) event timing; enabling resets the statistics */
+int llfe_set_profiling(llfe_ctx *ctx, int enable);
+/* copies up to cap entries, returns the number of kernels with statistics */
+int llfe_kernel_stats(llfe_ctx *ctx, llfe_kernel_stat *out, int32_t cap);
 
 /* ---- whole hot path ----------------------------------------------------
  * Replaces, per image of the batch:

@@ -70,6 +70,15 @@ class LlfeShape(C.Structure):
     ]
 
 
+class LlfeKernelStat(C.Structure):
+    _fields_ = [
+        ("name", C.c_char * 32),
+        ("launches", C.c_int64),
+        ("total_ms", C.c_double),
+        ("bytes", C.c_double),
+    ]
+
+
 # every symbol declared in include/llfe.h, with its ctypes signature
 _vp, _i32, _i64, _u32, _u64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint32, C.c_uint64
 SIGNATURES = {
@@ -77,6 +86,8 @@ SIGNATURES = {
     "llfe_destroy": (C.c_int, [_vp]),
     "llfe_last_error": (C.c_char_p, [_vp]),
     "llfe_abi_version": (C.c_int, []),
+    "llfe_set_profiling": (C.c_int, [_vp, C.c_int]),
+    "llfe_kernel_stats": (C.c_int, [_vp, C.POINTER(LlfeKernelStat), _i32]),
     "llfe_process_batch": (C.c_int, [_vp, C.POINTER(LlfeBatch), _u32, _u64, _vp, _vp, _i64, C.POINTER(C.c_int64), _vp]),
     "llfe_gray_blur5": (C.c_int, [_vp, _vp, _vp, _i32, _i32, _i32, _vp]),
     "llfe_shape_mask": (C.c_int, [_vp, _vp, _vp, _i32, _i32, _i32, _vp]),

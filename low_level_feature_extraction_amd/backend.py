@@ -100,6 +100,17 @@ class Backend:
         except Exception:
             pass
 
+    # ------------------------------------------------------------------ profiling
+    def set_profiling(self, enable: bool):
+        self._chk(self._lib.llfe_set_profiling(self.ctx, int(bool(enable))))
+
+    def kernel_stats(self) -> dict:
+        """{kernel: {"launches", "total_ms", "bytes"}} accumulated while profiling."""
+        arr = (L.LlfeKernelStat * 64)()
+        n = self._chk(self._lib.llfe_kernel_stats(self.ctx, arr, 64))
+        return {arr[i].name.decode(): {"launches": int(arr[i].launches), "total_ms": float(arr[i].total_ms),
+                                       "bytes": float(arr[i].bytes)} for i in range(min(n, 64))}
+
     # ------------------------------------------------------------------ helpers
     def _chk(self, rc):
         return L.check(self.ctx, rc)

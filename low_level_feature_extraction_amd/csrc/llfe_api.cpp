@@ -202,6 +202,73 @@ int pil_coeffs(int in_size, double in0, double in1, int out_size, std::vector<in
     return ksize;
 }
 
+// hipEvent pairs around launches (enabled by llfe_set_profiling)
+struct Profiler {
+    struct Rec {
+        int kid;
+        hipEvent_t a, b;
+        double bytes;
+    };
+    struct Stat {
+        std::string name;
+        int64_t launches = 0;
+        double ms = 0, bytes = 0;
+    };
+    bool on = false;
+    std::vector<hipEvent_t> pool;
+    size_t used = 0;
+    std::vector<Rec> pending;
+    std::vector<Stat> stats;
+    hipEvent_t ev() {
+        if (used == pool.size()) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return nullptr;
+            pool.push_back(e);
+        }
+        return pool[used++];
+    }
+    int kid(const char *name) {
+        for (size_t i = 0; i < stats.size(); i++)
+            if (stats[i].name == name) return (int)i;
+        stats.push_back(Stat{name});
+        return (int)stats.size() - 1;
+    }
+    hipEvent_t begin(hipStream_t s) {
+        if (!on) return nullptr;
+        hipEvent_t a = ev();
+        if (a) (void)hipEventRecord(a, s);
+        return a;
+    }
+    void end(hipEvent_t a, hipStream_t s, const char *name, double bytes) {
+        if (!on || !a) return;
+        hipEvent_t b = ev();
+        if (!b) return;
+        (void)hipEventRecord(b, s);
+        pending.push_back(Rec{kid(name), a, b, bytes});
+    }
+    // call after the stream has been synchronised
+    void collect() {
+        for (auto &r : pending) {
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
+                stats[r.kid].launches++;
+                stats[r.kid].ms += ms;
+                stats[r.kid].bytes += r.bytes;
+            }
+        }
+        pending.clear();
+        used = 0;
+    }
+    void reset() {
+        pending.clear();
+        used = 0;
+        stats.clear();
+    }
+    ~Profiler() {
+        for (auto e : pool) (void)hipEventDestroy(e);
+    }
+};
+
 int default_threads() {
     const char *e = getenv("LLFE_HOST_THREADS");
     if (e && atoi(e) > 0) return atoi(e);
@@ -215,6 +282,7 @@ struct llfe_ctx {
     int device = 0;
     std::string err;
     Pool *pool = nullptr;
+    Profiler prof;
     StencilParams sp{};
     // device workspace
     DevBuf<uint8_t> d_in, d_cls, d_dirty, d_rsz_tmp;
@@ -259,6 +327,14 @@ struct llfe_ctx {
                                                  __FILE__, __LINE__);                                       \
     } while (0)
 
+// launch `expr` bracketed by profiler events (name, algorithmic HBM bytes)
+#define TIMED(ctx, s, name, bytes, expr)                  \
+    do {                                                  \
+        hipEvent_t ev_a_ = (ctx)->prof.begin(s);          \
+        HIPCHK(ctx, expr);                                \
+        (ctx)->prof.end(ev_a_, s, name, (double)(bytes)); \
+    } while (0)
+
 namespace {
 
 constexpr int kChunk = 256;  // images per device pass (bounds workspace: ~15 MB / 1080p image)
@@ -296,7 +372,8 @@ int run_hysteresis(llfe_ctx *ctx, int n, int h, int w, hipStream_t s, int *launc
     for (;; it++) {
         HIPCHK(ctx, hipMemsetAsync(dout, 0, tiles, s));
         HIPCHK(ctx, hipMemsetAsync(ctx->d_changed.p, 0, sizeof(int), s));
-        HIPCHK(ctx, launch_hysteresis(ctx->d_cls.p, n, h, w, din, dout, ctx->d_changed.p, s));
+        TIMED(ctx, s, "k_hysteresis", (double)n * h * w,
+              launch_hysteresis(ctx->d_cls.p, n, h, w, din, dout, ctx->d_changed.p, s));
         HIPCHK(ctx, hipMemcpyAsync(ctx->h_changed.p, ctx->d_changed.p, sizeof(int), hipMemcpyDeviceToHost, s));
         HIPCHK(ctx, hipStreamSynchronize(s));
         if (*ctx->h_changed.p == 0) break;
@@ -317,8 +394,10 @@ int color_stage(llfe_ctx *ctx, const uint8_t *img, const int8_t *noise, int n, i
     HIPCHK(ctx, ctx->d_occ.ensure((size_t)n * kOccWords, true));
     HIPCHK(ctx, ctx->d_keys.ensure((size_t)n * key_stride));
     HIPCHK(ctx, ctx->d_nuniq.ensure(n));
-    HIPCHK(ctx, launch_color_bitmap(img, noise, n, h, w, seed, index_base, ctx->d_bitmap.p, ctx->d_occ.p, s));
-    HIPCHK(ctx, launch_color_compact(ctx->d_bitmap.p, ctx->d_occ.p, n, ctx->d_keys.p, key_stride, ctx->d_nuniq.p, s));
+    TIMED(ctx, s, "k_color_bitmap", (double)n * P * (noise ? 6 : 3),
+          launch_color_bitmap(img, noise, n, h, w, seed, index_base, ctx->d_bitmap.p, ctx->d_occ.p, s));
+    TIMED(ctx, s, "k_color_compact", (double)n * (4.0 * kBitmapWords),
+          launch_color_compact(ctx->d_bitmap.p, ctx->d_occ.p, n, ctx->d_keys.p, key_stride, ctx->d_nuniq.p, s));
     return LLFE_OK;
 }
 
@@ -337,8 +416,9 @@ int kmeans_stage(llfe_ctx *ctx, const uint32_t *keys, int64_t key_stride, const 
         ctx->h_rng.p[i] = st ? st : 0xFFFFFFFFull;
     }
     HIPCHK(ctx, hipMemcpyAsync(ctx->d_rng.p, ctx->h_rng.p, sizeof(uint64_t) * n, hipMemcpyHostToDevice, s));
-    HIPCHK(ctx, launch_kmeans(keys, key_stride, d_nuniq, n, n_colors, ctx->d_rng.p, ctx->d_order.p, ctx->d_kscratch.p,
-                              sstride, ctx->d_att.p, ctx->d_kout.p, s));
+    TIMED(ctx, s, "k_kmeans", 0,
+          launch_kmeans(keys, key_stride, d_nuniq, n, n_colors, ctx->d_rng.p, ctx->d_order.p, ctx->d_kscratch.p,
+                        sstride, ctx->d_att.p, ctx->d_kout.p, s));
     return LLFE_OK;
 }
 
@@ -396,6 +476,27 @@ int llfe_destroy(llfe_ctx *ctx) {
 
 const char *llfe_last_error(llfe_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
+int llfe_set_profiling(llfe_ctx *ctx, int enable) {
+    if (!ctx) return LLFE_ERR_INVALID;
+    if (enable) ctx->prof.reset();
+    ctx->prof.on = enable != 0;
+    return LLFE_OK;
+}
+
+int llfe_kernel_stats(llfe_ctx *ctx, llfe_kernel_stat *out, int32_t cap) {
+    if (!ctx) return LLFE_ERR_INVALID;
+    int n = (int)ctx->prof.stats.size();
+    for (int i = 0; i < n && i < cap && out; i++) {
+        const auto &st = ctx->prof.stats[i];
+        std::memset(&out[i], 0, sizeof(llfe_kernel_stat));
+        std::snprintf(out[i].name, sizeof(out[i].name), "%s", st.name.c_str());
+        out[i].launches = st.launches;
+        out[i].total_ms = st.ms;
+        out[i].bytes = st.bytes;
+    }
+    return n;
+}
+
 int llfe_process_batch(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_t seed,
                        llfe_image_result *results, llfe_shape *shapes, int64_t shape_capacity,
                        int64_t *shapes_needed, llfe_stream stream) {
@@ -421,9 +522,10 @@ int llfe_process_batch(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, ui
             HIPCHK(ctx, ctx->h_shadow.ensure(2 * (size_t)n));
             if (want_shp) HIPCHK(ctx, ctx->d_cls.ensure((size_t)n * P));
             if (want_shd) HIPCHK(ctx, hipMemsetAsync(ctx->d_shadow.p, 0, sizeof(unsigned long long) * 2 * n, s));
-            HIPCHK(ctx, launch_stencil(img, n, h, w, want_shp ? ctx->d_cls.p : nullptr, nullptr,
-                                       want_shd ? ctx->d_shadow.p : nullptr, want_shd ? ctx->d_shadow.p + n : nullptr,
-                                       ctx->sp, s));
+            TIMED(ctx, s, "k_stencil", (double)n * P * (3 + (want_shp ? 1 : 0)),
+                  launch_stencil(img, n, h, w, want_shp ? ctx->d_cls.p : nullptr, nullptr,
+                                 want_shd ? ctx->d_shadow.p : nullptr, want_shd ? ctx->d_shadow.p + n : nullptr,
+                                 ctx->sp, s));
         }
         if (want_col) {
             rc = color_stage(ctx, img, noise, n, h, w, seed, b->index_base + i0, s);
@@ -438,7 +540,8 @@ int llfe_process_batch(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, ui
             if (rc) return rc;
             HIPCHK(ctx, ctx->d_bits.ensure((size_t)n * h * wpr));
             HIPCHK(ctx, ctx->h_bits.ensure((size_t)n * h * wpr));
-            HIPCHK(ctx, launch_dilate_pack(ctx->d_cls.p, n, h, w, ctx->d_bits.p, nullptr, s));
+            TIMED(ctx, s, "k_dilate_pack", (double)n * P * 1.125,
+                  launch_dilate_pack(ctx->d_cls.p, n, h, w, ctx->d_bits.p, nullptr, s));
             HIPCHK(ctx, hipMemcpyAsync(ctx->h_bits.p, ctx->d_bits.p, sizeof(uint64_t) * n * h * wpr,
                                        hipMemcpyDeviceToHost, s));
         }
@@ -446,6 +549,7 @@ int llfe_process_batch(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, ui
             HIPCHK(ctx, hipMemcpyAsync(ctx->h_shadow.p, ctx->d_shadow.p, sizeof(unsigned long long) * 2 * n,
                                        hipMemcpyDeviceToHost, s));
         HIPCHK(ctx, hipStreamSynchronize(s));
+        ctx->prof.collect();
 
         for (int i = 0; i < n; i++) {
             llfe_image_result &r = results[i0 + i];
