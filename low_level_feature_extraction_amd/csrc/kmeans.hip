@@ -1,0 +1,676 @@
+// cv2.kmeans(float32(unique_colors), K, None, (EPS+MAX_ITER, 200, 0.2), 10,
+// KMEANS_PP_CENTERS) for a batch of images on gfx950
+// (app/services/analyze/color_extractor.py:189-197).
+//
+// One 1024-thread workgroup per (image, attempt); workgroups are issued largest-U
+// first (LPT) so the many short "ui" attempts back-fill behind the long "photo" ones.
+// The point set is the compacted unique-colour key list (4 B / point, ascending =
+// np.unique row order); wave w owns a contiguous range of 256-point steps and reads
+// it with 16-byte coalesced loads.
+//
+// OpenCV semantics restated (kmeans.cpp):
+//  * attempt a starts from cv::RNG state advanced by a * (1 + 6 (K-1)) draws
+//    (generateCentersPP consumes 1 + 3 trials x 2 draws per extra centre);
+//  * k-means++: c0 = rng % N; for k >= 1, three trials p = rng.double * sum(D) ->
+//    first i with prefix(D, i) >= p (exact: D are integers), keep the trial with the
+//    smallest sum(min(D, d(., ci))) (first on ties);
+//  * Lloyd: labels by the first minimum of the float32 normL2Sqr (t0*t0, fma, fma);
+//    centres = float(sum) * (1.f / count); empty clusters take the farthest point of
+//    the biggest cluster; stop when ++iter == 100 or max shift^2 <= 0.2^2;
+//  * compactness = sum of double(normL2Sqr) to the final centres with the labels of
+//    the last assignment.  Cluster sums are exact int64 (OpenCV accumulates float32
+//    sequentially; the difference is far below the uint8 truncation of the output).
+#include "llfe_internal.h"
+
+namespace llfe {
+namespace {
+
+constexpr int KT = 1024;          // threads per (image, attempt)
+constexpr int KW = KT / 64;       // waves
+constexpr int STEP = 256;         // points per wave step (64 lanes x 4)
+constexpr float kFar = 1e30f;     // coordinate of an unused centre: its distance is +inf
+
+__device__ __forceinline__ uint32_t cvrng_next(uint64_t &s) {
+    s = (uint64_t)(uint32_t)s * 4164903690ull + (uint32_t)(s >> 32);
+    return (uint32_t)s;
+}
+__device__ __forceinline__ double cvrng_double(uint64_t &s) {
+    uint32_t t = cvrng_next(s);
+    uint64_t v = ((uint64_t)t << 32) | cvrng_next(s);
+    return (double)v * 5.4210108624275221700372640043497e-20;
+}
+
+__device__ __forceinline__ float uni(float v) {
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+
+// OpenCV normL2Sqr<float>(dims = 3) of the AVX2/FMA3 dispatch: t0*t0, fma(t1), fma(t2)
+__device__ __forceinline__ float d2(float x, float y, float z, float cx, float cy, float cz) {
+    float t0 = x - cx, t1 = y - cy, t2 = z - cz;
+    float d = t0 * t0;
+    d = __builtin_fmaf(t1, t1, d);
+    d = __builtin_fmaf(t2, t2, d);
+    return d;
+}
+
+struct P3 {
+    float x, y, z;
+};
+__device__ __forceinline__ P3 unpack(uint32_t k) {
+    return P3{(float)((k >> 16) & 255u), (float)((k >> 8) & 255u), (float)(k & 255u)};
+}
+
+struct Cent {
+    float x[kMaxK], y[kMaxK], z[kMaxK];
+};
+
+// first minimum over 5 centres (unused centres sit at kFar -> +inf)
+__device__ __forceinline__ int label5(const P3 &p, const Cent &c, float &best) {
+    best = d2(p.x, p.y, p.z, c.x[0], c.y[0], c.z[0]);
+    int l = 0;
+#pragma unroll
+    for (int k = 1; k < kMaxK; k++) {
+        float d = d2(p.x, p.y, p.z, c.x[k], c.y[k], c.z[k]);
+        bool lt = d < best;
+        best = lt ? d : best;
+        l = lt ? k : l;
+    }
+    return l;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+struct KmSmem {
+    unsigned long long accA[kMaxK][KT];  // x | y << 32 per lane and cluster
+    unsigned long long accB[kMaxK][KT];  // z | 1 << 32
+    unsigned long long red[20][32];
+    unsigned long long wtot[KW][3];
+    unsigned long long scan_w[KW];
+    double dred[KW];
+    double maxd[KW];
+    int maxi[KW];
+    float c[kMaxK][3];
+    float cprev[kMaxK][3];
+    float cc[kMaxK][3];
+    long long sums[kMaxK][3];
+    int counts[kMaxK];
+    int moved_idx[kMaxK];
+    int moved_lbl[kMaxK];
+    int n_moved;
+    int found_step[3];
+    unsigned long long found_excl[3];
+    int ci[3];
+    int flag;
+};
+
+__device__ __forceinline__ Cent load_centres(const float (*c)[3]) {
+    Cent r;
+#pragma unroll
+    for (int k = 0; k < kMaxK; k++) {
+        r.x[k] = uni(c[k][0]);
+        r.y[k] = uni(c[k][1]);
+        r.z[k] = uni(c[k][2]);
+    }
+    return r;
+}
+
+__device__ __forceinline__ int moved_label(const KmSmem &sm, int i, int l) {
+    for (int m = 0; m < sm.n_moved; m++)
+        if (sm.moved_idx[m] == i) l = sm.moved_lbl[m];
+    return l;
+}
+
+__global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys, long long key_stride,
+                                               const long long *__restrict__ n_unique, int n_colors,
+                                               const uint64_t *__restrict__ rng_states, const int *__restrict__ order,
+                                               uint32_t *__restrict__ scratch, long long scratch_stride,
+                                               KmeansAttemptOut *__restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    KmSmem &sm = *reinterpret_cast<KmSmem *>(smem_raw);
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int img = order[blockIdx.x / kAttempts];
+    const int att = blockIdx.x % kAttempts;
+    const int N = (int)n_unique[img];
+    const int K = min(n_colors, N);
+    KmeansAttemptOut *o = out + (size_t)img * kAttempts + att;
+    if (K <= 1) {
+        if (tid == 0) {
+            o->compactness = 0.0;
+            o->iters = 0;
+        }
+        return;
+    }
+    const uint32_t *pts = keys + (size_t)img * key_stride;
+    const int M = (N + STEP - 1) / STEP;         // steps
+    const int Mw = (M + KW - 1) / KW;            // steps per wave
+    const int sb = min(M, wid * Mw), se = min(M, sb + Mw);
+    const int se_full = min(se, N / STEP);       // steps whose 256 points are all valid
+    uint32_t *ss = scratch + ((size_t)img * kAttempts + att) * (size_t)scratch_stride;
+#define SSLOT(slot) (ss + (size_t)(slot) * (size_t)M)
+
+    uint64_t rng = rng_states[img];
+    for (int q = 0, skip = att * (1 + 6 * (K - 1)); q < skip; q++) cvrng_next(rng);
+
+    // ------------------------------------------------ k-means++ (generateCentersPP)
+    int cur = 0;
+    {
+        const uint32_t c0 = cvrng_next(rng) % (uint32_t)N;
+        const P3 q0 = unpack(pts[c0]);
+        if (tid == 0) {
+            sm.cc[0][0] = q0.x; sm.cc[0][1] = q0.y; sm.cc[0][2] = q0.z;
+        }
+        const float cx = uni(q0.x), cy = uni(q0.y), cz = uni(q0.z);
+        unsigned long long wt = 0;
+        for (int s = sb; s < se; s++) {
+            const int i0 = s * STEP + lane * 4;
+            uint32_t ls = 0;
+            if (s < se_full) {
+                uint4 v = *(const uint4 *)(pts + i0);
+                uint32_t kq[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    P3 p = unpack(kq[j]);
+                    ls += (uint32_t)d2(p.x, p.y, p.z, cx, cy, cz);
+                }
+            } else {
+                for (int j = 0; j < 4; j++)
+                    if (i0 + j < N) {
+                        P3 p = unpack(pts[i0 + j]);
+                        ls += (uint32_t)d2(p.x, p.y, p.z, cx, cy, cz);
+                    }
+            }
+            uint32_t st = wave_sum(ls);
+            if (lane == 0) SSLOT(0)[s] = st;
+            wt += st;
+        }
+        if (lane == 0) sm.wtot[wid][0] = wt;
+    }
+    __syncthreads();
+    unsigned long long sum0 = 0;
+    for (int w = 0; w < KW; w++) sum0 += sm.wtot[w][0];
+    __syncthreads();
+
+    for (int kk = 1; kk < K; kk++) {
+        double p[3];
+#pragma unroll
+        for (int j = 0; j < 3; j++) p[j] = cvrng_double(rng) * (double)sum0;
+        // chosen centres so far (uniform)
+        Cent ch;
+#pragma unroll
+        for (int m = 0; m < kMaxK; m++) {
+            bool u = m < kk;
+            ch.x[m] = u ? uni(sm.cc[m][0]) : kFar;
+            ch.y[m] = u ? uni(sm.cc[m][1]) : kFar;
+            ch.z[m] = u ? uni(sm.cc[m][2]) : kFar;
+        }
+        // ---- locate the step holding prefix(D) >= p_j: thread-contiguous step ranges
+        {
+            const int q = (M + KT - 1) / KT;
+            const int t0 = min(M, tid * q), t1 = min(M, t0 + q);
+            unsigned long long R = 0;
+            const uint32_t *scur = SSLOT(cur);
+            for (int s = t0; s < t1; s++) R += scur[s];
+            unsigned long long x = R;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                unsigned long long y = __shfl_up(x, off);
+                if (lane >= off) x += y;
+            }
+            if (lane == 63) sm.scan_w[wid] = x;
+            if (tid < 3) {
+                sm.found_step[tid] = -1;
+                sm.ci[tid] = -1;
+            }
+            __syncthreads();
+            unsigned long long pre = 0;
+            for (int w = 0; w < wid; w++) pre += sm.scan_w[w];
+            const unsigned long long excl = pre + x - R;
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                if (p[j] > 0 && (double)excl < p[j] && p[j] <= (double)(excl + R)) {
+                    unsigned long long e = excl;
+                    for (int s = t0; s < t1; s++) {
+                        unsigned long long v = scur[s];
+                        if ((double)(e + v) >= p[j]) {
+                            sm.found_step[j] = s;
+                            sm.found_excl[j] = e;
+                            break;
+                        }
+                        e += v;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        // ---- waves 0..2 resolve the point inside the found step
+        if (wid < 3) {
+            const int j = wid;
+            const double pj = j == 0 ? p[0] : (j == 1 ? p[1] : p[2]);
+            if (!(pj > 0)) {
+                if (lane == 0) sm.ci[j] = 0;
+            } else if (sm.found_step[j] < 0) {
+                if (lane == 0) sm.ci[j] = N - 1;
+            } else {
+                const int s = sm.found_step[j];
+                const int i0 = s * STEP + lane * 4;
+                uint32_t dv[4], lsum = 0;
+#pragma unroll
+                for (int jj = 0; jj < 4; jj++) {
+                    dv[jj] = 0;
+                    if (i0 + jj < N) {
+                        P3 pp = unpack(pts[i0 + jj]);
+                        float d = d2(pp.x, pp.y, pp.z, ch.x[0], ch.y[0], ch.z[0]);
+#pragma unroll
+                        for (int m = 1; m < kMaxK; m++)
+                            if (m < kk) d = fminf(d, d2(pp.x, pp.y, pp.z, ch.x[m], ch.y[m], ch.z[m]));
+                        dv[jj] = (uint32_t)d;
+                    }
+                    lsum += dv[jj];
+                }
+                unsigned long long x = lsum;
+#pragma unroll
+                for (int off = 1; off < 64; off <<= 1) {
+                    unsigned long long y = __shfl_up(x, off);
+                    if (lane >= off) x += y;
+                }
+                unsigned long long e = sm.found_excl[j] + x - lsum;
+                int hit = -1;
+#pragma unroll
+                for (int jj = 0; jj < 4; jj++) {
+                    e += dv[jj];
+                    if (hit < 0 && (double)e >= pj) hit = jj;
+                }
+                unsigned long long bal = __ballot(hit >= 0);
+                int first = (int)__builtin_ctzll(bal);
+                int hitj = __shfl(hit, first);
+                if (lane == 0) sm.ci[j] = min(s * STEP + first * 4 + hitj, N - 1);
+            }
+        }
+        __syncthreads();
+        Cent tc;  // trial centres in x[0..2]
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            P3 pp = unpack(pts[sm.ci[j]]);
+            tc.x[j] = uni(pp.x);
+            tc.y[j] = uni(pp.y);
+            tc.z[j] = uni(pp.z);
+        }
+        // ---- trial pass: T_j(i) = min(D(i), d(i, ci_j)); step sums into three free slots
+        // the three slots other than `cur`, in increasing order
+        const int sl0 = cur == 0 ? 1 : 0, sl1 = cur <= 1 ? 2 : 1, sl2 = cur <= 2 ? 3 : 2;
+        uint32_t *o0 = SSLOT(sl0), *o1 = SSLOT(sl1), *o2 = SSLOT(sl2);
+        unsigned long long wt0 = 0, wt1 = 0, wt2 = 0;
+        for (int s = sb; s < se; s++) {
+            const int i0 = s * STEP + lane * 4;
+            uint32_t kq[4];
+            int cnt = 4;
+            if (s < se_full) {
+                uint4 v = *(const uint4 *)(pts + i0);
+                kq[0] = v.x; kq[1] = v.y; kq[2] = v.z; kq[3] = v.w;
+            } else {
+                cnt = max(0, min(4, N - i0));
+                for (int jj = 0; jj < 4; jj++) kq[jj] = jj < cnt ? pts[i0 + jj] : 0u;
+            }
+            uint32_t l0 = 0, l1 = 0, l2 = 0;
+#pragma unroll
+            for (int jj = 0; jj < 4; jj++) {
+                P3 pp = unpack(kq[jj]);
+                float d = d2(pp.x, pp.y, pp.z, ch.x[0], ch.y[0], ch.z[0]);
+#pragma unroll
+                for (int m = 1; m < kMaxK; m++)
+                    if (m < kk) d = fminf(d, d2(pp.x, pp.y, pp.z, ch.x[m], ch.y[m], ch.z[m]));
+                uint32_t v0 = (uint32_t)fminf(d, d2(pp.x, pp.y, pp.z, tc.x[0], tc.y[0], tc.z[0]));
+                uint32_t v1 = (uint32_t)fminf(d, d2(pp.x, pp.y, pp.z, tc.x[1], tc.y[1], tc.z[1]));
+                uint32_t v2 = (uint32_t)fminf(d, d2(pp.x, pp.y, pp.z, tc.x[2], tc.y[2], tc.z[2]));
+                bool ok = jj < cnt;
+                l0 += ok ? v0 : 0u;
+                l1 += ok ? v1 : 0u;
+                l2 += ok ? v2 : 0u;
+            }
+            uint32_t a0 = wave_sum(l0), a1 = wave_sum(l1), a2 = wave_sum(l2);
+            if (lane == 0) {
+                o0[s] = a0;
+                o1[s] = a1;
+                o2[s] = a2;
+            }
+            wt0 += a0;
+            wt1 += a1;
+            wt2 += a2;
+        }
+        if (lane == 0) {
+            sm.wtot[wid][0] = wt0;
+            sm.wtot[wid][1] = wt1;
+            sm.wtot[wid][2] = wt2;
+        }
+        __syncthreads();
+        unsigned long long S[3] = {0, 0, 0};
+        for (int w = 0; w < KW; w++)
+            for (int j = 0; j < 3; j++) S[j] += sm.wtot[w][j];
+        int best = 0;
+        double bs = 1.7976931348623157e308;
+        for (int j = 0; j < 3; j++)
+            if ((double)S[j] < bs) {
+                bs = (double)S[j];
+                best = j;
+            }
+        sum0 = S[best];
+        cur = best == 0 ? sl0 : (best == 1 ? sl1 : sl2);
+        __syncthreads();
+        if (tid == 0) {
+            sm.cc[kk][0] = tc.x[best];
+            sm.cc[kk][1] = tc.y[best];
+            sm.cc[kk][2] = tc.z[best];
+        }
+        __syncthreads();
+    }
+
+    // ------------------------------------------------ Lloyd iterations
+    if (tid < kMaxK * 3) {
+        int k = tid / 3, j = tid % 3;
+        sm.c[k][j] = k < K ? sm.cc[k][j] : kFar;
+    }
+    __syncthreads();
+
+    int iter = 1;
+    const double eps2 = 0.2 * 0.2;
+    for (;;) {
+        const Cent c = load_centres(sm.c);
+#pragma unroll
+        for (int k = 0; k < kMaxK; k++) {
+            sm.accA[k][tid] = 0;
+            sm.accB[k][tid] = 0;
+        }
+        // (lane-private slots: no barrier needed between zeroing and accumulation)
+#pragma unroll 2
+        for (int s = sb; s < se_full; s++) {
+            uint4 v = *(const uint4 *)(pts + s * STEP + lane * 4);
+            uint32_t kq[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int jj = 0; jj < 4; jj++) {
+                float bd;
+                int l = label5(unpack(kq[jj]), c, bd);
+                unsigned long long a = (unsigned long long)((kq[jj] >> 16) & 255u) |
+                                       ((unsigned long long)((kq[jj] >> 8) & 255u) << 32);
+                unsigned long long b = (unsigned long long)(kq[jj] & 255u) | (1ull << 32);
+                atomicAdd(&sm.accA[l][tid], a);
+                atomicAdd(&sm.accB[l][tid], b);
+            }
+        }
+        for (int s = se_full; s < se; s++) {  // at most one partial step
+            const int i0 = s * STEP + lane * 4;
+            for (int jj = 0; jj < 4; jj++) {
+                if (i0 + jj >= N) break;
+                uint32_t kq = pts[i0 + jj];
+                float bd;
+                int l = label5(unpack(kq), c, bd);
+                atomicAdd(&sm.accA[l][tid], (unsigned long long)((kq >> 16) & 255u) |
+                                                ((unsigned long long)((kq >> 8) & 255u) << 32));
+                atomicAdd(&sm.accB[l][tid], (unsigned long long)(kq & 255u) | (1ull << 32));
+            }
+        }
+        __syncthreads();
+        // reduce 20 values (5 clusters x {x, y, z, count}) over 1024 lanes
+        if (tid < 640) {
+            const int v = tid >> 5, part = tid & 31;
+            const int k = v >> 2, comp = v & 3;
+            unsigned long long acc = 0;
+            const unsigned long long *src = comp < 2 ? sm.accA[k] : sm.accB[k];
+#pragma unroll 4
+            for (int l = part * 32; l < part * 32 + 32; l++) {
+                unsigned long long wv = src[l];
+                acc += (comp & 1) ? (wv >> 32) : (wv & 0xFFFFFFFFull);
+            }
+            sm.red[v][part] = acc;
+        }
+        __syncthreads();
+        if (tid < 20) {
+            unsigned long long acc = 0;
+            for (int part = 0; part < 32; part++) acc += sm.red[tid][part];
+            const int k = tid >> 2, comp = tid & 3;
+            if (comp < 3) sm.sums[k][comp] = (long long)acc;
+            else sm.counts[k] = (int)acc;
+        } else if (tid < 20 + kMaxK * 3) {
+            const int q = tid - 20, k = q / 3, j = q % 3;
+            sm.cprev[k][j] = sm.c[k][j];
+        } else if (tid == 64) {
+            sm.n_moved = 0;
+        }
+        __syncthreads();
+
+        // ---- empty clusters: move the farthest point of the biggest cluster (rare)
+        for (int ek = 0; ek < K; ek++) {
+            if (sm.counts[ek] != 0) continue;  // uniform
+            int max_k = 0;
+            for (int k1 = 1; k1 < K; k1++)
+                if (sm.counts[max_k] < sm.counts[k1]) max_k = k1;
+            const float scale = 1.f / (float)sm.counts[max_k];
+            const float bx = (float)sm.sums[max_k][0] * scale, by = (float)sm.sums[max_k][1] * scale,
+                        bz = (float)sm.sums[max_k][2] * scale;
+            const Cent cp = load_centres(sm.cprev);
+            double md = -1.0;
+            int mi = -1;
+            for (int s = sb; s < se; s++) {
+                const int i0 = s * STEP + lane * 4;
+                for (int jj = 0; jj < 4; jj++) {
+                    const int i = i0 + jj;
+                    if (i >= N) break;
+                    P3 pp = unpack(pts[i]);
+                    float bd;
+                    int l = moved_label(sm, i, label5(pp, cp, bd));
+                    if (l != max_k) continue;
+                    double d = (double)d2(pp.x, pp.y, pp.z, bx, by, bz);
+                    if (md <= d) {
+                        md = d;
+                        mi = i;
+                    }
+                }
+            }
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+                double od = __shfl_xor(md, off);
+                int oi = __shfl_xor(mi, off);
+                if (od > md || (od == md && oi > mi)) {
+                    md = od;
+                    mi = oi;
+                }
+            }
+            if (lane == 0) {
+                sm.maxd[wid] = md;
+                sm.maxi[wid] = mi;
+            }
+            __syncthreads();
+            if (tid == 0) {
+                double bd2 = -1.0;
+                int bi = -1;
+                for (int w = 0; w < KW; w++)
+                    if (sm.maxd[w] > bd2 || (sm.maxd[w] == bd2 && sm.maxi[w] > bi)) {
+                        bd2 = sm.maxd[w];
+                        bi = sm.maxi[w];
+                    }
+                if (bi >= 0) {
+                    P3 pp = unpack(pts[bi]);
+                    sm.counts[max_k]--;
+                    sm.counts[ek]++;
+                    sm.sums[max_k][0] -= (long long)pp.x;
+                    sm.sums[max_k][1] -= (long long)pp.y;
+                    sm.sums[max_k][2] -= (long long)pp.z;
+                    sm.sums[ek][0] += (long long)pp.x;
+                    sm.sums[ek][1] += (long long)pp.y;
+                    sm.sums[ek][2] += (long long)pp.z;
+                    sm.moved_idx[sm.n_moved] = bi;
+                    sm.moved_lbl[sm.n_moved] = ek;
+                    sm.n_moved++;
+                }
+            }
+            __syncthreads();
+        }
+        if (tid == 0) {
+            double max_shift = 0.0;
+            for (int k = 0; k < K; k++) {
+                const float scale = 1.f / (float)sm.counts[k];
+                double dist = 0.0;
+                for (int j = 0; j < 3; j++) {
+                    float v = (float)sm.sums[k][j] * scale;
+                    sm.c[k][j] = v;
+                    double t = (double)(v - sm.cprev[k][j]);
+                    dist += t * t;
+                }
+                max_shift = fmax(max_shift, dist);
+            }
+            sm.flag = (iter + 1 == 100 || max_shift <= eps2) ? 1 : 0;
+        }
+        iter++;
+        __syncthreads();
+        if (sm.flag) break;
+    }
+
+    // ------------------------------------------------ compactness with the last labels
+    {
+        const Cent cp = load_centres(sm.cprev);
+        const Cent cn = load_centres(sm.c);
+        const bool moved = sm.n_moved > 0;
+        double acc = 0.0;
+        for (int s = sb; s < se; s++) {
+            const int i0 = s * STEP + lane * 4;
+            for (int jj = 0; jj < 4; jj++) {
+                const int i = i0 + jj;
+                if (i >= N) break;
+                P3 pp = unpack(pts[i]);
+                float bd;
+                int l = label5(pp, cp, bd);
+                if (moved) l = moved_label(sm, i, l);
+                float cx = cn.x[0], cy = cn.y[0], cz = cn.z[0];
+#pragma unroll
+                for (int k = 1; k < kMaxK; k++) {
+                    cx = l == k ? cn.x[k] : cx;
+                    cy = l == k ? cn.y[k] : cy;
+                    cz = l == k ? cn.z[k] : cz;
+                }
+                acc += (double)d2(pp.x, pp.y, pp.z, cx, cy, cz);
+            }
+        }
+        acc = wave_sum(acc);
+        if (lane == 0) sm.dred[wid] = acc;
+        __syncthreads();
+        if (tid == 0) {
+            double compactness = 0.0;
+            for (int w = 0; w < KW; w++) compactness += sm.dred[w];
+            o->compactness = compactness;
+            o->iters = iter;
+            for (int k = 0; k < kMaxK; k++) {
+                for (int j = 0; j < 3; j++) o->centers[k][j] = k < K ? sm.c[k][j] : 0.f;
+                o->counts[k] = k < K ? sm.counts[k] : 0;
+            }
+        }
+    }
+}
+
+// LPT order: images sorted by U descending (bitonic sort in LDS, n <= 4096)
+constexpr int OT = 1024;
+constexpr int OMAX = 4096;
+__global__ __launch_bounds__(OT) void k_kmeans_order(const long long *__restrict__ n_unique, int n,
+                                                     int *__restrict__ order) {
+    __shared__ long long key[OMAX];
+    __shared__ int idx[OMAX];
+    int np2 = 1;
+    while (np2 < n) np2 <<= 1;
+    for (int i = threadIdx.x; i < np2; i += OT) {
+        key[i] = i < n ? n_unique[i] : -1;
+        idx[i] = i;
+    }
+    __syncthreads();
+    for (int k = 2; k <= np2; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < np2; i += OT) {
+                int l = i ^ j;
+                if (l > i) {
+                    bool desc = (i & k) == 0;
+                    bool sw = desc ? (key[i] < key[l] || (key[i] == key[l] && idx[i] > idx[l]))
+                                   : (key[i] > key[l] || (key[i] == key[l] && idx[i] < idx[l]));
+                    if (sw) {
+                        long long tk = key[i];
+                        key[i] = key[l];
+                        key[l] = tk;
+                        int ti = idx[i];
+                        idx[i] = idx[l];
+                        idx[l] = ti;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    for (int i = threadIdx.x; i < n; i += OT) order[i] = idx[i];
+}
+
+__global__ void k_kmeans_finalize(const uint32_t *__restrict__ keys, long long key_stride,
+                                  const long long *__restrict__ n_unique, int n, int n_colors,
+                                  const KmeansAttemptOut *__restrict__ att, KmeansImageOut *__restrict__ out) {
+    int img = blockIdx.x * blockDim.x + threadIdx.x;
+    if (img >= n) return;
+    long long N = n_unique[img];
+    int K = (int)min((long long)n_colors, N);
+    KmeansImageOut r;
+    memset(&r, 0, sizeof r);
+    r.n_unique = N;
+    if (K <= 1) {
+        r.k = (int)N;
+        if (N == 1) {
+            uint32_t k = keys[(size_t)img * key_stride];
+            r.centers_rgb[0][0] = (uint8_t)(k >> 16);
+            r.centers_rgb[0][1] = (uint8_t)(k >> 8);
+            r.centers_rgb[0][2] = (uint8_t)k;
+            r.counts[0] = 1;
+        }
+        r.compactness = 0.0;
+    } else {
+        int best = 0;
+        double bc = 1.7976931348623157e308;
+        for (int a = 0; a < kAttempts; a++) {  // first attempt with the strictly smallest compactness
+            double c = att[(size_t)img * kAttempts + a].compactness;
+            if (c < bc) {
+                bc = c;
+                best = a;
+            }
+        }
+        const KmeansAttemptOut &b = att[(size_t)img * kAttempts + best];
+        r.k = K;
+        r.compactness = bc;
+        for (int k = 0; k < K; k++) {
+            for (int j = 0; j < 3; j++) r.centers_rgb[k][j] = (uint8_t)(int)b.centers[k][j];  // astype(uint8)
+            r.counts[k] = b.counts[k];
+        }
+    }
+    out[img] = r;
+}
+
+}  // namespace
+
+hipError_t launch_kmeans(const uint32_t *keys, int64_t key_stride, const int64_t *n_unique, int n, int n_colors,
+                         const uint64_t *rng_states, int32_t *order, uint32_t *scratch, int64_t scratch_stride,
+                         KmeansAttemptOut *attempts, KmeansImageOut *out, hipStream_t s) {
+    if (n > OMAX) return hipErrorInvalidValue;
+    if (n == 0) return hipSuccess;
+    static bool attr_set = false;
+    const size_t smem = sizeof(KmSmem);
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void *)k_kmeans, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    hipLaunchKernelGGL(k_kmeans_order, dim3(1), dim3(OT), 0, s, (const long long *)n_unique, n, order);
+    hipLaunchKernelGGL(k_kmeans, dim3(n * kAttempts), dim3(KT), smem, s, keys, (long long)key_stride,
+                       (const long long *)n_unique, n_colors, rng_states, order, scratch, (long long)scratch_stride,
+                       attempts);
+    hipLaunchKernelGGL(k_kmeans_finalize, dim3((n + 255) / 256), dim3(256), 0, s, keys, (long long)key_stride,
+                       (const long long *)n_unique, n, n_colors, attempts, out);
+    return hipGetLastError();
+}
+
+int64_t kmeans_scratch_stride(int64_t key_stride) { return 4 * ((key_stride + STEP - 1) / STEP) + 4; }
+
+}  // namespace llfe

@@ -112,6 +112,7 @@ struct DevBuf {
         p = nullptr;
         n = 0;
     }
+    ~DevBuf() { release(); }
 };
 
 template <typename T>
@@ -132,6 +133,7 @@ struct HostBuf {
         p = nullptr;
         n = 0;
     }
+    ~HostBuf() { release(); }
 };
 
 uint64_t splitmix64(uint64_t x) {
@@ -285,11 +287,12 @@ struct llfe_ctx {
     Profiler prof;
     StencilParams sp{};
     // device workspace
-    DevBuf<uint8_t> d_in, d_cls, d_dirty, d_rsz_tmp;
+    DevBuf<uint8_t> d_in, d_cls, d_rsz_tmp, d_sroot;
     DevBuf<int8_t> d_noise;
     DevBuf<uint64_t> d_bits, d_rng;
     DevBuf<unsigned long long> d_shadow;
-    DevBuf<int> d_changed, d_order;
+    DevBuf<int> d_order, d_parent, d_nroots;
+    DevBuf<uint16_t> d_lab, d_roots;
     DevBuf<uint32_t> d_bitmap, d_occ, d_keys, d_kscratch;
     DevBuf<int64_t> d_nuniq;
     DevBuf<KmeansAttemptOut> d_att;
@@ -299,7 +302,6 @@ struct llfe_ctx {
     HostBuf<uint64_t> h_bits;
     HostBuf<unsigned long long> h_shadow;
     HostBuf<KmeansImageOut> h_kout;
-    HostBuf<int> h_changed;
     HostBuf<uint64_t> h_rng;
     HostBuf<int64_t> h_nuniq;
     // per-thread host scratch
@@ -362,27 +364,18 @@ int stage_input(llfe_ctx *ctx, const llfe_batch *b, int i0, int n, const uint8_t
     return LLFE_OK;
 }
 
-int run_hysteresis(llfe_ctx *ctx, int n, int h, int w, hipStream_t s, int *launches) {
+// Canny hysteresis (connected components) + dilate + pack of ctx->d_cls.
+int run_hysteresis_dilate(llfe_ctx *ctx, int n, int h, int w, uint64_t *bits, uint8_t *mask_u8, hipStream_t s) {
+    const size_t ids = hysteresis_ids(n, h, w);
     const size_t tiles = (size_t)tiles_x(w) * tiles_y(h) * n;
-    HIPCHK(ctx, ctx->d_dirty.ensure(2 * tiles));
-    HIPCHK(ctx, ctx->d_changed.ensure(1));
-    HIPCHK(ctx, ctx->h_changed.ensure(1));
-    uint8_t *din = nullptr, *dout = ctx->d_dirty.p, *dspare = ctx->d_dirty.p + tiles;
-    int it = 0;
-    for (;; it++) {
-        HIPCHK(ctx, hipMemsetAsync(dout, 0, tiles, s));
-        HIPCHK(ctx, hipMemsetAsync(ctx->d_changed.p, 0, sizeof(int), s));
-        TIMED(ctx, s, "k_hysteresis", (double)n * h * w,
-              launch_hysteresis(ctx->d_cls.p, n, h, w, din, dout, ctx->d_changed.p, s));
-        HIPCHK(ctx, hipMemcpyAsync(ctx->h_changed.p, ctx->d_changed.p, sizeof(int), hipMemcpyDeviceToHost, s));
-        HIPCHK(ctx, hipStreamSynchronize(s));
-        if (*ctx->h_changed.p == 0) break;
-        if (it > 100000) return ctx->fail(LLFE_ERR_INVALID, "hysteresis did not converge");
-        uint8_t *t = din ? din : dspare;
-        din = dout;
-        dout = t;
-    }
-    if (launches) *launches = it + 1;
+    HIPCHK(ctx, ctx->d_lab.ensure((size_t)n * h * w));
+    HIPCHK(ctx, ctx->d_parent.ensure(ids));
+    HIPCHK(ctx, ctx->d_sroot.ensure(ids));
+    HIPCHK(ctx, ctx->d_roots.ensure(ids));
+    HIPCHK(ctx, ctx->d_nroots.ensure(tiles));
+    HystWork wk{ctx->d_lab.p, ctx->d_parent.p, ctx->d_sroot.p, ctx->d_roots.p, ctx->d_nroots.p};
+    TIMED(ctx, s, "k_hysteresis_dilate", (double)n * h * w * (1 + 2 + 2 + 1 + 0.125),
+          launch_hysteresis_dilate(ctx->d_cls.p, n, h, w, wk, bits, mask_u8, s));
     return LLFE_OK;
 }
 
@@ -462,15 +455,8 @@ int llfe_init(int device, llfe_ctx **out) {
 int llfe_destroy(llfe_ctx *ctx) {
     if (!ctx) return LLFE_OK;
     (void)hipSetDevice(ctx->device);
-    ctx->d_in.release(); ctx->d_cls.release(); ctx->d_dirty.release(); ctx->d_rsz_tmp.release();
-    ctx->d_noise.release(); ctx->d_bits.release(); ctx->d_rng.release(); ctx->d_shadow.release();
-    ctx->d_changed.release(); ctx->d_order.release(); ctx->d_bitmap.release(); ctx->d_occ.release();
-    ctx->d_keys.release(); ctx->d_kscratch.release(); ctx->d_nuniq.release(); ctx->d_att.release();
-    ctx->d_kout.release(); ctx->d_coef.release();
-    ctx->h_bits.release(); ctx->h_shadow.release(); ctx->h_kout.release(); ctx->h_changed.release();
-    ctx->h_rng.release(); ctx->h_nuniq.release();
     delete ctx->pool;
-    delete ctx;
+    delete ctx;  // DevBuf / HostBuf members free themselves
     return LLFE_OK;
 }
 
@@ -536,12 +522,10 @@ int llfe_process_batch(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, ui
             HIPCHK(ctx, hipMemcpyAsync(ctx->h_kout.p, ctx->d_kout.p, sizeof(KmeansImageOut) * n, hipMemcpyDeviceToHost, s));
         }
         if (want_shp) {
-            rc = run_hysteresis(ctx, n, h, w, s, nullptr);
-            if (rc) return rc;
             HIPCHK(ctx, ctx->d_bits.ensure((size_t)n * h * wpr));
             HIPCHK(ctx, ctx->h_bits.ensure((size_t)n * h * wpr));
-            TIMED(ctx, s, "k_dilate_pack", (double)n * P * 1.125,
-                  launch_dilate_pack(ctx->d_cls.p, n, h, w, ctx->d_bits.p, nullptr, s));
+            rc = run_hysteresis_dilate(ctx, n, h, w, ctx->d_bits.p, nullptr, s);
+            if (rc) return rc;
             HIPCHK(ctx, hipMemcpyAsync(ctx->h_bits.p, ctx->d_bits.p, sizeof(uint64_t) * n * h * wpr,
                                        hipMemcpyDeviceToHost, s));
         }
@@ -613,10 +597,10 @@ int llfe_shape_mask(llfe_ctx *ctx, const uint8_t *bgr, uint8_t *mask, int32_t n,
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(ctx, ctx->d_cls.ensure((size_t)n * h * w));
     HIPCHK(ctx, launch_stencil(bgr, n, h, w, ctx->d_cls.p, nullptr, nullptr, nullptr, ctx->sp, s));
-    int rc = run_hysteresis(ctx, n, h, w, s, nullptr);
+    int rc = run_hysteresis_dilate(ctx, n, h, w, nullptr, mask, s);
     if (rc) return rc;
-    HIPCHK(ctx, launch_dilate_pack(ctx->d_cls.p, n, h, w, nullptr, mask, s));
     HIPCHK(ctx, hipStreamSynchronize(s));
+    ctx->prof.collect();
     return LLFE_OK;
 }
 

@@ -23,16 +23,19 @@ hipError_t launch_stencil(const uint8_t *bgr, int n, int h, int w, uint8_t *cls,
                           unsigned long long *shadow_sum, unsigned long long *shadow_cnt, const StencilParams &p,
                           hipStream_t s);
 
-// Canny hysteresis on the class map (in place): one launch = tile-local flood +
-// cross-tile propagation through changed tile borders.  dirty_in/out: per-tile flags
-// (n * tiles) ; *changed (device) set when any tile border changed.
-hipError_t launch_hysteresis(uint8_t *cls, int n, int h, int w, const uint8_t *dirty_in, uint8_t *dirty_out,
-                             int *changed, hipStream_t s);
-
-// dilate(edges(cls==2), 3x3) -> bit-packed mask: n x h x words_per_row u64, bit
-// (x & 63) of word x>>6 ; and optional u8 0/255 mask.
-hipError_t launch_dilate_pack(const uint8_t *cls, int n, int h, int w, uint64_t *bits, uint8_t *mask_u8,
-                              hipStream_t s);
+// Canny hysteresis as connected components + dilate(3x3) + bit-pack (hysteresis.hip).
+// Workspace: lab n*h*w u16; parent/sroot/roots over hysteresis_ids() entries; nroots
+// per tile.  bits: n x h x words_per_row u64 (bit x&63 of word x>>6), mask_u8 optional.
+struct HystWork {
+    uint16_t *lab;
+    int *parent;
+    uint8_t *sroot;
+    uint16_t *roots;
+    int *nroots;
+};
+size_t hysteresis_ids(int n, int h, int w);
+hipError_t launch_hysteresis_dilate(const uint8_t *cls, int n, int h, int w, const HystWork &wk, uint64_t *bits,
+                                    uint8_t *mask_u8, hipStream_t s);
 
 inline int words_per_row(int w) { return (w + 63) / 64; }
 inline int tiles_x(int w) { return (w + kTileW - 1) / kTileW; }

@@ -208,102 +208,6 @@ __global__ __launch_bounds__(NT) void k_stencil(const uint8_t *__restrict__ bgr,
 #undef BLUR
 }
 
-// ---------------------------------------------------------------- hysteresis
-// Tile-local 8-connected flood of "strong" (2) through "weak" (0) pixels inside a
-// 64x32 tile staged in LDS with a 1-pixel halo read from the neighbours' current
-// state.  A tile whose outer ring changes marks its 8 neighbours dirty for the next
-// launch; the host relaunches until no ring changes (monotone 0 -> 2 updates, so
-// concurrent halo reads are benign).
-constexpr int HW2 = TW + 2, HH2 = TH + 2;
-
-__global__ __launch_bounds__(NT) void k_hysteresis(uint8_t *__restrict__ cls, int H, int W, int ntx, int nty,
-                                                   const uint8_t *__restrict__ dirty_in, uint8_t *__restrict__ dirty_out,
-                                                   int *__restrict__ changed) {
-    __shared__ uint8_t tile[HH2][HW2];
-    __shared__ int s_flag;
-    const int tid = threadIdx.x;
-    const int img = blockIdx.y;
-    const int t = blockIdx.x;
-    const int ntiles = ntx * nty;
-    if (dirty_in && !dirty_in[(size_t)img * ntiles + t]) return;
-    const int tx0 = (t % ntx) * TW, ty0 = (t / ntx) * TH;
-    uint8_t *base = cls + (size_t)img * H * W;
-    bool any_weak = false, any_strong = false;
-    for (int i = tid; i < HH2 * HW2; i += NT) {
-        int ly = i / HW2, lx = i - ly * HW2;
-        int y = ty0 - 1 + ly, x = tx0 - 1 + lx;
-        uint8_t v = 1;
-        if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W) v = base[(size_t)y * W + x];
-        tile[ly][lx] = v;
-        bool inner = ly >= 1 && ly <= TH && lx >= 1 && lx <= TW;
-        any_weak |= inner && v == 0;
-        any_strong |= v == 2;
-    }
-    int has = __syncthreads_or(any_weak) && __syncthreads_or(any_strong);
-    if (!has) return;
-    // iterate until stable
-    bool ring_changed = false;
-    for (;;) {
-        bool ch = false;
-        for (int i = tid; i < TH * TW; i += NT) {
-            int ly = i / TW + 1, lx = (i % TW) + 1;
-            if (tile[ly][lx] != 0) continue;
-            bool s = tile[ly - 1][lx - 1] == 2 || tile[ly - 1][lx] == 2 || tile[ly - 1][lx + 1] == 2 ||
-                     tile[ly][lx - 1] == 2 || tile[ly][lx + 1] == 2 || tile[ly + 1][lx - 1] == 2 ||
-                     tile[ly + 1][lx] == 2 || tile[ly + 1][lx + 1] == 2;
-            if (s) {
-                tile[ly][lx] = 2;
-                ch = true;
-                int y = ty0 + ly - 1, x = tx0 + lx - 1;
-                base[(size_t)y * W + x] = 2;
-                if (ly == 1 || ly == TH || lx == 1 || lx == TW) ring_changed = true;
-            }
-        }
-        if (!__syncthreads_or(ch)) break;
-    }
-    if (threadIdx.x == 0) s_flag = 0;
-    __syncthreads();
-    if (ring_changed) s_flag = 1;
-    __syncthreads();
-    if (tid == 0 && s_flag) {
-        *changed = 1;
-        int txi = t % ntx, tyi = t / ntx;
-        for (int dy = -1; dy <= 1; dy++)
-            for (int dx = -1; dx <= 1; dx++) {
-                int nx = txi + dx, ny = tyi + dy;
-                if ((dx || dy) && nx >= 0 && nx < ntx && ny >= 0 && ny < nty)
-                    dirty_out[(size_t)img * ntiles + ny * ntx + nx] = 1;
-            }
-    }
-}
-
-// ---------------------------------------------------------------- dilate + pack
-// One wave per 64-pixel word: lane = pixel; dilated bit = any strong in 3x3.
-__global__ __launch_bounds__(NT) void k_dilate_pack(const uint8_t *__restrict__ cls, int H, int W, int wpr,
-                                                    uint64_t *__restrict__ bits, uint8_t *__restrict__ mask_u8,
-                                                    long long total_words) {
-    long long wave = ((long long)blockIdx.x * NT + threadIdx.x) >> 6;
-    int lane = threadIdx.x & 63;
-    if (wave >= total_words) return;
-    long long row = wave / wpr;  // global row over the batch
-    int wx = (int)(wave - row * wpr);
-    int img = (int)(row / H), y = (int)(row - (long long)img * H);
-    int x = wx * 64 + lane;
-    const uint8_t *base = cls + (size_t)img * H * W;
-    bool on = false;
-    if (x < W) {
-        int x0 = max(x - 1, 0), x1 = min(x + 1, W - 1);
-        int y0 = max(y - 1, 0), y1 = min(y + 1, H - 1);
-        for (int yy = y0; yy <= y1 && !on; yy++) {
-            const uint8_t *r = base + (size_t)yy * W;
-            on = (r[x0] == 2) | (r[x] == 2) | (r[x1] == 2);
-        }
-        if (mask_u8) mask_u8[((size_t)img * H + y) * W + x] = on ? 255 : 0;
-    }
-    unsigned long long b = __ballot(on);
-    if (lane == 0 && bits) bits[wave] = b;
-}
-
 }  // namespace
 
 hipError_t launch_stencil(const uint8_t *bgr, int n, int h, int w, uint8_t *cls, uint8_t *blurred,
@@ -312,23 +216,6 @@ hipError_t launch_stencil(const uint8_t *bgr, int n, int h, int w, uint8_t *cls,
     int ntx = tiles_x(w), nty = tiles_y(h);
     dim3 grid(ntx * nty, n);
     hipLaunchKernelGGL(k_stencil, grid, dim3(NT), 0, s, bgr, h, w, ntx, nty, cls, blurred, shadow_sum, shadow_cnt, p);
-    return hipGetLastError();
-}
-
-hipError_t launch_hysteresis(uint8_t *cls, int n, int h, int w, const uint8_t *dirty_in, uint8_t *dirty_out,
-                             int *changed, hipStream_t s) {
-    int ntx = tiles_x(w), nty = tiles_y(h);
-    dim3 grid(ntx * nty, n);
-    hipLaunchKernelGGL(k_hysteresis, grid, dim3(NT), 0, s, cls, h, w, ntx, nty, dirty_in, dirty_out, changed);
-    return hipGetLastError();
-}
-
-hipError_t launch_dilate_pack(const uint8_t *cls, int n, int h, int w, uint64_t *bits, uint8_t *mask_u8,
-                              hipStream_t s) {
-    int wpr = words_per_row(w);
-    long long total = (long long)n * h * wpr;
-    long long blocks = (total * 64 + NT - 1) / NT;
-    hipLaunchKernelGGL(k_dilate_pack, dim3((unsigned)blocks), dim3(NT), 0, s, cls, h, w, wpr, bits, mask_u8, total);
     return hipGetLastError();
 }
 
