@@ -98,20 +98,18 @@ def main():
 
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    from low_level_feature_extraction_amd import synth
+    from low_level_feature_extraction_amd import shard, synth
     from low_level_feature_extraction_amd.backend import Backend
 
     be = Backend.get(local)
     feats = tuple(f for f in args.features.split(",") if f)
     B, H, W = args.batch, args.height, args.width
-    base = rank * B
+    base, _ = shard.shard_bounds(B * world, rank, world)  # weak scaling: B images per rank
     imgs = synth.synth_batch(B, H, W, seed=args.seed, device=f"cuda:{local}", index_base=base)
     torch.cuda.synchronize()
 
     def barrier():
-        torch.cuda.synchronize()
-        if dist is not None:
-            dist.barrier()
+        shard.barrier(device=local)
 
     for w_ in range(args.warmup):
         be.process(imgs, feats, seed=args.seed + 1000 + w_, index_base=base)
@@ -125,11 +123,7 @@ def main():
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier()
-    dt = t1 - t0
-    if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    dt = shard.max_over_ranks(t1 - t0, device=f"cuda:{local}")
     stats = be.kernel_stats()
     be.set_profiling(False)
 

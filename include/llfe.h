@@ -71,7 +71,7 @@ typedef struct {
      * distribution. */
     const int8_t *noise;
     int32_t noise_on_device;
-    int32_t reserved;
+    int32_t n_colors;      /* extract_colors(n_colors=...) in [1, 5]; 0 -> 5 (the default) */
     int64_t index_base;    /* global index of image 0 (seeds are per global index) */
 } llfe_batch;
 
@@ -158,6 +158,19 @@ int llfe_kmeans(llfe_ctx *ctx, const uint32_t *keys, int64_t key_stride, const i
  * box may be NULL (whole image). src/dst device. */
 int llfe_resize_lanczos_pil(llfe_ctx *ctx, const uint8_t *src, int32_t h, int32_t w, int32_t ch, uint8_t *dst,
                             int32_t out_h, int32_t out_w, const double *box, llfe_stream stream);
+/* Pillow Image.reduce((fx, fy)) box averaging of a device u8 HWC image; dst holds
+ * ceil(h/fy) x ceil(w/fx) x ch bytes. */
+int llfe_reduce_pil(llfe_ctx *ctx, const uint8_t *src, int32_t h, int32_t w, int32_t ch, int32_t fx, int32_t fy,
+                    uint8_t *dst, llfe_stream stream);
+/* PIL Image.thumbnail size rule (preserve_aspect_ratio): returns 1 and the new size
+ * when a resize happens, 0 when (w, h) already fits (max_w, max_h). Host only. */
+int llfe_thumbnail_size(int32_t w, int32_t h, int32_t max_w, int32_t max_h, int32_t *out_w, int32_t *out_h);
+/* ImageProcessor.auto_process_image resize step (image_processor.py:221-224):
+ * thumbnail((max_w, max_h), LANCZOS) incl. reducing_gap=2.0's reduce() pre-pass, on a
+ * device u8 HWC image.  dst (device) needs out_h * out_w * ch <= dst_capacity bytes. */
+int llfe_thumbnail_pil(llfe_ctx *ctx, const uint8_t *src, int32_t h, int32_t w, int32_t ch, int32_t max_w,
+                       int32_t max_h, uint8_t *dst, int64_t dst_capacity, int32_t *out_h, int32_t *out_w,
+                       llfe_stream stream);
 /* host-side external contours (findContours RETR_EXTERNAL/CHAIN_APPROX_SIMPLE,
  * shape pyc @L140) on a host u8 mask; points x,y pairs; offsets[n_contours+1].
  * Returns the number of contours, or LLFE_ERR_CAPACITY with *needed_points set. */

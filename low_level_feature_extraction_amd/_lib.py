@@ -36,7 +36,7 @@ class LlfeBatch(C.Structure):
         ("on_device", C.c_int32),
         ("noise", C.c_void_p),
         ("noise_on_device", C.c_int32),
-        ("reserved", C.c_int32),
+        ("n_colors", C.c_int32),
         ("index_base", C.c_int64),
     ]
 
@@ -96,7 +96,11 @@ SIGNATURES = {
     "llfe_color_unique": (C.c_int, [_vp, C.POINTER(LlfeBatch), _u64, _vp, _vp, _vp]),
     "llfe_kmeans": (C.c_int, [_vp, _vp, _i64, _vp, _i32, _i32, _u64, _i64, _vp, _vp]),
     "llfe_resize_lanczos_pil": (C.c_int, [_vp, _vp, _i32, _i32, _i32, _vp, _i32, _i32, _vp, _vp]),
-    "llfe_find_contours": (C.c_int, [_vp, _i32, _i32, _vp, _i64, _vp, _i32, C.POINTER(C.c_int64)]),
+    "llfe_reduce_pil": (C.c_int, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp]),
+    "llfe_thumbnail_size": (C.c_int, [_i32, _i32, _i32, _i32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "llfe_thumbnail_pil": (C.c_int, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _i64, C.POINTER(C.c_int32),
+                                     C.POINTER(C.c_int32), _vp]),
+    "llfe_find_contours":(C.c_int, [_vp, _i32, _i32, _vp, _i64, _vp, _i32, C.POINTER(C.c_int64)]),
     "llfe_border_radius": (C.c_double, [_vp, _i32, C.c_double]),
     "llfe_classify_contour": (C.c_int, [_vp, _i32, C.POINTER(LlfeShape)]),
     "llfe_shapes_from_mask": (C.c_int, [_vp, _i32, _i32, _vp, _i32, C.POINTER(C.c_int32)]),

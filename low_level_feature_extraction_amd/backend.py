@@ -153,14 +153,14 @@ class Backend:
 
     # ------------------------------------------------------------------ hot path
     def process(self, images, features=("colors", "shapes", "shadows"), seed: int = 0, noise=None,
-                index_base: int = 0) -> list:
+                index_base: int = 0, n_colors: int = 5) -> list:
         """Run the batched hot path. ``images``: N x H x W x 3 BGR uint8 (numpy host
         array or torch tensor, host or GPU).  Returns a list of ImageFeatures."""
         ptr, n, h, w, on_dev, keep = self._batch_view(images)
         nptr, n_on_dev, nkeep = self._noise_view(noise, n, h, w)
         mask = feature_mask(features)
-        b = L.LlfeBatch(C.c_void_p(ptr), n, h, w, on_dev, C.c_void_p(nptr) if nptr else None, n_on_dev, 0,
-                        index_base)
+        b = L.LlfeBatch(C.c_void_p(ptr), n, h, w, on_dev, C.c_void_p(nptr) if nptr else None, n_on_dev,
+                        int(n_colors), index_base)
         results = (L.LlfeImageResult * max(n, 1))()
         cap = max(64 * n, 64)
         needed = C.c_int64(0)
@@ -287,6 +287,44 @@ class Backend:
         self._chk(self._lib.llfe_resize_lanczos_pil(self.ctx, x.data_ptr(), h, w, ch, out.data_ptr(), out_h, out_w,
                                                     bx, self._stream(x)))
         return out
+
+
+    def reduce_pil(self, image, fx, fy):
+        torch = _torch()
+        x = image if _is_torch(image) else torch.from_numpy(np.ascontiguousarray(image, np.uint8))
+        x = x.to(f"cuda:{self.device}").contiguous()
+        if x.dim() == 2:
+            x = x[:, :, None]
+        h, w, ch = x.shape
+        out = torch.empty(((h + fy - 1) // fy, (w + fx - 1) // fx, ch), dtype=torch.uint8, device=x.device)
+        self._chk(self._lib.llfe_reduce_pil(self.ctx, x.data_ptr(), h, w, ch, fx, fy, out.data_ptr(),
+                                            self._stream(x)))
+        return out
+
+    def thumbnail_pil(self, image, max_w=1920, max_h=1080):
+        """PIL thumbnail((max_w, max_h), LANCZOS) of one H x W x C uint8 image."""
+        torch = _torch()
+        x = image if _is_torch(image) else torch.from_numpy(np.ascontiguousarray(image, np.uint8))
+        x = x.to(f"cuda:{self.device}").contiguous()
+        squeeze = x.dim() == 2
+        if squeeze:
+            x = x[:, :, None]
+        h, w, ch = x.shape
+        out = torch.empty(h * w * ch, dtype=torch.uint8, device=x.device)
+        oh, ow = C.c_int32(0), C.c_int32(0)
+        self._chk(self._lib.llfe_thumbnail_pil(self.ctx, x.data_ptr(), h, w, ch, max_w, max_h, out.data_ptr(),
+                                               out.numel(), C.byref(oh), C.byref(ow), self._stream(x)))
+        out = out[: oh.value * ow.value * ch].view(oh.value, ow.value, ch)
+        return out[:, :, 0] if squeeze else out
+
+
+def thumbnail_size(w, h, max_w=1920, max_h=1080):
+    """-> (new_w, new_h) or None when PIL's thumbnail would not resize."""
+    ow, oh = C.c_int32(0), C.c_int32(0)
+    rc = L.lib().llfe_thumbnail_size(w, h, max_w, max_h, C.byref(ow), C.byref(oh))
+    if rc < 0:
+        raise L.LlfeError(rc, "invalid thumbnail geometry")
+    return (ow.value, oh.value) if rc == 1 else None
 
 
 # ---------------------------------------------------------------------- host-only geometry

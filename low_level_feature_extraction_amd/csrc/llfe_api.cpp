@@ -4,8 +4,8 @@
 //
 // Per chunk of images (all on the caller's stream):
 //   stencil (gray/blur5/Canny-NMS/adaptive mean)  -> class map + shadow sums
-//   hysteresis relaunches until no tile border changes
-//   dilate + bit-pack -> D2H (1 bit / pixel)
+//   hysteresis as connected components (4 launches) fused with dilate + bit-pack
+//   -> D2H (1 bit / pixel)
 //   colour bitmap -> compaction -> k-means (10 attempts / image) -> D2H 64 B / image
 //   host thread pool: external contours + shape geometry from the packed masks
 #include <hip/hip_runtime.h>
@@ -287,7 +287,7 @@ struct llfe_ctx {
     Profiler prof;
     StencilParams sp{};
     // device workspace
-    DevBuf<uint8_t> d_in, d_cls, d_rsz_tmp, d_sroot;
+    DevBuf<uint8_t> d_in, d_cls, d_rsz_tmp, d_rsz_src, d_sroot;
     DevBuf<int8_t> d_noise;
     DevBuf<uint64_t> d_bits, d_rng;
     DevBuf<unsigned long long> d_shadow;
@@ -489,6 +489,8 @@ int llfe_process_batch(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, ui
     if (!ctx || !b || !results) return LLFE_ERR_INVALID;
     if (!valid_dims(b->n, b->height, b->width) || (b->n > 0 && !b->data))
         return ctx->fail(LLFE_ERR_INVALID, "invalid batch n=%d h=%d w=%d", b->n, b->height, b->width);
+    if (b->n_colors < 0 || b->n_colors > kMaxK)
+        return ctx->fail(LLFE_ERR_UNSUPPORTED, "n_colors=%d outside [1, %d]", b->n_colors, kMaxK);
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t s = (hipStream_t)stream;
     const int h = b->height, w = b->width, wpr = words_per_row(w);
@@ -516,7 +518,8 @@ int llfe_process_batch(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, ui
         if (want_col) {
             rc = color_stage(ctx, img, noise, n, h, w, seed, b->index_base + i0, s);
             if (rc) return rc;
-            rc = kmeans_stage(ctx, ctx->d_keys.p, key_stride, ctx->d_nuniq.p, n, 5, seed, b->index_base + i0, s);
+            rc = kmeans_stage(ctx, ctx->d_keys.p, key_stride, ctx->d_nuniq.p, n, b->n_colors ? b->n_colors : kMaxK,
+                              seed, b->index_base + i0, s);
             if (rc) return rc;
             HIPCHK(ctx, ctx->h_kout.ensure(n));
             HIPCHK(ctx, hipMemcpyAsync(ctx->h_kout.p, ctx->d_kout.p, sizeof(KmeansImageOut) * n, hipMemcpyDeviceToHost, s));
@@ -704,6 +707,78 @@ int llfe_resize_lanczos_pil(llfe_ctx *ctx, const uint8_t *src, int32_t h, int32_
         HIPCHK(ctx, launch_resize_v(ctx->d_rsz_tmp.p, out_w, ch, dst, out_h, dbv, dkv, ksv, s));
     }
     HIPCHK(ctx, hipStreamSynchronize(s));  // host coefficient vectors die here
+    return LLFE_OK;
+}
+
+// PIL Image.thumbnail's preserve_aspect_ratio (Python float semantics).  Returns 1
+// and the new size when a resize happens, 0 when the image already fits.
+int llfe_thumbnail_size(int32_t w, int32_t h, int32_t max_w, int32_t max_h, int32_t *out_w, int32_t *out_h) {
+    if (w <= 0 || h <= 0 || max_w <= 0 || max_h <= 0 || !out_w || !out_h) return LLFE_ERR_INVALID;
+    *out_w = w;
+    *out_h = h;
+    int64_t x = max_w, y = max_h;
+    if (x >= w && y >= h) return 0;
+    const double aspect = (double)w / (double)h;
+    if ((double)x / (double)y >= aspect) {
+        double num = (double)y * aspect;
+        int64_t f = (int64_t)std::floor(num), c = (int64_t)std::ceil(num);
+        double kf = std::fabs(aspect - (double)f / (double)y), kc = std::fabs(aspect - (double)c / (double)y);
+        x = std::max<int64_t>(kc < kf ? c : f, 1);  // min(floor, ceil, key=...) keeps floor on ties
+    } else {
+        double num = (double)x / aspect;
+        int64_t f = (int64_t)std::floor(num), c = (int64_t)std::ceil(num);
+        auto key = [&](int64_t n) { return n == 0 ? 0.0 : std::fabs(aspect - (double)x / (double)n); };
+        y = std::max<int64_t>(key(c) < key(f) ? c : f, 1);
+    }
+    *out_w = (int32_t)x;
+    *out_h = (int32_t)y;
+    return (x != w || y != h) ? 1 : 0;
+}
+
+// ImageProcessor.auto_process_image's resize: PIL thumbnail((max_w, max_h), LANCZOS,
+// reducing_gap=2.0) on a device u8 HWC image (image_processor.py:221-224).  dst must hold
+// out_h * out_w * ch bytes (at most h * w * ch).
+int llfe_thumbnail_pil(llfe_ctx *ctx, const uint8_t *src, int32_t h, int32_t w, int32_t ch, int32_t max_w,
+                       int32_t max_h, uint8_t *dst, int64_t dst_capacity, int32_t *out_h, int32_t *out_w,
+                       llfe_stream stream) {
+    if (!ctx || !src || !dst || !out_h || !out_w || ch <= 0) return LLFE_ERR_INVALID;
+    int32_t ow, oh;
+    int rc = llfe_thumbnail_size(w, h, max_w, max_h, &ow, &oh);
+    if (rc < 0) return ctx->fail(rc, "invalid thumbnail geometry");
+    if ((int64_t)ow * oh * ch > dst_capacity) return ctx->fail(LLFE_ERR_CAPACITY, "thumbnail dst too small");
+    *out_w = ow;
+    *out_h = oh;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = (hipStream_t)stream;
+    if (rc == 0) {
+        HIPCHK(ctx, hipMemcpyAsync(dst, src, (size_t)h * w * ch, hipMemcpyDeviceToDevice, s));
+        HIPCHK(ctx, hipStreamSynchronize(s));
+        return LLFE_OK;
+    }
+    // Image.resize(size, LANCZOS, box=None, reducing_gap=2.0)
+    const double gap = 2.0;
+    int fx = (int)((double)w / ow / gap), fy = (int)((double)h / oh / gap);
+    if (fx < 1) fx = 1;
+    if (fy < 1) fy = 1;
+    if (fx > 1 || fy > 1) {
+        // _get_safe_box of the full image is the full image itself
+        const int rw = (w + fx - 1) / fx, rh = (h + fy - 1) / fy;
+        HIPCHK(ctx, ctx->d_rsz_src.ensure((size_t)rw * rh * ch));
+        HIPCHK(ctx, launch_reduce(src, w, ch, 0, 0, w, h, fx, fy, ctx->d_rsz_src.p, rw, rh, s));
+        const double box[4] = {0.0, 0.0, (double)w / fx, (double)h / fy};
+        return llfe_resize_lanczos_pil(ctx, ctx->d_rsz_src.p, rh, rw, ch, dst, oh, ow, box, stream);
+    }
+    return llfe_resize_lanczos_pil(ctx, src, h, w, ch, dst, oh, ow, nullptr, stream);
+}
+
+int llfe_reduce_pil(llfe_ctx *ctx, const uint8_t *src, int32_t h, int32_t w, int32_t ch, int32_t fx, int32_t fy,
+                    uint8_t *dst, llfe_stream stream) {
+    if (!ctx || !src || !dst || h <= 0 || w <= 0 || ch <= 0 || fx <= 0 || fy <= 0) return LLFE_ERR_INVALID;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = (hipStream_t)stream;
+    const int rw = (w + fx - 1) / fx, rh = (h + fy - 1) / fy;
+    HIPCHK(ctx, launch_reduce(src, w, ch, 0, 0, w, h, fx, fy, dst, rw, rh, s));
+    HIPCHK(ctx, hipStreamSynchronize(s));
     return LLFE_OK;
 }
 

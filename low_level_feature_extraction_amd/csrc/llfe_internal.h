@@ -85,5 +85,7 @@ hipError_t launch_resize_h(const uint8_t *src, int src_h, int src_w, int ch, int
                            int out_w, const int32_t *bounds, const int32_t *coeffs, int ksize, hipStream_t s);
 hipError_t launch_resize_v(const uint8_t *src, int src_w, int ch, uint8_t *dst, int out_h, const int32_t *bounds,
                            const int32_t *coeffs, int ksize, hipStream_t s);
+hipError_t launch_reduce(const uint8_t *src, int src_w, int ch, int x0, int y0, int x1, int y1, int fx, int fy,
+                         uint8_t *dst, int out_w, int out_h, hipStream_t s);
 
 }  // namespace llfe

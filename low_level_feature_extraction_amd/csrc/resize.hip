@@ -50,7 +50,34 @@ __global__ __launch_bounds__(RT) void k_resize_v(const uint8_t *__restrict__ src
     dst[(size_t)yy * rowlen + i] = clip8(ss);
 }
 
+// Pillow Image.reduce((fx, fy), box) (libImaging/Reduce.c): box mean with
+// out = ((sum + n/2) * floor(2^32 / (256 n))) >> 24, n = pixels in the (possibly
+// clipped) box; used by thumbnail(..., reducing_gap=2.0) when the input is >= 4x the
+// target in a dimension.
+__global__ __launch_bounds__(RT) void k_reduce(const uint8_t *__restrict__ src, int src_w, int ch, int x0, int y0,
+                                               int x1, int y1, int fx, int fy, uint8_t *__restrict__ dst, int out_w) {
+    const int yy = blockIdx.y;
+    const int i = blockIdx.x * RT + threadIdx.x;
+    if (i >= out_w * ch) return;
+    const int xx = i / ch, c = i - xx * ch;
+    const int ya = y0 + yy * fy, yb = min(y1, ya + fy);
+    const int xa = x0 + xx * fx, xb = min(x1, xa + fx);
+    const uint32_t n = (uint32_t)((yb - ya) * (xb - xa));
+    const uint32_t mult = (uint32_t)(4294967296.0f / (float)(256u * n));
+    uint32_t ss = n / 2;
+    for (int y = ya; y < yb; y++)
+        for (int x = xa; x < xb; x++) ss += src[((size_t)y * src_w + x) * ch + c];
+    dst[(size_t)yy * out_w * ch + i] = (uint8_t)((ss * mult) >> 24);
+}
+
 }  // namespace
+
+hipError_t launch_reduce(const uint8_t *src, int src_w, int ch, int x0, int y0, int x1, int y1, int fx, int fy,
+                         uint8_t *dst, int out_w, int out_h, hipStream_t s) {
+    dim3 grid((out_w * ch + RT - 1) / RT, out_h);
+    hipLaunchKernelGGL(k_reduce, grid, dim3(RT), 0, s, src, src_w, ch, x0, y0, x1, y1, fx, fy, dst, out_w);
+    return hipGetLastError();
+}
 
 hipError_t launch_resize_h(const uint8_t *src, int src_h, int src_w, int ch, int row0, int rows, uint8_t *dst,
                            int out_w, const int32_t *bounds, const int32_t *coeffs, int ksize, hipStream_t s) {

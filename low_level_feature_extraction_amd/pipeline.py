@@ -1,0 +1,96 @@
+"""Batched hot path with reference-shaped results.
+
+``run_batch(images, features)`` groups images by size, runs each group through
+``llfe_process_batch`` and assembles, per image, exactly what the reference's
+per-image calls return:
+
+* ``colors``  -> ColorFeatures      (ColorExtractor.extract_colors, color_extractor.py:204-300)
+* ``shapes``  -> {"shapes", "total_shapes", "metadata"}  (ShapeAnalyzer.analyze_shapes @L184-189)
+* ``shadows`` -> {"shadow_level": "Low" | "Moderate" | "High"}  (analyze_shadow_level
+  @L21-31; wrapped in a dict because UnifiedAnalysisResponse rejects a bare str)
+"""
+from __future__ import annotations
+
+from collections import defaultdict
+from typing import Iterable, List, Optional, Sequence
+
+import numpy as np
+
+from .backend import Backend, feature_mask  # noqa: F401  (feature_mask validates names)
+
+
+def shadow_level(mask_sum: int, mask_count: int) -> str:
+    """shadow pyc @L22-31: empty mask -> Low; avg_darkness = 255 - mean(shadow pixels)."""
+    if mask_count == 0:
+        return "Low"
+    avg_darkness = 255 - np.float64(mask_sum) / np.float64(mask_count)
+    if avg_darkness < 30:
+        return "Low"
+    if avg_darkness < 60:
+        return "Moderate"
+    return "High"
+
+
+def shapes_result(r) -> dict:
+    return {"shapes": list(r.shapes), "total_shapes": len(r.shapes),
+            "metadata": {"image_width": r.width, "image_height": r.height}}
+
+
+def assemble(r, features: Iterable[str]) -> dict:
+    from .color_extractor import ColorExtractor
+
+    out = {}
+    for f in features:
+        f = getattr(f, "value", f)
+        if f == "colors":
+            out["colors"] = ColorExtractor._palette(r.centers_rgb, r.counts)
+        elif f == "shapes":
+            out["shapes"] = shapes_result(r)
+        elif f == "shadows":
+            out["shadows"] = {"shadow_level": shadow_level(r.shadow_sum, r.shadow_count)}
+    return out
+
+
+def run_batch(images, features: Sequence[str] = ("colors", "shapes", "shadows"), seed: Optional[int] = None,
+              noise=None, backend: Optional[Backend] = None, raw: bool = False, n_colors: int = 5) -> List[dict]:
+    """images: N x H x W x 3 BGR uint8 array / torch tensor, or a list of H x W x 3
+    arrays of any sizes.  Returns one dict per image, in input order."""
+    from . import color_extractor as ce
+
+    be = backend or Backend.get()
+    feats = tuple(getattr(f, "value", f) for f in features)
+    feature_mask(feats)
+    if seed is None:
+        seed = ce._SEED
+    if isinstance(images, np.ndarray) and images.ndim == 4 or hasattr(images, "data_ptr"):
+        n = int(images.shape[0])
+        base = ce._next_index(n)
+        res = be.process(images, feats, seed=seed, noise=noise, index_base=base, n_colors=n_colors)
+        return res if raw else [assemble(r, feats) for r in res]
+    imgs = [np.ascontiguousarray(np.asarray(im, np.uint8)) for im in images]
+    for im in imgs:
+        if im.ndim != 3 or im.shape[2] != 3:
+            raise ValueError(f"expected H x W x 3 BGR uint8 images, got {im.shape}")
+    base = ce._next_index(len(imgs))
+    groups = defaultdict(list)
+    for i, im in enumerate(imgs):
+        groups[im.shape[:2]].append(i)
+    out: List[Optional[dict]] = [None] * len(imgs)
+    for (h, w), idx in groups.items():
+        batch = np.stack([imgs[i] for i in idx])
+        nz = None
+        if noise is not None:
+            nz = np.stack([np.asarray(noise[i], np.int8).reshape(h * w, 3) for i in idx])
+        # every image keeps its own global index, so results do not depend on grouping:
+        # one launch per run of consecutive indices
+        runs, start = [], 0
+        for j in range(1, len(idx) + 1):
+            if j == len(idx) or idx[j] != idx[j - 1] + 1:
+                runs.append((start, j))
+                start = j
+        for a, b in runs:
+            res = be.process(batch[a:b], feats, seed=seed, noise=None if nz is None else nz[a:b],
+                             index_base=base + idx[a], n_colors=n_colors)
+            for j, r in zip(range(a, b), res):
+                out[idx[j]] = r if raw else assemble(r, feats)
+    return out  # type: ignore[return-value]

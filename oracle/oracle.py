@@ -395,6 +395,35 @@ def pil_resize_lanczos(img, out_w, out_h, box=None):
     return out
 
 
+def pil_reduce(img, fx, fy):
+    img = np.ascontiguousarray(img, np.uint8)
+    if img.ndim == 2:
+        img = img[:, :, None]
+    h, w, ch = img.shape
+    out = np.empty(((h + fy - 1) // fy, (w + fx - 1) // fx, ch), np.uint8)
+    lib().orc_pil_reduce(_p(img), h, w, ch, fx, fy, _p(out))
+    return out
+
+
+def pil_thumbnail(img, max_w=1920, max_h=1080, reducing_gap=2.0):
+    """PIL Image.thumbnail((max_w, max_h), LANCZOS) restated: size rule, reduce()
+    pre-pass when the input is >= 2 * reducing_gap x the target, then resize with the
+    fractional box left by the reduction."""
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape[:2]
+    size = thumbnail_size(w, h, max_w, max_h)
+    if size is None:
+        return img
+    ow, oh = size
+    fx = int(w / ow / reducing_gap) or 1
+    fy = int(h / oh / reducing_gap) or 1
+    box = None
+    if fx > 1 or fy > 1:
+        img = pil_reduce(img, fx, fy)
+        box = (0.0, 0.0, w / fx, h / fy)
+    return pil_resize_lanczos(img, ow, oh, box)
+
+
 def preprocess_size(w, h, mode):
     """utils.py:118-143: (new_w, new_h, interpolation) or None when no resize."""
     limits = {"auto": (2000, "area"), "high_quality": (4000, "lanczos4"), "performance": (1000, "linear")}

@@ -1,0 +1,109 @@
+"""The C-ABI boundary (include/llfe.h): the library loads, exports every declared entry
+point, its struct layouts match the header, and the host-only entry points (geometry,
+thumbnail size rule) agree with the oracle.  No GPU compute here."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from low_level_feature_extraction_amd import _lib as L
+from low_level_feature_extraction_amd import backend as B
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "llfe.h")
+
+
+def _header_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(llfe_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_the_bound_symbols():
+    assert set(_header_functions()) == set(L.SIGNATURES)
+
+
+def test_library_exports_every_header_symbol():
+    lib = L.lib()
+    for name in _header_functions():
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", L.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    missing = set(_header_functions()) - exported
+    assert not missing, missing
+    # nothing but the C ABI is exported with C linkage under the llfe_ prefix
+    assert {s for s in exported if s.startswith("llfe_")} == set(_header_functions())
+
+
+def test_abi_version_and_struct_sizes():
+    assert L.lib().llfe_abi_version() == 1
+    assert C.sizeof(L.LlfeBatch) == 48
+    assert C.sizeof(L.LlfeImageResult) == 88
+    assert C.sizeof(L.LlfeShape) == 40
+    assert C.sizeof(L.LlfeKernelStat) == 56
+
+
+def test_struct_layout_matches_header_via_compiler(tmp_path):
+    """Compile a tiny C program against include/llfe.h and compare offsetof/sizeof."""
+    src = tmp_path / "lay.c"
+    fields = {
+        "llfe_batch": [f for f, _ in L.LlfeBatch._fields_],
+        "llfe_image_result": [f for f, _ in L.LlfeImageResult._fields_ if not f.endswith("_")],
+        "llfe_shape": [f for f, _ in L.LlfeShape._fields_ if not f.endswith("_")],
+        "llfe_kernel_stat": [f for f, _ in L.LlfeKernelStat._fields_],
+    }
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "llfe.h"', "int main(void){"]
+    for st, fs in fields.items():
+        lines.append(f'printf("{st} sizeof %zu\\n", sizeof({st}));')
+        for f in fs:
+            lines.append(f'printf("{st} {f} %zu\\n", offsetof({st}, {f}));')
+    lines.append("return 0;}")
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "lay"
+    subprocess.run(["gcc", "-std=c99", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = {}
+    for ln in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.splitlines():
+        st, f, v = ln.split()
+        got[(st, f)] = int(v)
+    pystructs = {"llfe_batch": L.LlfeBatch, "llfe_image_result": L.LlfeImageResult, "llfe_shape": L.LlfeShape,
+                 "llfe_kernel_stat": L.LlfeKernelStat}
+    for st, cls in pystructs.items():
+        assert got[(st, "sizeof")] == C.sizeof(cls), st
+        for f in fields[st]:
+            assert got[(st, f)] == getattr(cls, f).offset, (st, f)
+
+
+def test_init_without_gpu_fails_loudly():
+    """No CPU fallback: creating a context without a usable GPU is an error."""
+    try:
+        import torch
+
+        if torch.cuda.is_available():
+            pytest.skip("a GPU is present")
+    except ImportError:
+        pass
+    ctx = C.c_void_p()
+    rc = L.lib().llfe_init(0, C.byref(ctx))
+    assert rc < 0 and not ctx.value
+    with pytest.raises(L.LlfeError):
+        B.Backend(0)
+
+
+def test_invalid_arguments_rejected():
+    lib = L.lib()
+    ow, oh = C.c_int32(), C.c_int32()
+    assert lib.llfe_thumbnail_size(0, 10, 1920, 1080, C.byref(ow), C.byref(oh)) < 0
+    assert lib.llfe_thumbnail_size(10, 10, 0, 1080, C.byref(ow), C.byref(oh)) < 0
+    assert lib.llfe_find_contours(None, 4, 4, None, 0, None, 0, None) < 0
+    assert lib.llfe_classify_contour(None, 3, None) < 0
+
+
+@pytest.mark.parametrize("wh", [(3840, 2160), (2000, 1125), (3000, 2001), (1000, 4000), (1920, 1080), (7680, 4320),
+                                (5, 10000), (10000, 3), (1919, 1081), (1, 1), (1921, 1), (1, 1081), (4000, 4000),
+                                (2561, 1440), (1081, 1920)])
+def test_thumbnail_size_matches_oracle(orc, wh):
+    assert B.thumbnail_size(*wh) == orc.thumbnail_size(*wh)
+    assert B.thumbnail_size(*wh, max_w=40, max_h=20) == orc.thumbnail_size(*wh, 40, 20)

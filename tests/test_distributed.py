@@ -1,0 +1,81 @@
+"""N>1 path on CPU: world_size-2 gloo process groups exercising the sharding,
+timing reduction and result gather that bench.py and run_sharded use on RCCL."""
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+from low_level_feature_extraction_amd.shard import shard_bounds
+
+
+def test_shard_bounds_partition():
+    for n in range(0, 40):
+        for world in range(1, 9):
+            spans = [shard_bounds(n, r, world) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+            sizes = [b - a for a, b in spans]
+            assert max(sizes) - min(sizes) <= 1
+    with pytest.raises(ValueError):
+        shard_bounds(4, 2, 2)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, n_total, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from low_level_feature_extraction_amd import shard
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # stand-in per-image work: a record derived only from the global index, as the
+        # real pipeline's results are (seeds are per global image index)
+        def process(a, b):
+            return [{"index": i, "rank": rank, "value": (i * 2654435761) % 1000} for i in range(a, b)]
+
+        got = shard.run_sharded(n_total, process, gather_to=0)
+        local = shard.run_sharded(n_total, process, gather_to=None)
+        t = shard.max_over_ranks(1.5 if rank == 1 else 0.25)
+        shard.barrier()
+        q.put((rank, got, [r["index"] for r in local], t))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n_total", [7, 64])
+def test_gloo_world2_sharded_run(n_total):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, n_total, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(2):
+        rank, got, local, t = q.get(timeout=120)
+        out[rank] = (got, local, t)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    got0 = out[0][0]
+    assert out[1][0] is None
+    assert [r["index"] for r in got0] == list(range(n_total))
+    assert [r["value"] for r in got0] == [(i * 2654435761) % 1000 for i in range(n_total)]
+    a0, b0 = shard_bounds(n_total, 0, 2)
+    assert out[0][1] == list(range(a0, b0)) and out[1][1] == list(range(b0, n_total))
+    assert {r["rank"] for r in got0[:b0]} == {0} and {r["rank"] for r in got0[b0:]} == {1}
+    assert out[0][2] == out[1][2] == 1.5  # MAX over ranks
+
+
+def test_single_process_fallthrough():
+    from low_level_feature_extraction_amd import shard
+
+    assert shard.run_sharded(5, lambda a, b: list(range(a, b))) == [0, 1, 2, 3, 4]
+    assert shard.max_over_ranks(3.0) == 3.0
