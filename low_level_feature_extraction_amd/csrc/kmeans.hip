@@ -149,7 +149,9 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
     const int M = (N + STEP - 1) / STEP;         // steps
     const int Mw = (M + KW - 1) / KW;            // steps per wave
     const int sb = min(M, wid * Mw), se = min(M, sb + Mw);
-    const int se_full = min(se, N / STEP);       // steps whose 256 points are all valid
+    // steps whose 256 points are all valid end at se_full; [se_full, se) is at most the
+    // one partial step, and empty for waves whose range lies past it (sb == se == M)
+    const int se_full = max(sb, min(se, N / STEP));
     uint32_t *ss = scratch + ((size_t)img * kAttempts + att) * (size_t)scratch_stride;
 #define SSLOT(slot) (ss + (size_t)(slot) * (size_t)M)
 

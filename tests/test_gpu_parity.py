@@ -154,6 +154,7 @@ def test_kmeans_vs_oracle(backend, orc, h, w):
         comp, labels, centers, counts, iters = orc.kmeans(data, K, rng_state=orc.image_rng_state(seed, i))
         gc, gcount, gcomp = got[i]
         assert gc.shape == (K, 3)
+        assert int(gcount.sum()) == len(k)  # every unique colour labelled exactly once
         assert delta_e_matched(gc, centers.astype(np.uint8)) <= 2.5
         assert abs(gcomp - comp) <= 1e-3 * max(1.0, comp)
 
