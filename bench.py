@@ -29,6 +29,17 @@ sys.path.insert(0, ROOT)
 
 METRIC = "images/sec, 1080p batch, full colors+shapes+shadows pipeline @1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# HBM bytes per launch measured with rocprofv3 PMC counters (tools/profile.sh ->
+# profiles/traffic_latest.json); None when unmeasured.
+def _load_traffic():
+    try:
+        with open(os.path.join(ROOT, "profiles", "traffic_latest.json")) as f:
+            return {k: round(v["bytes"]) for k, v in json.load(f)["kernels"].items()}
+    except (OSError, KeyError, ValueError):
+        return {}
+
+
+TRAFFIC: dict = _load_traffic()
 
 
 def _cpu_worker(args):
@@ -133,34 +144,28 @@ def main():
         return
 
     total_images = B * world * args.steps
+    def roof(name):
+        """HBM roofline of one kernel: algorithmic bytes per launch
+        / its average hipEvent-timed launch duration."""
+        st = stats[name]
+        avg_ms = st["total_ms"] / max(st["launches"], 1)
+        bpl = st["bytes"] / max(st["launches"], 1)
+        achieved = bpl / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+        return {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": TRAFFIC.get(name),
+                "bytes_per_launch": bpl, "avg_launch_ms": round(avg_ms, 4)}
+
     kernels = {}
     for name, st in stats.items():
-        avg_ms = st["total_ms"] / max(st["launches"], 1)
-        kernels[name] = {
-            "launches": st["launches"],
-            "avg_ms": round(avg_ms, 4),
-            "share_of_step": round(st["total_ms"] / (dt * 1e3), 4),
-            "gbs": round(st["bytes"] / max(st["total_ms"], 1e-9) / 1e6, 1) if st["bytes"] else None,
-        }
-    # HBM roofline of the fused stencil front-end (the kernel the SURVEY's >=60 % HBM
-    # target is stated for): algorithmic bytes = 3P read + P class-map write per image.
-    rk = "k_stencil" if "k_stencil" in stats else max(stats, key=lambda k: stats[k]["total_ms"])
-    st = stats[rk]
-    avg_ms = st["total_ms"] / max(st["launches"], 1)
-    bytes_per_launch = st["bytes"] / max(st["launches"], 1)
-    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-    roofline = {
-        "kernel": rk,
-        "bound": "hbm",
-        "achieved": round(achieved, 1),
-        "peak": HBM_PEAK_GBS,
-        "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBS, 4),
-        "traffic": None,
-        "bytes_per_launch": bytes_per_launch,
-        "avg_launch_ms": round(avg_ms, 4),
-    }
+        r = roof(name)
+        kernels[name] = {"launches": st["launches"], "avg_ms": r["avg_launch_ms"],
+                         "share_of_step": round(st["total_ms"] / (dt * 1e3), 4),
+                         "gbs": r["achieved"] if st["bytes"] else None, "frac": r["frac"] if st["bytes"] else None}
+    # `roofline` is the dominant kernel's (largest total time); k_kmeans' algorithmic
+    # bytes are 4 U per full sweep over the unique-colour keys x the sweeps it made.
     dominant = max(stats, key=lambda k: stats[k]["total_ms"]) if stats else None
+    roofline = roof(dominant) if dominant else None
+    roofline_stencil = roof("k_stencil") if "k_stencil" in stats else None
 
     cpu = None
     if args.cpu_baseline == "auto" and world == 1:
@@ -191,6 +196,7 @@ def main():
             "parallelism": f"replicas x{world} (host-side shard, no collective)",
         },
         "roofline": roofline,
+        "roofline_stencil": roofline_stencil,
         "dominant_kernel": dominant,
         "kernels": kernels,
         "shapes_per_image": round(n_shapes / (B * args.steps), 2),

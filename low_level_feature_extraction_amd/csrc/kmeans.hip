@@ -640,6 +640,8 @@ __global__ void k_kmeans_finalize(const uint32_t *__restrict__ keys, long long k
             }
         }
         const KmeansAttemptOut &b = att[(size_t)img * kAttempts + best];
+        // PP init: 1 + (K - 1) sweeps; Lloyd: iters - 1; compactness: 1
+        for (int a = 0; a < kAttempts; a++) r.key_passes += K + att[(size_t)img * kAttempts + a].iters;
         r.k = K;
         r.compactness = bc;
         for (int k = 0; k < K; k++) {

@@ -261,6 +261,10 @@ struct Profiler {
         pending.clear();
         used = 0;
     }
+    // bytes known only after the launch completed (k-means sweeps)
+    void add_bytes(const char *name, double bytes) {
+        if (on) stats[kid(name)].bytes += bytes;
+    }
     void reset() {
         pending.clear();
         used = 0;
@@ -537,6 +541,11 @@ int llfe_process_batch(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, ui
                                        hipMemcpyDeviceToHost, s));
         HIPCHK(ctx, hipStreamSynchronize(s));
         ctx->prof.collect();
+        if (want_col && ctx->prof.on) {
+            double kb = 0;
+            for (int i = 0; i < n; i++) kb += 4.0 * (double)ctx->h_kout.p[i].n_unique * (double)ctx->h_kout.p[i].key_passes;
+            ctx->prof.add_bytes("k_kmeans", kb);
+        }
 
         for (int i = 0; i < n; i++) {
             llfe_image_result &r = results[i0 + i];

@@ -69,6 +69,7 @@ struct KmeansImageOut {
     uint8_t pad[1];
     int64_t n_unique;
     double compactness;
+    int64_t key_passes;  // full sweeps over the U keys, summed over the attempts (roofline bytes = 4 U passes)
 };
 
 // per image: K = min(n_colors, U); attempts run as separate workgroups
