@@ -30,6 +30,14 @@ constexpr int KW = KT / 64;       // waves
 constexpr int STEP = 256;         // points per wave step (64 lanes x 4)
 constexpr float kFar = 1e30f;     // coordinate of an unused centre: its distance is +inf
 
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    uint64_t z = x;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
 __device__ __forceinline__ uint32_t cvrng_next(uint64_t &s) {
     s = (uint64_t)(uint32_t)s * 4164903690ull + (uint32_t)(s >> 32);
     return (uint32_t)s;
@@ -78,6 +86,56 @@ __device__ __forceinline__ int label5(const P3 &p, const Cent &c, float &best) {
     return l;
 }
 
+// Same labels as label5, with the distances of centre pairs (0,1), (2,3), (4,far) in
+// packed FP32 (v_pk_add/mul/fma_f32: two IEEE lanes, bit-identical to the scalar ops)
+// and the arg-min as min-then-first-equal (= the first strict minimum of the scan).
+typedef float f2 __attribute__((ext_vector_type(2)));
+struct CentP {
+    f2 x[3], y[3], z[3];
+};
+
+__device__ __forceinline__ CentP pack_centres(const Cent &c) {
+    CentP r;
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        const int a = 2 * j, b = 2 * j + 1;
+        r.x[j] = f2{c.x[a], b < kMaxK ? c.x[b] : kFar};
+        r.y[j] = f2{c.y[a], b < kMaxK ? c.y[b] : kFar};
+        r.z[j] = f2{c.z[a], b < kMaxK ? c.z[b] : kFar};
+    }
+    return r;
+}
+
+__device__ __forceinline__ int label5p(uint32_t key, const CentP &c) {
+    const float x = (float)((key >> 16) & 255u), y = (float)((key >> 8) & 255u), z = (float)(key & 255u);
+    const f2 px = f2{x, x}, py = f2{y, y}, pz = f2{z, z};
+    f2 d[3];
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        const f2 t0 = px - c.x[j], t1 = py - c.y[j], t2 = pz - c.z[j];
+        f2 dd = t0 * t0;
+        dd = __builtin_elementwise_fma(t1, t1, dd);
+        dd = __builtin_elementwise_fma(t2, t2, dd);
+        d[j] = dd;
+    }
+    const float m = fminf(fminf(fminf(d[0].x, d[0].y), fminf(d[1].x, d[1].y)), d[2].x);
+    int l = 4;
+    l = d[1].y == m ? 3 : l;
+    l = d[1].x == m ? 2 : l;
+    l = d[0].y == m ? 1 : l;
+    l = d[0].x == m ? 0 : l;
+    return l;
+}
+
+constexpr int PF = 4;  // steps of 16-B key loads kept in flight per wave
+constexpr int FQ = 8;  // boundary cubes labelled per round of the pruned sweep
+
+// the 4 keys of lane `lane` in 256-point step `s` (zeros past the full steps)
+__device__ __forceinline__ uint4 load_step(const uint32_t *pts, int s, int se_full, int lane) {
+    if (s < se_full) return *(const uint4 *)(pts + (size_t)s * STEP + lane * 4);
+    return make_uint4(0u, 0u, 0u, 0u);
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll
@@ -106,6 +164,7 @@ struct KmSmem {
     unsigned long long found_excl[3];
     int ci[3];
     int flag;
+    unsigned long long fail_pts;  // keys read point by point in this Lloyd sweep
 };
 
 __device__ __forceinline__ Cent load_centres(const float (*c)[3]) {
@@ -127,9 +186,10 @@ __device__ __forceinline__ int moved_label(const KmSmem &sm, int i, int l) {
 
 __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys, long long key_stride,
                                                const long long *__restrict__ n_unique, int n_colors,
-                                               const uint64_t *__restrict__ rng_states, const int *__restrict__ order,
+                                               unsigned long long seed, long long index_base,
+                                               const int *__restrict__ order,
                                                uint32_t *__restrict__ scratch, long long scratch_stride,
-                                               KmeansAttemptOut *__restrict__ out) {
+                                               KmeansAttemptOut *__restrict__ out, const KmeansCubes cubes) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     KmSmem &sm = *reinterpret_cast<KmSmem *>(smem_raw);
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -138,10 +198,20 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
     const int N = (int)n_unique[img];
     const int K = min(n_colors, N);
     KmeansAttemptOut *o = out + (size_t)img * kAttempts + att;
+    if (tid == 0) {
+        unsigned hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        o->t_start = wall_clock64();
+        o->hw_id = hw;
+        o->xcc_id = xcc;
+    }
     if (K <= 1) {
         if (tid == 0) {
             o->compactness = 0.0;
             o->iters = 0;
+            o->bytes = 0;
+            o->t_end = wall_clock64();
         }
         return;
     }
@@ -153,9 +223,20 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
     // one partial step, and empty for waves whose range lies past it (sb == se == M)
     const int se_full = max(sb, min(se, N / STEP));
     uint32_t *ss = scratch + ((size_t)img * kAttempts + att) * (size_t)scratch_stride;
+    // cube-pruned Lloyd sweeps (when the cube table was built): waves own contiguous
+    // ranges of cubes
+    const bool use_cubes = cubes.ckeys != nullptr;
+    const int C = use_cubes ? cubes.n_cubes[img] : 0;
+    const CubeEnt *ctab = use_cubes ? cubes.cubes + (size_t)img * cubes.cube_stride : nullptr;
+    const uint32_t *ckp = use_cubes ? cubes.ckeys + (size_t)img * key_stride : nullptr;
+    const int Cw = (C + KW - 1) / KW;
+    const int cb = min(C, wid * Cw), cend = min(C, cb + Cw);
+    unsigned long long bytes = 4ull * (unsigned long long)N * (unsigned long long)(K + 1);  // PP + compactness
+    if (tid == 0) sm.fail_pts = 0;
 #define SSLOT(slot) (ss + (size_t)(slot) * (size_t)M)
 
-    uint64_t rng = rng_states[img];
+    uint64_t rng = splitmix64(seed + (unsigned long long)(index_base + img));
+    if (rng == 0) rng = 0xFFFFFFFFull;  // cv::RNG(0) takes the default state
     for (int q = 0, skip = att * (1 + 6 * (K - 1)); q < skip; q++) cvrng_next(rng);
 
     // ------------------------------------------------ k-means++ (generateCentersPP)
@@ -371,6 +452,7 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
         __syncthreads();
     }
 
+    if (tid == 0) o->t_pp = wall_clock64();
     // ------------------------------------------------ Lloyd iterations
     if (tid < kMaxK * 3) {
         int k = tid / 3, j = tid % 3;
@@ -381,26 +463,136 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
     int iter = 1;
     const double eps2 = 0.2 * 0.2;
     for (;;) {
-        const Cent c = load_centres(sm.c);
+        const CentP c = pack_centres(load_centres(sm.c));
 #pragma unroll
         for (int k = 0; k < kMaxK; k++) {
             sm.accA[k][tid] = 0;
             sm.accB[k][tid] = 0;
         }
         // (lane-private slots: no barrier needed between zeroing and accumulation)
-#pragma unroll 2
-        for (int s = sb; s < se_full; s++) {
-            uint4 v = *(const uint4 *)(pts + s * STEP + lane * 4);
-            uint32_t kq[4] = {v.x, v.y, v.z, v.w};
+        if (use_cubes) {
+            // Margin test per 4x4x4 cube, q = its centre, k = argmin d(q, c_k):
+            //   d_j(p) - d_k(p) is linear in p, so over the cube it is >= (d_j(q) - d_k(q))
+            //   - 3 L1(c_j - c_k); when the second-smallest gap at q exceeds
+            //   3 max_j L1(c_j - c_k) + 1, every colour of the cube is at least 1 closer
+            //   to c_k than to any other centre in exact arithmetic, far above the float
+            //   error of normL2Sqr (< 0.1 at these magnitudes): OpenCV labels it k.
+            const Cent cu = load_centres(sm.c);
+            float thr[kMaxK];
 #pragma unroll
-            for (int jj = 0; jj < 4; jj++) {
-                float bd;
-                int l = label5(unpack(kq[jj]), c, bd);
-                unsigned long long a = (unsigned long long)((kq[jj] >> 16) & 255u) |
-                                       ((unsigned long long)((kq[jj] >> 8) & 255u) << 32);
-                unsigned long long b = (unsigned long long)(kq[jj] & 255u) | (1ull << 32);
-                atomicAdd(&sm.accA[l][tid], a);
-                atomicAdd(&sm.accB[l][tid], b);
+            for (int k = 0; k < kMaxK; k++) {
+                float mx = 0.f;
+#pragma unroll
+                for (int j = 0; j < kMaxK; j++)
+                    if (j != k && j < K)
+                        mx = fmaxf(mx, fabsf(cu.x[j] - cu.x[k]) + fabsf(cu.y[j] - cu.y[k]) + fabsf(cu.z[j] - cu.z[k]));
+                thr[k] = 3.f * mx + 1.f;
+            }
+            unsigned long long fails = 0;
+            CubeEnt enext;
+            enext.offset = 0;
+            enext.id = 0;
+            enext.sums = 0;
+            if (cb + lane < cend) enext = ctab[cb + lane];
+            for (int base = cb; base < cend; base += 64) {
+                const int ci = base + lane;
+                const bool valid = ci < cend;
+                const CubeEnt e = enext;  // this batch's entry; the next batch's is loaded
+                if (ci + 64 < cend) enext = ctab[ci + 64];  // behind the labelling below
+                bool pass = false;
+                int k = 0;
+                if (valid) {
+                    const float qx = (float)(e.id >> 12) * 4.f + 1.5f, qy = (float)((e.id >> 6) & 63u) * 4.f + 1.5f,
+                                qz = (float)(e.id & 63u) * 4.f + 1.5f;
+                    const f2 px = f2{qx, qx}, py = f2{qy, qy}, pz = f2{qz, qz};
+                    f2 d[3];
+#pragma unroll
+                    for (int j = 0; j < 3; j++) {
+                        const f2 t0 = px - c.x[j], t1 = py - c.y[j], t2 = pz - c.z[j];
+                        f2 dd = t0 * t0;
+                        dd = __builtin_elementwise_fma(t1, t1, dd);
+                        dd = __builtin_elementwise_fma(t2, t2, dd);
+                        d[j] = dd;
+                    }
+                    const float dv[5] = {d[0].x, d[0].y, d[1].x, d[1].y, d[2].x};
+                    const float m1 = fminf(fminf(fminf(dv[0], dv[1]), fminf(dv[2], dv[3])), dv[4]);
+                    k = 4;
+                    k = dv[3] == m1 ? 3 : k;
+                    k = dv[2] == m1 ? 2 : k;
+                    k = dv[1] == m1 ? 1 : k;
+                    k = dv[0] == m1 ? 0 : k;
+                    float m2 = __builtin_inff(), t = thr[0];
+#pragma unroll
+                    for (int j = 0; j < 5; j++) {
+                        m2 = j == k ? m2 : fminf(m2, dv[j]);
+                        t = j == k ? thr[j] : t;
+                    }
+                    pass = m2 - m1 > t;
+                }
+                if (pass) {
+                    const unsigned long long s = e.sums;
+                    atomicAdd(&sm.accA[k][tid], (s & 0xFFFFull) | (((s >> 16) & 0xFFFFull) << 32));
+                    atomicAdd(&sm.accB[k][tid], ((s >> 32) & 0xFFFFull) | ((s >> 48) << 32));
+                }
+                // cubes straddling a boundary: one key per lane, FQ cubes per round so
+                // that FQ independent key loads are in flight (a cube at a time would
+                // serialise one memory latency per cube)
+                unsigned long long fm = __ballot(valid && !pass);
+                const uint32_t cnt_mine = (uint32_t)(e.sums >> 48);
+                while (fm) {
+                    uint32_t off[FQ], cnt[FQ], kq[FQ];
+#pragma unroll
+                    for (int u = 0; u < FQ; u++) {
+                        cnt[u] = 0;
+                        off[u] = 0;
+                        if (fm) {
+                            const int src = __builtin_ctzll(fm);
+                            fm &= fm - 1;
+                            off[u] = (uint32_t)__shfl((int)e.offset, src);
+                            cnt[u] = (uint32_t)__shfl((int)cnt_mine, src);
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < FQ; u++) kq[u] = (uint32_t)lane < cnt[u] ? ckp[off[u] + lane] : 0u;
+#pragma unroll
+                    for (int u = 0; u < FQ; u++) {
+                        if ((uint32_t)lane < cnt[u]) {
+                            const int l = label5p(kq[u], c);
+                            atomicAdd(&sm.accA[l][tid], (unsigned long long)((kq[u] >> 16) & 255u) |
+                                                            ((unsigned long long)((kq[u] >> 8) & 255u) << 32));
+                            atomicAdd(&sm.accB[l][tid], (unsigned long long)(kq[u] & 255u) | (1ull << 32));
+                        }
+                        fails += cnt[u];
+                    }
+                }
+            }
+            if (lane == 0 && fails) atomicAdd(&sm.fail_pts, fails);
+        } else {
+        // The sweep is load-latency bound: keep the next PF steps' 16-B loads in flight
+        // while the current PF steps are labelled.
+        {
+            uint4 cur[PF], nxt[PF];
+#pragma unroll
+            for (int d = 0; d < PF; d++) cur[d] = load_step(pts, sb + d, se_full, lane);
+            for (int s = sb; s < se_full; s += PF) {
+#pragma unroll
+                for (int d = 0; d < PF; d++) nxt[d] = load_step(pts, s + PF + d, se_full, lane);
+#pragma unroll
+                for (int d = 0; d < PF; d++) {
+                    if (s + d >= se_full) break;
+                    const uint32_t kq[4] = {cur[d].x, cur[d].y, cur[d].z, cur[d].w};
+#pragma unroll
+                    for (int jj = 0; jj < 4; jj++) {
+                        int l = label5p(kq[jj], c);
+                        unsigned long long a = (unsigned long long)((kq[jj] >> 16) & 255u) |
+                                               ((unsigned long long)((kq[jj] >> 8) & 255u) << 32);
+                        unsigned long long b = (unsigned long long)(kq[jj] & 255u) | (1ull << 32);
+                        atomicAdd(&sm.accA[l][tid], a);
+                        atomicAdd(&sm.accB[l][tid], b);
+                    }
+                }
+#pragma unroll
+                for (int d = 0; d < PF; d++) cur[d] = nxt[d];
             }
         }
         for (int s = se_full; s < se; s++) {  // at most one partial step
@@ -408,14 +600,22 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
             for (int jj = 0; jj < 4; jj++) {
                 if (i0 + jj >= N) break;
                 uint32_t kq = pts[i0 + jj];
-                float bd;
-                int l = label5(unpack(kq), c, bd);
+                int l = label5p(kq, c);
                 atomicAdd(&sm.accA[l][tid], (unsigned long long)((kq >> 16) & 255u) |
                                                 ((unsigned long long)((kq >> 8) & 255u) << 32));
                 atomicAdd(&sm.accB[l][tid], (unsigned long long)(kq & 255u) | (1ull << 32));
             }
         }
+        }  // point sweep
         __syncthreads();
+        if (tid == 0) {
+            if (use_cubes) {
+                bytes += 16ull * (unsigned long long)C + 4ull * sm.fail_pts;
+                sm.fail_pts = 0;
+            } else {
+                bytes += 4ull * (unsigned long long)N;
+            }
+        }
         // reduce 20 values (5 clusters x {x, y, z, count}) over 1024 lanes
         if (tid < 640) {
             const int v = tid >> 5, part = tid & 31;
@@ -531,6 +731,7 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
         if (sm.flag) break;
     }
 
+    if (tid == 0) o->t_lloyd = wall_clock64();
     // ------------------------------------------------ compactness with the last labels
     {
         const Cent cp = load_centres(sm.cprev);
@@ -564,6 +765,8 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
             for (int w = 0; w < KW; w++) compactness += sm.dred[w];
             o->compactness = compactness;
             o->iters = iter;
+            o->bytes = bytes;
+            o->t_end = wall_clock64();
             for (int k = 0; k < kMaxK; k++) {
                 for (int j = 0; j < 3; j++) o->centers[k][j] = k < K ? sm.c[k][j] : 0.f;
                 o->counts[k] = k < K ? sm.counts[k] : 0;
@@ -640,8 +843,7 @@ __global__ void k_kmeans_finalize(const uint32_t *__restrict__ keys, long long k
             }
         }
         const KmeansAttemptOut &b = att[(size_t)img * kAttempts + best];
-        // PP init: 1 + (K - 1) sweeps; Lloyd: iters - 1; compactness: 1
-        for (int a = 0; a < kAttempts; a++) r.key_passes += K + att[(size_t)img * kAttempts + a].iters;
+        for (int a = 0; a < kAttempts; a++) r.bytes += att[(size_t)img * kAttempts + a].bytes;
         r.k = K;
         r.compactness = bc;
         for (int k = 0; k < K; k++) {
@@ -652,11 +854,134 @@ __global__ void k_kmeans_finalize(const uint32_t *__restrict__ keys, long long k
     out[img] = r;
 }
 
+// ---------------------------------------------------------------- cube compaction
+// One 1024-thread workgroup per image walks the 64 red slabs R (rows r = 4R..4R+3):
+// the slab's 4 x 2048 bitmap words are staged in LDS (skipped when their occupancy is
+// empty); thread t owns cubes (G = t / 16, B = 4 (t % 16) .. + 3), gathers each cube's
+// 64-bit occupancy from 16 nibbles, and a block scan places cubes and keys in cube-id
+// order.  Bit i*16 + j*4 + bb of a cube mask = colour (4R+i, 4G+j, 4B+bb).
+constexpr int CT = 1024;
+
+__device__ __forceinline__ unsigned long long block_excl_scan_u64(unsigned long long v, unsigned long long *tmp,
+                                                                  unsigned long long *total) {
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    unsigned long long x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        unsigned long long y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) tmp[wid] = x;
+    __syncthreads();
+    if (wid == 0) {
+        unsigned long long s = lane < CT / 64 ? tmp[lane] : 0ull;
+#pragma unroll
+        for (int off = 1; off < CT / 64; off <<= 1) {
+            unsigned long long y = __shfl_up(s, off);
+            if (lane >= off) s += y;
+        }
+        if (lane < CT / 64) tmp[lane] = s;  // inclusive wave prefix
+    }
+    __syncthreads();
+    const unsigned long long r = (wid ? tmp[wid - 1] : 0ull) + x - v;
+    *total = tmp[CT / 64 - 1];
+    __syncthreads();
+    return r;
+}
+
+__global__ __launch_bounds__(CT) void k_cube_compact(const uint32_t *__restrict__ bitmap,
+                                                     const uint32_t *__restrict__ occ, uint32_t *__restrict__ ckeys,
+                                                     long long key_stride, CubeEnt *__restrict__ cubes,
+                                                     long long cube_stride, int *__restrict__ n_cubes) {
+    __shared__ __attribute__((aligned(16))) uint32_t W[4 * 2048];
+    __shared__ unsigned long long tmp[CT / 64];
+    const int img = blockIdx.x, t = threadIdx.x;
+    const uint32_t *bm = bitmap + (size_t)img * kBitmapWords;
+    const uint32_t *oc = occ + (size_t)img * kOccWords;
+    uint32_t *ck = ckeys + (size_t)img * key_stride;
+    CubeEnt *ce = cubes + (size_t)img * cube_stride;
+    const int G = t >> 4, B0 = (t & 15) * 4;
+    const int wsel = (G << 5) | ((t & 15) >> 1);  // word (j = 0) holding this thread's 4 cubes
+    const int sh0 = (t & 1) * 16;                  // nibble offset of cube B0 in that word
+    unsigned long long run = 0;                    // cubes << 32 | keys placed so far
+    for (int R = 0; R < 64; R++) {
+        // occupancy words of rows 4R..4R+3 are 16R .. 16R + 15
+        const uint32_t o = t < 16 ? oc[16 * R + t] : 0u;
+        if (!__syncthreads_or(o != 0u)) continue;
+        const uint4 *src = (const uint4 *)bm;
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const int idx = t + q * CT;  // uint4 index within the 4 x 512 staged
+            const int row = idx >> 9, within = idx & 511;
+            ((uint4 *)W)[idx] = src[((size_t)(4 * R + row) << 9) + within];
+        }
+        __syncthreads();
+        uint32_t w[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) w[i][j] = W[i * 2048 + wsel + (j << 3)];
+        unsigned long long mask[4];
+        unsigned long long mine = 0;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            unsigned long long m = 0;
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    m |= (unsigned long long)((w[i][j] >> (sh0 + 4 * c)) & 15u) << (i * 16 + j * 4);
+            mask[c] = m;
+            mine += m ? (1ull << 32) + (unsigned long long)__popcll(m) : 0ull;
+        }
+        unsigned long long total;
+        const unsigned long long pos = run + block_excl_scan_u64(mine, tmp, &total);
+        unsigned ci = (unsigned)(pos >> 32), pi = (unsigned)pos;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const unsigned long long m = mask[c];
+            if (!m) continue;
+            const int B = B0 + c;
+            const unsigned cnt = (unsigned)__popcll(m);
+            unsigned sr = 4u * R * cnt, sg = 4u * G * cnt, sb = 4u * B * cnt;
+#pragma unroll
+            for (int i = 1; i < 4; i++) sr += i * (unsigned)__popcll(m & (0xFFFFull << (16 * i)));
+#pragma unroll
+            for (int j = 1; j < 4; j++) sg += j * (unsigned)__popcll(m & (0x000F000F000F000Full << (4 * j)));
+#pragma unroll
+            for (int bb = 1; bb < 4; bb++) sb += bb * (unsigned)__popcll(m & (0x1111111111111111ull << bb));
+            CubeEnt e;
+            e.offset = pi;
+            e.id = ((unsigned)R << 12) | ((unsigned)G << 6) | (unsigned)B;
+            e.sums = (unsigned long long)sr | ((unsigned long long)sg << 16) | ((unsigned long long)sb << 32) |
+                     ((unsigned long long)cnt << 48);
+            ce[ci++] = e;
+            for (unsigned long long mm = m; mm; mm &= mm - 1) {
+                const int bit = __builtin_ctzll(mm);
+                const int i = bit >> 4, j = (bit >> 2) & 3, bb = bit & 3;
+                ck[pi++] = ((unsigned)(4 * R + i) << 16) | ((unsigned)(4 * G + j) << 8) | (unsigned)(4 * B + bb);
+            }
+        }
+        run += total;
+    }
+    if (t == 0) n_cubes[img] = (int)(run >> 32);
+}
+
 }  // namespace
 
+hipError_t launch_cube_compact(const uint32_t *bitmap, const uint32_t *occ, int n, uint32_t *ckeys,
+                               int64_t key_stride, CubeEnt *cubes, int64_t cube_stride, int32_t *n_cubes,
+                               hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_cube_compact, dim3(n), dim3(CT), 0, s, bitmap, occ, ckeys, (long long)key_stride, cubes,
+                       (long long)cube_stride, n_cubes);
+    return hipGetLastError();
+}
+
 hipError_t launch_kmeans(const uint32_t *keys, int64_t key_stride, const int64_t *n_unique, int n, int n_colors,
-                         const uint64_t *rng_states, int32_t *order, uint32_t *scratch, int64_t scratch_stride,
-                         KmeansAttemptOut *attempts, KmeansImageOut *out, hipStream_t s) {
+                         uint64_t seed, int64_t index_base, int32_t *order, uint32_t *scratch, int64_t scratch_stride,
+                         KmeansAttemptOut *attempts, KmeansImageOut *out, const KmeansCubes &cubes,
+                         hipStream_t s) {
     if (n > OMAX) return hipErrorInvalidValue;
     if (n == 0) return hipSuccess;
     static bool attr_set = false;
@@ -668,8 +993,8 @@ hipError_t launch_kmeans(const uint32_t *keys, int64_t key_stride, const int64_t
     }
     hipLaunchKernelGGL(k_kmeans_order, dim3(1), dim3(OT), 0, s, (const long long *)n_unique, n, order);
     hipLaunchKernelGGL(k_kmeans, dim3(n * kAttempts), dim3(KT), smem, s, keys, (long long)key_stride,
-                       (const long long *)n_unique, n_colors, rng_states, order, scratch, (long long)scratch_stride,
-                       attempts);
+                       (const long long *)n_unique, n_colors, (unsigned long long)seed, (long long)index_base, order,
+                       scratch, (long long)scratch_stride, attempts, cubes);
     hipLaunchKernelGGL(k_kmeans_finalize, dim3((n + 255) / 256), dim3(256), 0, s, keys, (long long)key_stride,
                        (const long long *)n_unique, n, n_colors, attempts, out);
     return hipGetLastError();

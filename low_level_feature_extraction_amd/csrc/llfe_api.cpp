@@ -51,7 +51,8 @@ class Pool {
     void parallel_for(int n, const std::function<void(int, int)> &f) {
         if (n <= 0) return;
         std::atomic<int> next{0};
-        std::atomic<int> done{0};
+        int done = 0;  // guarded by m_: the waiter checks it under the same lock, so a
+                       // completion can never slip between its check and its sleep
         int workers = std::min((int)th_.size(), n);
         auto job = [&](int wid) {
             for (int i; (i = next.fetch_add(1)) < n;) f(i, wid);
@@ -61,14 +62,15 @@ class Pool {
             for (int w = 0; w < workers; w++)
                 q_.push_back([&, w] {
                     job(w + 1);
-                    done.fetch_add(1);
+                    std::lock_guard<std::mutex> g2(m_);
+                    done++;
                     cv_done_.notify_all();
                 });
         }
         cv_.notify_all();
         job(0);
         std::unique_lock<std::mutex> lk(m_);
-        cv_done_.wait(lk, [&] { return done.load() == workers; });
+        cv_done_.wait(lk, [&] { return done == workers; });
     }
 
   private:
@@ -135,14 +137,6 @@ struct HostBuf {
     }
     ~HostBuf() { release(); }
 };
-
-uint64_t splitmix64(uint64_t x) {
-    x += 0x9E3779B97F4A7C15ull;
-    uint64_t z = x;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-}
 
 // CV_32F Gaussian kernel of getGaussianKernel(n, sigma<=0): bit-exact softdouble
 // construction (sigma = 0.15 n + 0.35, normalised, centre = 1/sum) cast to float.
@@ -293,20 +287,25 @@ struct llfe_ctx {
     // device workspace
     DevBuf<uint8_t> d_in, d_cls, d_rsz_tmp, d_rsz_src, d_sroot;
     DevBuf<int8_t> d_noise;
-    DevBuf<uint64_t> d_bits, d_rng;
+    DevBuf<uint64_t> d_bits;
     DevBuf<unsigned long long> d_shadow;
     DevBuf<int> d_order, d_parent, d_nroots;
     DevBuf<uint16_t> d_lab, d_roots;
-    DevBuf<uint32_t> d_bitmap, d_occ, d_keys, d_kscratch;
+    DevBuf<uint32_t> d_bitmap, d_occ, d_keys, d_kscratch, d_ckeys;
+    DevBuf<CubeEnt> d_cubes;
+    DevBuf<int32_t> d_ncubes;
     DevBuf<int64_t> d_nuniq;
     DevBuf<KmeansAttemptOut> d_att;
     DevBuf<KmeansImageOut> d_kout;
     DevBuf<int32_t> d_coef;
-    // pinned host staging
-    HostBuf<uint64_t> h_bits;
-    HostBuf<unsigned long long> h_shadow;
+    // pinned host staging; the per-chunk results are double-buffered so the host can
+    // trace chunk c's contours while the GPU runs chunk c + 1
+    HostBuf<uint64_t> h_bits_s[2];
+    HostBuf<unsigned long long> h_shadow_s[2];
+    HostBuf<KmeansImageOut> h_kout_s[2];
+    hipEvent_t chunk_done[2] = {nullptr, nullptr};
+    int chunk = 256;  // images per device pass (LLFE_CHUNK)
     HostBuf<KmeansImageOut> h_kout;
-    HostBuf<uint64_t> h_rng;
     HostBuf<int64_t> h_nuniq;
     // per-thread host scratch
     std::vector<std::vector<int8_t>> work;
@@ -342,8 +341,6 @@ struct llfe_ctx {
     } while (0)
 
 namespace {
-
-constexpr int kChunk = 256;  // images per device pass (bounds workspace: ~15 MB / 1080p image)
 
 int stage_input(llfe_ctx *ctx, const llfe_batch *b, int i0, int n, const uint8_t **d_img, const int8_t **d_noise,
                 hipStream_t s) {
@@ -393,29 +390,50 @@ int color_stage(llfe_ctx *ctx, const uint8_t *img, const int8_t *noise, int n, i
     HIPCHK(ctx, ctx->d_nuniq.ensure(n));
     TIMED(ctx, s, "k_color_bitmap", (double)n * P * (noise ? 6 : 3),
           launch_color_bitmap(img, noise, n, h, w, seed, index_base, ctx->d_bitmap.p, ctx->d_occ.p, s));
+    // cube-ordered keys + cube table for the pruned Lloyd sweeps (reads the bitmap
+    // before the compaction clears it)
+    const int64_t cube_stride = std::min<int64_t>(key_stride, kMaxCubes);
+    HIPCHK(ctx, ctx->d_ckeys.ensure((size_t)n * key_stride));
+    HIPCHK(ctx, ctx->d_cubes.ensure((size_t)n * cube_stride));
+    HIPCHK(ctx, ctx->d_ncubes.ensure(n));
+    TIMED(ctx, s, "k_cube_compact", (double)n * (4.0 * kBitmapWords),
+          launch_cube_compact(ctx->d_bitmap.p, ctx->d_occ.p, n, ctx->d_ckeys.p, key_stride, ctx->d_cubes.p,
+                              cube_stride, ctx->d_ncubes.p, s));
     TIMED(ctx, s, "k_color_compact", (double)n * (4.0 * kBitmapWords),
           launch_color_compact(ctx->d_bitmap.p, ctx->d_occ.p, n, ctx->d_keys.p, key_stride, ctx->d_nuniq.p, s));
     return LLFE_OK;
 }
 
 int kmeans_stage(llfe_ctx *ctx, const uint32_t *keys, int64_t key_stride, const int64_t *d_nuniq, int n,
-                 int n_colors, uint64_t seed, int64_t index_base, hipStream_t s) {
+                 int n_colors, uint64_t seed, int64_t index_base, const KmeansCubes &cubes, hipStream_t s) {
     if (n_colors < 1 || n_colors > kMaxK) return ctx->fail(LLFE_ERR_UNSUPPORTED, "n_colors must be in [1, 5]");
     const int64_t sstride = kmeans_scratch_stride(key_stride);
-    HIPCHK(ctx, ctx->d_rng.ensure(n));
-    HIPCHK(ctx, ctx->h_rng.ensure(n));
     HIPCHK(ctx, ctx->d_order.ensure(n));
     HIPCHK(ctx, ctx->d_kscratch.ensure((size_t)n * kAttempts * sstride));
     HIPCHK(ctx, ctx->d_att.ensure((size_t)n * kAttempts));
     HIPCHK(ctx, ctx->d_kout.ensure(n));
-    for (int i = 0; i < n; i++) {
-        uint64_t st = splitmix64(seed + (uint64_t)(index_base + i));
-        ctx->h_rng.p[i] = st ? st : 0xFFFFFFFFull;
-    }
-    HIPCHK(ctx, hipMemcpyAsync(ctx->d_rng.p, ctx->h_rng.p, sizeof(uint64_t) * n, hipMemcpyHostToDevice, s));
+    // per-image cv::RNG state = splitmix64(seed + global index) is derived on the device
     TIMED(ctx, s, "k_kmeans", 0,
-          launch_kmeans(keys, key_stride, d_nuniq, n, n_colors, ctx->d_rng.p, ctx->d_order.p, ctx->d_kscratch.p,
-                        sstride, ctx->d_att.p, ctx->d_kout.p, s));
+          launch_kmeans(keys, key_stride, d_nuniq, n, n_colors, seed, index_base, ctx->d_order.p, ctx->d_kscratch.p,
+                        sstride, ctx->d_att.p, ctx->d_kout.p, cubes, s));
+    if (const char *path = getenv("LLFE_KM_TRACE")) {  // debug: per-attempt timeline + U
+        std::vector<KmeansAttemptOut> att((size_t)n * kAttempts);
+        std::vector<int64_t> nu(n);
+        HIPCHK(ctx, hipMemcpyAsync(att.data(), ctx->d_att.p, sizeof(KmeansAttemptOut) * att.size(),
+                                   hipMemcpyDeviceToHost, s));
+        HIPCHK(ctx, hipMemcpyAsync(nu.data(), d_nuniq, sizeof(int64_t) * n, hipMemcpyDeviceToHost, s));
+        HIPCHK(ctx, hipStreamSynchronize(s));
+        if (FILE *f = fopen(path, "a")) {
+            for (int i = 0; i < n; i++)
+                for (int a = 0; a < kAttempts; a++) {
+                    const KmeansAttemptOut &o = att[(size_t)i * kAttempts + a];
+                    fprintf(f, "%d %d %lld %d %llu %llu %u %u %llu %llu %llu\n", i, a, (long long)nu[i], o.iters,
+                            (unsigned long long)o.t_start, (unsigned long long)o.t_end, o.hw_id, o.xcc_id,
+                            (unsigned long long)o.t_pp, (unsigned long long)o.t_lloyd, (unsigned long long)o.bytes);
+                }
+            fclose(f);
+        }
+    }
     return LLFE_OK;
 }
 
@@ -430,6 +448,102 @@ void fill_color_result(const KmeansImageOut &k, llfe_image_result &r) {
 }
 
 bool valid_dims(int n, int h, int w) { return n >= 0 && h > 0 && w > 0 && (int64_t)h * w < (1LL << 31); }
+
+// Device half of one chunk: every kernel, then the D2H of the per-image results into
+// host slot `slot`, then an event the host half waits on.
+int enqueue_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_t seed, int i0, int n, int slot,
+                  hipStream_t s) {
+    const int h = b->height, w = b->width, wpr = words_per_row(w);
+    const bool want_col = features & LLFE_FEATURE_COLORS, want_shp = features & LLFE_FEATURE_SHAPES,
+               want_shd = features & LLFE_FEATURE_SHADOWS;
+    const int64_t P = (int64_t)h * w;
+    const int64_t key_stride = (std::max<int64_t>(P, 1) + 3) & ~int64_t(3);
+    const uint8_t *img;
+    const int8_t *noise;
+    int rc = stage_input(ctx, b, i0, n, &img, &noise, s);
+    if (rc) return rc;
+    if (want_shp || want_shd) {
+        HIPCHK(ctx, ctx->d_shadow.ensure(2 * (size_t)n));
+        if (want_shp) HIPCHK(ctx, ctx->d_cls.ensure((size_t)n * P));
+        if (want_shd) HIPCHK(ctx, hipMemsetAsync(ctx->d_shadow.p, 0, sizeof(unsigned long long) * 2 * n, s));
+        TIMED(ctx, s, "k_stencil", (double)n * P * (3 + (want_shp ? 1 : 0)),
+              launch_stencil(img, n, h, w, want_shp ? ctx->d_cls.p : nullptr, nullptr,
+                             want_shd ? ctx->d_shadow.p : nullptr, want_shd ? ctx->d_shadow.p + n : nullptr, ctx->sp,
+                             s));
+    }
+    if (want_col) {
+        rc = color_stage(ctx, img, noise, n, h, w, seed, b->index_base + i0, s);
+        if (rc) return rc;
+        const KmeansCubes cubes{ctx->d_ckeys.p, ctx->d_cubes.p, std::min<int64_t>(key_stride, kMaxCubes),
+                                ctx->d_ncubes.p};
+        rc = kmeans_stage(ctx, ctx->d_keys.p, key_stride, ctx->d_nuniq.p, n, b->n_colors ? b->n_colors : kMaxK, seed,
+                          b->index_base + i0, cubes, s);
+        if (rc) return rc;
+        HIPCHK(ctx, ctx->h_kout_s[slot].ensure(n));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->h_kout_s[slot].p, ctx->d_kout.p, sizeof(KmeansImageOut) * n,
+                                   hipMemcpyDeviceToHost, s));
+    }
+    if (want_shp) {
+        HIPCHK(ctx, ctx->d_bits.ensure((size_t)n * h * wpr));
+        HIPCHK(ctx, ctx->h_bits_s[slot].ensure((size_t)n * h * wpr));
+        rc = run_hysteresis_dilate(ctx, n, h, w, ctx->d_bits.p, nullptr, s);
+        if (rc) return rc;
+        HIPCHK(ctx, hipMemcpyAsync(ctx->h_bits_s[slot].p, ctx->d_bits.p, sizeof(uint64_t) * n * h * wpr,
+                                   hipMemcpyDeviceToHost, s));
+    }
+    if (want_shd) {
+        HIPCHK(ctx, ctx->h_shadow_s[slot].ensure(2 * (size_t)n));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->h_shadow_s[slot].p, ctx->d_shadow.p, sizeof(unsigned long long) * 2 * n,
+                                   hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(ctx, hipEventRecord(ctx->chunk_done[slot], s));
+    return LLFE_OK;
+}
+
+// Host half of one chunk: wait for its slot, fill the result records, trace contours.
+int finish_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, int i0, int n, int slot,
+                 llfe_image_result *results, llfe_shape *shapes, int64_t shape_capacity, int64_t &total_shapes) {
+    const int h = b->height, w = b->width, wpr = words_per_row(w);
+    const bool want_col = features & LLFE_FEATURE_COLORS, want_shp = features & LLFE_FEATURE_SHAPES,
+               want_shd = features & LLFE_FEATURE_SHADOWS;
+    HIPCHK(ctx, hipEventSynchronize(ctx->chunk_done[slot]));
+    const KmeansImageOut *ko = ctx->h_kout_s[slot].p;
+    const unsigned long long *sh = ctx->h_shadow_s[slot].p;
+    if (want_col && ctx->prof.on) {
+        double kb = 0;
+        for (int i = 0; i < n; i++) kb += (double)ko[i].bytes;
+        ctx->prof.add_bytes("k_kmeans", kb);
+    }
+    for (int i = 0; i < n; i++) {
+        llfe_image_result &r = results[i0 + i];
+        std::memset(&r, 0, sizeof r);
+        if (want_col) fill_color_result(ko[i], r);
+        if (want_shd) {
+            r.shadow_sum = sh[i];
+            r.shadow_count = sh[n + i];
+        }
+    }
+    if (want_shp) {
+        ctx->img_shapes.resize(n);
+        ctx->img_ncont.assign(n, 0);
+        const uint64_t *hb = ctx->h_bits_s[slot].p;
+        ctx->pool->parallel_for(n, [&](int i, int wid) {
+            external_contours_bits(hb + (size_t)i * h * wpr, h, w, wpr, ctx->work[wid], ctx->cont[wid]);
+            ctx->img_ncont[i] = shapes_from_contours(ctx->cont[wid], ctx->shs[wid], ctx->img_shapes[i]);
+        });
+        for (int i = 0; i < n; i++) {
+            llfe_image_result &r = results[i0 + i];
+            r.shape_offset = total_shapes;
+            r.n_shapes = (int32_t)ctx->img_shapes[i].size();
+            r.n_contours = ctx->img_ncont[i];
+            for (size_t k = 0; k < ctx->img_shapes[i].size(); k++) {
+                if (shapes && total_shapes + (int64_t)k < shape_capacity) shapes[total_shapes + k] = ctx->img_shapes[i][k];
+            }
+            total_shapes += r.n_shapes;
+        }
+    }
+    return LLFE_OK;
+}
 
 }  // namespace
 
@@ -446,6 +560,12 @@ int llfe_init(int device, llfe_ctx **out) {
     if (hipSetDevice(device) != hipSuccess) return LLFE_ERR_HIP;
     llfe_ctx *c = new llfe_ctx();
     c->device = device;
+    for (auto &e : c->chunk_done)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+            delete c;
+            return LLFE_ERR_HIP;
+        }
+    if (const char *ch = getenv("LLFE_CHUNK"); ch && atoi(ch) > 0) c->chunk = std::min(atoi(ch), kMaxKmeansBatch);
     gauss_kernel_f32(11, c->sp.k11);
     c->pool = new Pool(default_threads() - 1);
     int nt = c->pool->size() + 1;
@@ -459,6 +579,8 @@ int llfe_init(int device, llfe_ctx **out) {
 int llfe_destroy(llfe_ctx *ctx) {
     if (!ctx) return LLFE_OK;
     (void)hipSetDevice(ctx->device);
+    for (auto e : ctx->chunk_done)
+        if (e) (void)hipEventDestroy(e);
     delete ctx->pool;
     delete ctx;  // DevBuf / HostBuf members free themselves
     return LLFE_OK;
@@ -497,86 +619,28 @@ int llfe_process_batch(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, ui
         return ctx->fail(LLFE_ERR_UNSUPPORTED, "n_colors=%d outside [1, %d]", b->n_colors, kMaxK);
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t s = (hipStream_t)stream;
-    const int h = b->height, w = b->width, wpr = words_per_row(w);
-    const bool want_col = features & LLFE_FEATURE_COLORS, want_shp = features & LLFE_FEATURE_SHAPES,
-               want_shd = features & LLFE_FEATURE_SHADOWS;
-    const int64_t P = (int64_t)h * w;
-    const int64_t key_stride = (std::max<int64_t>(P, 1) + 3) & ~int64_t(3);
+    const bool want_shp = features & LLFE_FEATURE_SHAPES;
     int64_t total_shapes = 0;
-    for (int i0 = 0; i0 < b->n; i0 += kChunk) {
-        const int n = std::min(kChunk, b->n - i0);
-        const uint8_t *img;
-        const int8_t *noise;
-        int rc = stage_input(ctx, b, i0, n, &img, &noise, s);
+    // two-slot software pipeline: enqueue chunk c (kernels + D2H into slot c & 1), then
+    // finish chunk c - 1 on the host (contours, result records) while the GPU runs c
+    int prev_i0 = -1, prev_n = 0, slot = 0;
+    for (int i0 = 0; i0 < b->n; i0 += ctx->chunk) {
+        const int n = std::min(ctx->chunk, b->n - i0);
+        int rc = enqueue_chunk(ctx, b, features, seed, i0, n, slot, s);
         if (rc) return rc;
-        if (want_shp || want_shd) {
-            HIPCHK(ctx, ctx->d_shadow.ensure(2 * (size_t)n));
-            HIPCHK(ctx, ctx->h_shadow.ensure(2 * (size_t)n));
-            if (want_shp) HIPCHK(ctx, ctx->d_cls.ensure((size_t)n * P));
-            if (want_shd) HIPCHK(ctx, hipMemsetAsync(ctx->d_shadow.p, 0, sizeof(unsigned long long) * 2 * n, s));
-            TIMED(ctx, s, "k_stencil", (double)n * P * (3 + (want_shp ? 1 : 0)),
-                  launch_stencil(img, n, h, w, want_shp ? ctx->d_cls.p : nullptr, nullptr,
-                                 want_shd ? ctx->d_shadow.p : nullptr, want_shd ? ctx->d_shadow.p + n : nullptr,
-                                 ctx->sp, s));
-        }
-        if (want_col) {
-            rc = color_stage(ctx, img, noise, n, h, w, seed, b->index_base + i0, s);
+        if (prev_i0 >= 0) {
+            rc = finish_chunk(ctx, b, features, prev_i0, prev_n, slot ^ 1, results, shapes, shape_capacity, total_shapes);
             if (rc) return rc;
-            rc = kmeans_stage(ctx, ctx->d_keys.p, key_stride, ctx->d_nuniq.p, n, b->n_colors ? b->n_colors : kMaxK,
-                              seed, b->index_base + i0, s);
-            if (rc) return rc;
-            HIPCHK(ctx, ctx->h_kout.ensure(n));
-            HIPCHK(ctx, hipMemcpyAsync(ctx->h_kout.p, ctx->d_kout.p, sizeof(KmeansImageOut) * n, hipMemcpyDeviceToHost, s));
         }
-        if (want_shp) {
-            HIPCHK(ctx, ctx->d_bits.ensure((size_t)n * h * wpr));
-            HIPCHK(ctx, ctx->h_bits.ensure((size_t)n * h * wpr));
-            rc = run_hysteresis_dilate(ctx, n, h, w, ctx->d_bits.p, nullptr, s);
-            if (rc) return rc;
-            HIPCHK(ctx, hipMemcpyAsync(ctx->h_bits.p, ctx->d_bits.p, sizeof(uint64_t) * n * h * wpr,
-                                       hipMemcpyDeviceToHost, s));
-        }
-        if (want_shd)
-            HIPCHK(ctx, hipMemcpyAsync(ctx->h_shadow.p, ctx->d_shadow.p, sizeof(unsigned long long) * 2 * n,
-                                       hipMemcpyDeviceToHost, s));
-        HIPCHK(ctx, hipStreamSynchronize(s));
-        ctx->prof.collect();
-        if (want_col && ctx->prof.on) {
-            double kb = 0;
-            for (int i = 0; i < n; i++) kb += 4.0 * (double)ctx->h_kout.p[i].n_unique * (double)ctx->h_kout.p[i].key_passes;
-            ctx->prof.add_bytes("k_kmeans", kb);
-        }
-
-        for (int i = 0; i < n; i++) {
-            llfe_image_result &r = results[i0 + i];
-            std::memset(&r, 0, sizeof r);
-            if (want_col) fill_color_result(ctx->h_kout.p[i], r);
-            if (want_shd) {
-                r.shadow_sum = ctx->h_shadow.p[i];
-                r.shadow_count = ctx->h_shadow.p[n + i];
-            }
-        }
-        if (want_shp) {
-            ctx->img_shapes.resize(n);
-            ctx->img_ncont.assign(n, 0);
-            const uint64_t *hb = ctx->h_bits.p;
-            ctx->pool->parallel_for(n, [&](int i, int wid) {
-                external_contours_bits(hb + (size_t)i * h * wpr, h, w, wpr, ctx->work[wid], ctx->cont[wid]);
-                ctx->img_ncont[i] = shapes_from_contours(ctx->cont[wid], ctx->shs[wid], ctx->img_shapes[i]);
-            });
-            for (int i = 0; i < n; i++) {
-                llfe_image_result &r = results[i0 + i];
-                r.shape_offset = total_shapes;
-                r.n_shapes = (int32_t)ctx->img_shapes[i].size();
-                r.n_contours = ctx->img_ncont[i];
-                for (size_t k = 0; k < ctx->img_shapes[i].size(); k++) {
-                    if (shapes && total_shapes + (int64_t)k < shape_capacity)
-                        shapes[total_shapes + k] = ctx->img_shapes[i][k];
-                }
-                total_shapes += r.n_shapes;
-            }
-        }
+        prev_i0 = i0;
+        prev_n = n;
+        slot ^= 1;
     }
+    if (prev_i0 >= 0) {
+        int rc = finish_chunk(ctx, b, features, prev_i0, prev_n, slot ^ 1, results, shapes, shape_capacity, total_shapes);
+        if (rc) return rc;
+    }
+    ctx->prof.collect();
     if (shapes_needed) *shapes_needed = total_shapes;
     if (want_shp && total_shapes > shape_capacity)
         return ctx->fail(LLFE_ERR_CAPACITY, "shape capacity %lld < %lld", (long long)shape_capacity,
@@ -633,7 +697,8 @@ int llfe_shadow_stats(llfe_ctx *ctx, const uint8_t *bgr, uint64_t *sums, uint64_
 int llfe_color_unique(llfe_ctx *ctx, const llfe_batch *b, uint64_t seed, uint32_t *keys, int64_t *n_unique,
                       llfe_stream stream) {
     if (!ctx || !b || !keys || !n_unique || !valid_dims(b->n, b->height, b->width)) return LLFE_ERR_INVALID;
-    if (b->n > kChunk) return ctx->fail(LLFE_ERR_UNSUPPORTED, "llfe_color_unique: n > %d", kChunk);
+    constexpr int kMaxUniqueBatch = 1024;  // 2 MiB of bitmap per image
+    if (b->n > kMaxUniqueBatch) return ctx->fail(LLFE_ERR_UNSUPPORTED, "llfe_color_unique: n > %d", kMaxUniqueBatch);
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t s = (hipStream_t)stream;
     const int h = b->height, w = b->width, n = b->n;
@@ -666,7 +731,8 @@ int llfe_kmeans(llfe_ctx *ctx, const uint32_t *keys, int64_t key_stride, const i
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(ctx, ctx->d_nuniq.ensure(n));
     HIPCHK(ctx, hipMemcpyAsync(ctx->d_nuniq.p, n_points, sizeof(int64_t) * n, hipMemcpyHostToDevice, s));
-    int rc = kmeans_stage(ctx, keys, key_stride, ctx->d_nuniq.p, n, n_colors, seed, index_base, s);
+    const KmeansCubes none{nullptr, nullptr, 0, nullptr};  // plain sweeps over caller-supplied keys
+    int rc = kmeans_stage(ctx, keys, key_stride, ctx->d_nuniq.p, n, n_colors, seed, index_base, none, s);
     if (rc) return rc;
     HIPCHK(ctx, ctx->h_kout.ensure(n));
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_kout.p, ctx->d_kout.p, sizeof(KmeansImageOut) * n, hipMemcpyDeviceToHost, s));

@@ -60,6 +60,10 @@ struct KmeansAttemptOut {
     int32_t counts[kMaxK];
     int32_t iters;
     int32_t pad;
+    uint64_t bytes;  // algorithmic bytes this attempt read (keys, cube table)
+    // workgroup timeline (s_memrealtime, 100 MHz) and placement, for LLFE_KM_TRACE
+    uint64_t t_start, t_pp, t_lloyd, t_end;  // start, k-means++ done, Lloyd done, end
+    uint32_t hw_id, xcc_id;
 };
 
 struct KmeansImageOut {
@@ -69,14 +73,38 @@ struct KmeansImageOut {
     uint8_t pad[1];
     int64_t n_unique;
     double compactness;
-    int64_t key_passes;  // full sweeps over the U keys, summed over the attempts (roofline bytes = 4 U passes)
+    uint64_t bytes;  // algorithmic bytes read, summed over the attempts (roofline)
 };
+
+// Lloyd pruning by 4x4x4 colour cubes: the unique keys regrouped cube by cube, with a
+// per-cube entry holding where its keys start and their exact coordinate sums.
+// A cube whose whole box provably has one label (margin test) is accumulated from its
+// sums; the others are labelled point by point -- the labels are OpenCV's either way.
+struct CubeEnt {
+    uint32_t offset;  // first key of the cube in the cube-ordered key array
+    uint32_t id;      // R << 12 | G << 6 | B (cube = [4R, 4R+3] x [4G, 4G+3] x [4B, 4B+3])
+    uint64_t sums;    // sum r | sum g << 16 | sum b << 32 | count << 48
+};
+constexpr int kMaxCubes = 1 << 18;
+struct KmeansCubes {
+    const uint32_t *ckeys;  // per image (key_stride): keys in cube order (nullptr: no pruning)
+    const CubeEnt *cubes;   // per image (cube_stride) entries in cube-id order
+    int64_t cube_stride;
+    const int32_t *n_cubes;
+};
+// bitmap -> cube-ordered keys + cube table (run before launch_color_compact, which
+// clears the bitmap)
+hipError_t launch_cube_compact(const uint32_t *bitmap, const uint32_t *occ, int n, uint32_t *ckeys,
+                               int64_t key_stride, CubeEnt *cubes, int64_t cube_stride, int32_t *n_cubes,
+                               hipStream_t s);
 
 // per image: K = min(n_colors, U); attempts run as separate workgroups
 // (ordered largest U first), then a finalize kernel picks the best attempt.
+// cv::RNG state of image i = splitmix64(seed + index_base + i), 0 -> 0xffffffff
 hipError_t launch_kmeans(const uint32_t *keys, int64_t key_stride, const int64_t *n_unique, int n, int n_colors,
-                         const uint64_t *rng_states, int32_t *order, uint32_t *scratch, int64_t scratch_stride,
-                         KmeansAttemptOut *attempts, KmeansImageOut *out, hipStream_t s);
+                         uint64_t seed, int64_t index_base, int32_t *order, uint32_t *scratch, int64_t scratch_stride,
+                         KmeansAttemptOut *attempts, KmeansImageOut *out, const KmeansCubes &cubes,
+                         hipStream_t s);
 // u32 scratch per (image, attempt) for k-means++ step sums
 int64_t kmeans_scratch_stride(int64_t key_stride);
 constexpr int kMaxKmeansBatch = 4096;
