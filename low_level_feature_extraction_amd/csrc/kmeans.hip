@@ -128,7 +128,7 @@ __device__ __forceinline__ int label5p(uint32_t key, const CentP &c) {
 }
 
 constexpr int PF = 4;  // steps of 16-B key loads kept in flight per wave
-constexpr int FQ = 8;  // boundary cubes labelled per round of the pruned sweep
+constexpr int FQ = 8;  // boundary cubes labelled per round of the pruned sweep (16: no gain)
 
 // the 4 keys of lane `lane` in 256-point step `s` (zeros past the full steps)
 __device__ __forceinline__ uint4 load_step(const uint32_t *pts, int s, int se_full, int lane) {
@@ -854,129 +854,7 @@ __global__ void k_kmeans_finalize(const uint32_t *__restrict__ keys, long long k
     out[img] = r;
 }
 
-// ---------------------------------------------------------------- cube compaction
-// One 1024-thread workgroup per image walks the 64 red slabs R (rows r = 4R..4R+3):
-// the slab's 4 x 2048 bitmap words are staged in LDS (skipped when their occupancy is
-// empty); thread t owns cubes (G = t / 16, B = 4 (t % 16) .. + 3), gathers each cube's
-// 64-bit occupancy from 16 nibbles, and a block scan places cubes and keys in cube-id
-// order.  Bit i*16 + j*4 + bb of a cube mask = colour (4R+i, 4G+j, 4B+bb).
-constexpr int CT = 1024;
-
-__device__ __forceinline__ unsigned long long block_excl_scan_u64(unsigned long long v, unsigned long long *tmp,
-                                                                  unsigned long long *total) {
-    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-    unsigned long long x = v;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        unsigned long long y = __shfl_up(x, off);
-        if (lane >= off) x += y;
-    }
-    if (lane == 63) tmp[wid] = x;
-    __syncthreads();
-    if (wid == 0) {
-        unsigned long long s = lane < CT / 64 ? tmp[lane] : 0ull;
-#pragma unroll
-        for (int off = 1; off < CT / 64; off <<= 1) {
-            unsigned long long y = __shfl_up(s, off);
-            if (lane >= off) s += y;
-        }
-        if (lane < CT / 64) tmp[lane] = s;  // inclusive wave prefix
-    }
-    __syncthreads();
-    const unsigned long long r = (wid ? tmp[wid - 1] : 0ull) + x - v;
-    *total = tmp[CT / 64 - 1];
-    __syncthreads();
-    return r;
-}
-
-__global__ __launch_bounds__(CT) void k_cube_compact(const uint32_t *__restrict__ bitmap,
-                                                     const uint32_t *__restrict__ occ, uint32_t *__restrict__ ckeys,
-                                                     long long key_stride, CubeEnt *__restrict__ cubes,
-                                                     long long cube_stride, int *__restrict__ n_cubes) {
-    __shared__ __attribute__((aligned(16))) uint32_t W[4 * 2048];
-    __shared__ unsigned long long tmp[CT / 64];
-    const int img = blockIdx.x, t = threadIdx.x;
-    const uint32_t *bm = bitmap + (size_t)img * kBitmapWords;
-    const uint32_t *oc = occ + (size_t)img * kOccWords;
-    uint32_t *ck = ckeys + (size_t)img * key_stride;
-    CubeEnt *ce = cubes + (size_t)img * cube_stride;
-    const int G = t >> 4, B0 = (t & 15) * 4;
-    const int wsel = (G << 5) | ((t & 15) >> 1);  // word (j = 0) holding this thread's 4 cubes
-    const int sh0 = (t & 1) * 16;                  // nibble offset of cube B0 in that word
-    unsigned long long run = 0;                    // cubes << 32 | keys placed so far
-    for (int R = 0; R < 64; R++) {
-        // occupancy words of rows 4R..4R+3 are 16R .. 16R + 15
-        const uint32_t o = t < 16 ? oc[16 * R + t] : 0u;
-        if (!__syncthreads_or(o != 0u)) continue;
-        const uint4 *src = (const uint4 *)bm;
-#pragma unroll
-        for (int q = 0; q < 2; q++) {
-            const int idx = t + q * CT;  // uint4 index within the 4 x 512 staged
-            const int row = idx >> 9, within = idx & 511;
-            ((uint4 *)W)[idx] = src[((size_t)(4 * R + row) << 9) + within];
-        }
-        __syncthreads();
-        uint32_t w[4][4];
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-#pragma unroll
-            for (int j = 0; j < 4; j++) w[i][j] = W[i * 2048 + wsel + (j << 3)];
-        unsigned long long mask[4];
-        unsigned long long mine = 0;
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-            unsigned long long m = 0;
-#pragma unroll
-            for (int i = 0; i < 4; i++)
-#pragma unroll
-                for (int j = 0; j < 4; j++)
-                    m |= (unsigned long long)((w[i][j] >> (sh0 + 4 * c)) & 15u) << (i * 16 + j * 4);
-            mask[c] = m;
-            mine += m ? (1ull << 32) + (unsigned long long)__popcll(m) : 0ull;
-        }
-        unsigned long long total;
-        const unsigned long long pos = run + block_excl_scan_u64(mine, tmp, &total);
-        unsigned ci = (unsigned)(pos >> 32), pi = (unsigned)pos;
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-            const unsigned long long m = mask[c];
-            if (!m) continue;
-            const int B = B0 + c;
-            const unsigned cnt = (unsigned)__popcll(m);
-            unsigned sr = 4u * R * cnt, sg = 4u * G * cnt, sb = 4u * B * cnt;
-#pragma unroll
-            for (int i = 1; i < 4; i++) sr += i * (unsigned)__popcll(m & (0xFFFFull << (16 * i)));
-#pragma unroll
-            for (int j = 1; j < 4; j++) sg += j * (unsigned)__popcll(m & (0x000F000F000F000Full << (4 * j)));
-#pragma unroll
-            for (int bb = 1; bb < 4; bb++) sb += bb * (unsigned)__popcll(m & (0x1111111111111111ull << bb));
-            CubeEnt e;
-            e.offset = pi;
-            e.id = ((unsigned)R << 12) | ((unsigned)G << 6) | (unsigned)B;
-            e.sums = (unsigned long long)sr | ((unsigned long long)sg << 16) | ((unsigned long long)sb << 32) |
-                     ((unsigned long long)cnt << 48);
-            ce[ci++] = e;
-            for (unsigned long long mm = m; mm; mm &= mm - 1) {
-                const int bit = __builtin_ctzll(mm);
-                const int i = bit >> 4, j = (bit >> 2) & 3, bb = bit & 3;
-                ck[pi++] = ((unsigned)(4 * R + i) << 16) | ((unsigned)(4 * G + j) << 8) | (unsigned)(4 * B + bb);
-            }
-        }
-        run += total;
-    }
-    if (t == 0) n_cubes[img] = (int)(run >> 32);
-}
-
 }  // namespace
-
-hipError_t launch_cube_compact(const uint32_t *bitmap, const uint32_t *occ, int n, uint32_t *ckeys,
-                               int64_t key_stride, CubeEnt *cubes, int64_t cube_stride, int32_t *n_cubes,
-                               hipStream_t s) {
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_cube_compact, dim3(n), dim3(CT), 0, s, bitmap, occ, ckeys, (long long)key_stride, cubes,
-                       (long long)cube_stride, n_cubes);
-    return hipGetLastError();
-}
 
 hipError_t launch_kmeans(const uint32_t *keys, int64_t key_stride, const int64_t *n_unique, int n, int n_colors,
                          uint64_t seed, int64_t index_base, int32_t *order, uint32_t *scratch, int64_t scratch_stride,

@@ -291,8 +291,8 @@ struct llfe_ctx {
     DevBuf<unsigned long long> d_shadow;
     DevBuf<int> d_order, d_parent, d_nroots;
     DevBuf<uint16_t> d_lab, d_roots;
-    DevBuf<uint32_t> d_bitmap, d_occ, d_keys, d_kscratch, d_ckeys;
-    DevBuf<CubeEnt> d_cubes;
+    DevBuf<uint32_t> d_raw, d_keys, d_kscratch, d_ckeys, d_pmeta;
+    DevBuf<CubeEnt> d_segcubes, d_cubes;
     DevBuf<int32_t> d_ncubes;
     DevBuf<int64_t> d_nuniq;
     DevBuf<KmeansAttemptOut> d_att;
@@ -306,7 +306,6 @@ struct llfe_ctx {
     hipEvent_t chunk_done[2] = {nullptr, nullptr};
     int chunk = 256;  // images per device pass (LLFE_CHUNK)
     HostBuf<KmeansImageOut> h_kout;
-    HostBuf<int64_t> h_nuniq;
     // per-thread host scratch
     std::vector<std::vector<int8_t>> work;
     std::vector<Contours> cont;
@@ -382,25 +381,32 @@ int run_hysteresis_dilate(llfe_ctx *ctx, int n, int h, int w, uint64_t *bits, ui
 
 int color_stage(llfe_ctx *ctx, const uint8_t *img, const int8_t *noise, int n, int h, int w, uint64_t seed,
                 int64_t index_base, hipStream_t s) {
+    // unique colours -> ctx->d_keys (sorted, key_stride) + cube table for k-means
     const int64_t P = (int64_t)h * w;
     const int64_t key_stride = (std::max<int64_t>(P, 1) + 3) & ~int64_t(3);
-    HIPCHK(ctx, ctx->d_bitmap.ensure((size_t)n * kBitmapWords, true));
-    HIPCHK(ctx, ctx->d_occ.ensure((size_t)n * kOccWords, true));
-    HIPCHK(ctx, ctx->d_keys.ensure((size_t)n * key_stride));
-    HIPCHK(ctx, ctx->d_nuniq.ensure(n));
-    TIMED(ctx, s, "k_color_bitmap", (double)n * P * (noise ? 6 : 3),
-          launch_color_bitmap(img, noise, n, h, w, seed, index_base, ctx->d_bitmap.p, ctx->d_occ.p, s));
-    // cube-ordered keys + cube table for the pruned Lloyd sweeps (reads the bitmap
-    // before the compaction clears it)
     const int64_t cube_stride = std::min<int64_t>(key_stride, kMaxCubes);
+    HIPCHK(ctx, ctx->d_raw.ensure((size_t)n * key_stride));
+    HIPCHK(ctx, ctx->d_keys.ensure((size_t)n * key_stride));
     HIPCHK(ctx, ctx->d_ckeys.ensure((size_t)n * key_stride));
+    HIPCHK(ctx, ctx->d_segcubes.ensure((size_t)n * kParts * kCubesPerPart));
     HIPCHK(ctx, ctx->d_cubes.ensure((size_t)n * cube_stride));
+    HIPCHK(ctx, ctx->d_pmeta.ensure((size_t)n * kParts * 4));
+    HIPCHK(ctx, ctx->d_nuniq.ensure(n));
     HIPCHK(ctx, ctx->d_ncubes.ensure(n));
-    TIMED(ctx, s, "k_cube_compact", (double)n * (4.0 * kBitmapWords),
-          launch_cube_compact(ctx->d_bitmap.p, ctx->d_occ.p, n, ctx->d_ckeys.p, key_stride, ctx->d_cubes.p,
-                              cube_stride, ctx->d_ncubes.p, s));
-    TIMED(ctx, s, "k_color_compact", (double)n * (4.0 * kBitmapWords),
-          launch_color_compact(ctx->d_bitmap.p, ctx->d_occ.p, n, ctx->d_keys.p, key_stride, ctx->d_nuniq.p, s));
+    uint32_t *hist = ctx->d_pmeta.p, *cursor = hist + (size_t)n * kParts, *uq = cursor + (size_t)n * kParts,
+             *cc = uq + (size_t)n * kParts;
+    HIPCHK(ctx, hipMemsetAsync(hist, 0, sizeof(uint32_t) * 2 * n * kParts, s));
+    TIMED(ctx, s, "k_uq_keys", (double)n * P * (noise ? 10 : 7),
+          launch_uq_keys(img, noise, n, h, w, seed, index_base, key_stride, ctx->d_raw.p, hist, s));
+    TIMED(ctx, s, "k_uq_scatter", (double)n * P * 8,
+          launch_uq_scatter(ctx->d_raw.p, n, P, key_stride, hist, cursor, ctx->d_keys.p, s));
+    // the partitions' sorted unique keys overwrite the (dead) raw keys
+    TIMED(ctx, s, "k_uq_part", (double)n * P * 4,
+          launch_uq_part(ctx->d_keys.p, n, key_stride, hist, ctx->d_raw.p, ctx->d_ckeys.p, ctx->d_segcubes.p, uq, cc,
+                         s));
+    TIMED(ctx, s, "k_uq_gather", 0,
+          launch_uq_gather(ctx->d_raw.p, n, key_stride, hist, uq, cc, ctx->d_segcubes.p, ctx->d_keys.p, ctx->d_cubes.p,
+                           cube_stride, ctx->d_nuniq.p, ctx->d_ncubes.p, s));
     return LLFE_OK;
 }
 
@@ -511,8 +517,16 @@ int finish_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, int i0, 
     const unsigned long long *sh = ctx->h_shadow_s[slot].p;
     if (want_col && ctx->prof.on) {
         double kb = 0;
-        for (int i = 0; i < n; i++) kb += (double)ko[i].bytes;
+        double ub = 0;
+        for (int i = 0; i < n; i++) {
+            kb += (double)ko[i].bytes;
+            ub += 8.0 * (double)ko[i].n_unique;
+        }
         ctx->prof.add_bytes("k_kmeans", kb);
+        // unique keys written twice by k_uq_part (sorted + cube order), read + written
+        // by k_uq_gather (cube entries, <= U / 1, not counted)
+        ctx->prof.add_bytes("k_uq_part", ub);
+        ctx->prof.add_bytes("k_uq_gather", ub);
     }
     for (int i = 0; i < n; i++) {
         llfe_image_result &r = results[i0 + i];
@@ -697,22 +711,20 @@ int llfe_shadow_stats(llfe_ctx *ctx, const uint8_t *bgr, uint64_t *sums, uint64_
 int llfe_color_unique(llfe_ctx *ctx, const llfe_batch *b, uint64_t seed, uint32_t *keys, int64_t *n_unique,
                       llfe_stream stream) {
     if (!ctx || !b || !keys || !n_unique || !valid_dims(b->n, b->height, b->width)) return LLFE_ERR_INVALID;
-    constexpr int kMaxUniqueBatch = 1024;  // 2 MiB of bitmap per image
-    if (b->n > kMaxUniqueBatch) return ctx->fail(LLFE_ERR_UNSUPPORTED, "llfe_color_unique: n > %d", kMaxUniqueBatch);
+    if (b->n > ctx->chunk) return ctx->fail(LLFE_ERR_UNSUPPORTED, "llfe_color_unique: n > %d", ctx->chunk);
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t s = (hipStream_t)stream;
     const int h = b->height, w = b->width, n = b->n;
     const int64_t P = (int64_t)h * w;
+    const int64_t key_stride = (std::max<int64_t>(P, 1) + 3) & ~int64_t(3);
     const uint8_t *img;
     const int8_t *noise;
     int rc = stage_input(ctx, b, 0, n, &img, &noise, s);
     if (rc) return rc;
-    HIPCHK(ctx, ctx->d_bitmap.ensure((size_t)n * kBitmapWords, true));
-    HIPCHK(ctx, ctx->d_occ.ensure((size_t)n * kOccWords, true));
-    HIPCHK(ctx, ctx->d_nuniq.ensure(n));
-    HIPCHK(ctx, ctx->h_nuniq.ensure(n));
-    HIPCHK(ctx, launch_color_bitmap(img, noise, n, h, w, seed, b->index_base, ctx->d_bitmap.p, ctx->d_occ.p, s));
-    HIPCHK(ctx, launch_color_compact(ctx->d_bitmap.p, ctx->d_occ.p, n, keys, P, ctx->d_nuniq.p, s));
+    rc = color_stage(ctx, img, noise, n, h, w, seed, b->index_base, s);
+    if (rc) return rc;
+    HIPCHK(ctx, hipMemcpy2DAsync(keys, sizeof(uint32_t) * P, ctx->d_keys.p, sizeof(uint32_t) * key_stride,
+                                 sizeof(uint32_t) * P, n, hipMemcpyDeviceToDevice, s));
     HIPCHK(ctx, hipMemcpyAsync(n_unique, ctx->d_nuniq.p, sizeof(int64_t) * n, hipMemcpyDeviceToHost, s));
     HIPCHK(ctx, hipStreamSynchronize(s));
     return LLFE_OK;

@@ -42,17 +42,10 @@ inline int tiles_x(int w) { return (w + kTileW - 1) / kTileW; }
 inline int tiles_y(int h) { return (h + kTileH - 1) / kTileH; }
 
 // ---------------------------------------------------------------- colours
-constexpr int kBitmapWords = 1 << 19;  // 2^24 bits as u32 words (2 MiB per image)
-constexpr int kOccWords = 1 << 10;     // 1 bit per 512-bit block -> 32768 bits
 constexpr int kMaxK = 5;
 constexpr int kAttempts = 10;
-
-// BGR->RGB, noise (host int8 RGB stream or Philox), presence bitmap + occupancy.
-hipError_t launch_color_bitmap(const uint8_t *bgr, const int8_t *noise, int n, int h, int w, uint64_t seed,
-                               int64_t index_base, uint32_t *bitmap, uint32_t *occ, hipStream_t s);
-// bitmap -> ascending keys (np.unique order), clears bitmap+occ for reuse.
-hipError_t launch_color_compact(uint32_t *bitmap, uint32_t *occ, int n, uint32_t *keys, int64_t key_stride,
-                                int64_t *n_unique, hipStream_t s);
+constexpr int kParts = 64;         // key partitions by red quarter r >> 2
+constexpr int kCubesPerPart = 4096;  // 64 x 64 cubes of 4x4x4 per partition
 
 struct KmeansAttemptOut {
     double compactness;
@@ -92,11 +85,23 @@ struct KmeansCubes {
     int64_t cube_stride;
     const int32_t *n_cubes;
 };
-// bitmap -> cube-ordered keys + cube table (run before launch_color_compact, which
-// clears the bitmap)
-hipError_t launch_cube_compact(const uint32_t *bitmap, const uint32_t *occ, int n, uint32_t *ckeys,
-                               int64_t key_stride, CubeEnt *cubes, int64_t cube_stride, int32_t *n_cubes,
-                               hipStream_t s);
+// Unique colours (unique.hip), all per image with stride key_stride (u32 keys):
+//   keys:    pixels -> noised keys into `raw`, partition histogram `hist` (n x 64, zeroed)
+//   scatter: raw -> `part` grouped by partition (`cursor` n x 64, zeroed)
+//   part:    per (image, partition): sorted unique keys -> `skeys` (may alias raw),
+//            cube-ordered keys -> `ckeys`, cube entries -> `seg_cubes` (n x 64 x 4096),
+//            counts -> uq, cc (n x 64)
+//   gather:  contiguous sorted keys -> `keys` (may alias part), cube table -> `cubes`,
+//            n_unique, n_cubes
+hipError_t launch_uq_keys(const uint8_t *bgr, const int8_t *noise, int n, int h, int w, uint64_t seed,
+                          int64_t index_base, int64_t key_stride, uint32_t *raw, uint32_t *hist, hipStream_t s);
+hipError_t launch_uq_scatter(const uint32_t *raw, int n, int64_t P, int64_t key_stride, const uint32_t *hist,
+                             uint32_t *cursor, uint32_t *part, hipStream_t s);
+hipError_t launch_uq_part(const uint32_t *part, int n, int64_t key_stride, const uint32_t *hist, uint32_t *skeys,
+                          uint32_t *ckeys, CubeEnt *seg_cubes, uint32_t *uq, uint32_t *cc, hipStream_t s);
+hipError_t launch_uq_gather(const uint32_t *skeys, int n, int64_t key_stride, const uint32_t *hist, const uint32_t *uq,
+                            const uint32_t *cc, const CubeEnt *seg_cubes, uint32_t *keys, CubeEnt *cubes,
+                            int64_t cube_stride, int64_t *n_unique, int32_t *n_cubes, hipStream_t s);
 
 // per image: K = min(n_colors, U); attempts run as separate workgroups
 // (ordered largest U first), then a finalize kernel picks the best attempt.

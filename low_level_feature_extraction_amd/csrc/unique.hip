@@ -1,0 +1,442 @@
+// Dominant-colour front half of ColorExtractor.extract_colors on gfx950
+// (app/services/analyze/color_extractor.py:217-236): BGR->RGB (:150-151), + int8(N(0,0.5))
+// noise and clip (:223-225), then the set of distinct colours in ascending packed-key
+// order = np.unique(pixels, axis=0) (:177), plus the 4x4x4 colour cubes the k-means
+// Lloyd sweeps prune with (kmeans.hip).
+//
+// No global atomics on colours: keys are partitioned by their red quarter R = r >> 2
+// (64 partitions; a partition is a contiguous range of the sorted key space), and each
+// partition is deduplicated in a 32 KB LDS bitmap by one workgroup.
+//
+//   k_uq_keys     pixel -> key r<<16|g<<8|b (4 B) + per-image histogram of R
+//   k_uq_scatter  counting sort of the keys by R (block-local LDS sort, 64 global
+//                 cursors per image, coalesced runs out)
+//   k_uq_part     one 1024-thread workgroup per (image, R): LDS bitmap of the partition's
+//                 4 x 256 x 256 colours -> its sorted unique keys, its cubes and the cube-
+//                 ordered keys (written in place of the partition)
+//   k_uq_gather   per image: prefix over the partitions, contiguous sorted keys + cube
+//                 table (cube offsets keep pointing into the partitioned cube keys)
+#include <algorithm>
+
+#include "llfe_internal.h"
+
+namespace llfe {
+namespace {
+
+// ------------------------------------------------------------------ noise
+// trunc(0.5 * Z), Z ~ N(0, 1), from a 21-bit uniform u via tail thresholds:
+// P(Z <= -2) * 2^21 = 47710.9 -> 47711, P(Z <= -4) * 2^21 = 66.4 -> 66 (|n| = 3 has
+// probability 1e-9 per channel and is not produced).
+__device__ __forceinline__ int noise21(uint32_t u) {
+    const uint32_t T1 = 47711u, T2 = 66u;
+    const bool neg = u < (1u << 20);
+    const uint32_t v = neg ? u : (1u << 21) - 1u - u;
+    const int mag = (v < T1) + (v < T2);
+    return neg ? -mag : mag;
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+constexpr int KB = 256;   // threads per block (keys / scatter)
+constexpr int PPT = 16;   // pixels per thread per block step
+constexpr int NPART = 64;
+
+__device__ __forceinline__ uint32_t key_of(int b, int g, int r, int nb, int ng, int nr) {
+    r = min(max(r + nr, 0), 255);
+    g = min(max(g + ng, 0), 255);
+    b = min(max(b + nb, 0), 255);
+    return ((uint32_t)r << 16) | ((uint32_t)g << 8) | (uint32_t)b;
+}
+
+// grid (blocks, n).  noise: parity-mode int8 stream in RGB order (p*3 + c) or null
+// (counter-based: h = splitmix64(image stream + pixel), three 21-bit uniforms).
+__global__ __launch_bounds__(KB) void k_uq_keys(const uint8_t *__restrict__ bgr, const int8_t *__restrict__ noise,
+                                                long long P, long long key_stride, unsigned long long seed,
+                                                long long index_base, uint32_t *__restrict__ keys,
+                                                uint32_t *__restrict__ hist) {
+    __shared__ uint32_t lh[NPART];
+    const int img = blockIdx.y;
+    const uint8_t *src = bgr + (size_t)img * P * 3;
+    const int8_t *nz = noise ? noise + (size_t)img * P * 3 : nullptr;
+    uint32_t *out = keys + (size_t)img * key_stride;
+    const uint64_t stream = mix64(seed ^ mix64((uint64_t)(index_base + img) + 0x4C4C46454C4C4645ull));
+    if (threadIdx.x < NPART) lh[threadIdx.x] = 0;
+    __syncthreads();
+    const long long nchunks = (P + PPT - 1) / PPT;
+    for (long long c = (long long)blockIdx.x * KB + threadIdx.x; c < nchunks; c += (long long)gridDim.x * KB) {
+        const long long p0 = c * PPT;
+        const int cnt = (int)min((long long)PPT, P - p0);
+        uint8_t px[3 * PPT];
+        int8_t nv[3 * PPT];
+        const uint8_t *sp = src + p0 * 3;
+        if (cnt == PPT && (((uintptr_t)sp) & 15) == 0) {
+            *(uint4 *)&px[0] = ((const uint4 *)sp)[0];
+            *(uint4 *)&px[16] = ((const uint4 *)sp)[1];
+            *(uint4 *)&px[32] = ((const uint4 *)sp)[2];
+        } else {
+            for (int i = 0; i < 3 * PPT; i++) px[i] = i < cnt * 3 ? sp[i] : 0;
+        }
+        if (nz) {
+            const int8_t *np_ = nz + p0 * 3;
+            if (cnt == PPT && (((uintptr_t)np_) & 15) == 0) {
+                *(uint4 *)&nv[0] = ((const uint4 *)np_)[0];
+                *(uint4 *)&nv[16] = ((const uint4 *)np_)[1];
+                *(uint4 *)&nv[32] = ((const uint4 *)np_)[2];
+            } else {
+                for (int i = 0; i < 3 * PPT; i++) nv[i] = i < cnt * 3 ? np_[i] : 0;
+            }
+        }
+        uint32_t kv[PPT];
+        uint32_t run_bin = 0xFFFFFFFFu, run_len = 0;
+#pragma unroll
+        for (int i = 0; i < PPT; i++) {
+            int nr, ng, nb;
+            if (nz) {
+                nr = nv[3 * i];
+                ng = nv[3 * i + 1];
+                nb = nv[3 * i + 2];
+            } else {
+                const uint64_t hsh = mix64(stream + 0x9E3779B97F4A7C15ull * (uint64_t)(p0 + i + 1));
+                nr = noise21((uint32_t)hsh & 0x1FFFFFu);
+                ng = noise21((uint32_t)(hsh >> 21) & 0x1FFFFFu);
+                nb = noise21((uint32_t)(hsh >> 42) & 0x1FFFFFu);
+            }
+            kv[i] = key_of(px[3 * i], px[3 * i + 1], px[3 * i + 2], nb, ng, nr);
+            if (i < cnt) {  // run-length histogram: neighbouring pixels share a partition
+                const uint32_t bin = kv[i] >> 18;
+                if (bin != run_bin) {
+                    if (run_len) atomicAdd(&lh[run_bin], run_len);
+                    run_bin = bin;
+                    run_len = 0;
+                }
+                run_len++;
+            }
+        }
+        if (run_len) atomicAdd(&lh[run_bin], run_len);
+        uint32_t *op = out + p0;
+        if (cnt == PPT && (((uintptr_t)op) & 15) == 0) {
+#pragma unroll
+            for (int q = 0; q < PPT / 4; q++)
+                ((uint4 *)op)[q] = make_uint4(kv[4 * q], kv[4 * q + 1], kv[4 * q + 2], kv[4 * q + 3]);
+        } else {
+            for (int i = 0; i < cnt; i++) op[i] = kv[i];
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < NPART && lh[threadIdx.x]) atomicAdd(hist + (size_t)img * NPART + threadIdx.x, lh[threadIdx.x]);
+}
+
+// exclusive prefix of the image's 64 partition sizes (one wave)
+__device__ __forceinline__ uint32_t part_base(const uint32_t *h, int lane, uint32_t *total) {
+    uint32_t v = lane < NPART ? h[lane] : 0u, x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        uint32_t y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+    }
+    *total = __shfl(x, 63);
+    return x - v;
+}
+
+constexpr int SK = KB * PPT;  // keys per scatter block step
+
+__global__ __launch_bounds__(KB) void k_uq_scatter(const uint32_t *__restrict__ keys, long long P, long long key_stride,
+                                                   const uint32_t *__restrict__ hist, uint32_t *__restrict__ cursor,
+                                                   uint32_t *__restrict__ part) {
+    __shared__ uint32_t base[NPART], cnt[NPART], lbase[NPART], gbase[NPART];
+    __shared__ uint32_t stage[SK];
+    const int img = blockIdx.y, t = threadIdx.x;
+    const uint32_t *in = keys + (size_t)img * key_stride;
+    uint32_t *out = part + (size_t)img * key_stride;
+    if (t < 64) {
+        uint32_t tot;
+        const uint32_t b = part_base(hist + (size_t)img * NPART, t, &tot);
+        base[t] = b;
+    }
+    const long long nsteps = (P + SK - 1) / SK;
+    for (long long st = blockIdx.x; st < nsteps; st += gridDim.x) {
+        const long long p0 = st * SK + (long long)t * PPT;
+        const int n = (int)max(0LL, min((long long)PPT, P - p0));
+        if (t < NPART) cnt[t] = 0;
+        __syncthreads();
+        uint32_t kv[PPT], pos[PPT];
+        if (n == PPT && (((uintptr_t)(in + p0)) & 15) == 0) {
+#pragma unroll
+            for (int q = 0; q < PPT / 4; q++) {
+                const uint4 v = ((const uint4 *)(in + p0))[q];
+                kv[4 * q] = v.x;
+                kv[4 * q + 1] = v.y;
+                kv[4 * q + 2] = v.z;
+                kv[4 * q + 3] = v.w;
+            }
+        } else {
+            for (int i = 0; i < PPT; i++) kv[i] = i < n ? in[p0 + i] : 0u;
+        }
+        // rank within the block's bin: one LDS atomic per run of equal bins
+        {
+            int i = 0;
+            while (i < n) {
+                const uint32_t bin = kv[i] >> 18;
+                int j = i + 1;
+                while (j < n && (kv[j] >> 18) == bin) j++;
+                const uint32_t r0 = atomicAdd(&cnt[bin], (uint32_t)(j - i));
+                for (int q = i; q < j; q++) pos[q] = r0 + (uint32_t)(q - i);
+                i = j;
+            }
+        }
+        __syncthreads();
+        if (t < 64) {
+            const uint32_t c = cnt[t];
+            uint32_t x = c;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                uint32_t y = __shfl_up(x, off);
+                if (t >= off) x += y;
+            }
+            lbase[t] = x - c;
+            gbase[t] = c ? base[t] + atomicAdd(cursor + (size_t)img * NPART + t, c) : 0u;
+        }
+        __syncthreads();
+        for (int i = 0; i < n; i++) stage[lbase[kv[i] >> 18] + pos[i]] = kv[i];
+        __syncthreads();
+        const int tot = (int)min((long long)SK, P - st * SK);
+        for (int i = t; i < tot; i += KB) {
+            const uint32_t k = stage[i];
+            const uint32_t bin = k >> 18;
+            out[gbase[bin] + (uint32_t)i - lbase[bin]] = k;
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------ partitions
+constexpr int UT = 1024;
+
+__device__ __forceinline__ unsigned long long scan_u64_1024(unsigned long long v, unsigned long long *tmp,
+                                                            unsigned long long *total) {
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    unsigned long long x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        unsigned long long y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) tmp[wid] = x;
+    __syncthreads();
+    if (wid == 0) {
+        unsigned long long s = lane < UT / 64 ? tmp[lane] : 0ull;
+#pragma unroll
+        for (int off = 1; off < UT / 64; off <<= 1) {
+            unsigned long long y = __shfl_up(s, off);
+            if (lane >= off) s += y;
+        }
+        if (lane < UT / 64) tmp[lane] = s;
+    }
+    __syncthreads();
+    const unsigned long long r = (wid ? tmp[wid - 1] : 0ull) + x - v;
+    *total = tmp[UT / 64 - 1];
+    __syncthreads();
+    return r;
+}
+
+// grid (64, n).  Reads the partition's keys from `part`, writes (in place of those
+// keys, so capacity is the partition size) the sorted unique keys to `skeys` and the
+// cube-ordered keys to `ckeys`, and up to 4096 cube entries to `seg_cubes`.
+__global__ __launch_bounds__(UT) void k_uq_part(const uint32_t *__restrict__ part, long long key_stride,
+                                                const uint32_t *__restrict__ hist, uint32_t *__restrict__ skeys,
+                                                uint32_t *__restrict__ ckeys, CubeEnt *__restrict__ seg_cubes,
+                                                uint32_t *__restrict__ uq, uint32_t *__restrict__ cc) {
+    __shared__ __attribute__((aligned(16))) uint32_t W[4 * 2048];  // rows r = 4R + i, word g << 3 | b >> 5
+    __shared__ unsigned long long tmp[UT / 64];
+    __shared__ uint32_t sbase, scount;
+    const int R = blockIdx.x, img = blockIdx.y, t = threadIdx.x;
+    if (t < 64) {
+        uint32_t tot;
+        const uint32_t b = part_base(hist + (size_t)img * NPART, t, &tot);
+        if (t == R) {
+            sbase = b;
+            scount = hist[(size_t)img * NPART + R];
+        }
+    }
+    for (int i = t; i < 4 * 2048 / 4; i += UT) ((uint4 *)W)[i] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    const uint32_t start = sbase, count = scount;
+    if (count == 0) {
+        if (t == 0) {
+            uq[(size_t)img * NPART + R] = 0;
+            cc[(size_t)img * NPART + R] = 0;
+        }
+        return;
+    }
+    const uint32_t *in = part + (size_t)img * key_stride + start;
+    for (uint32_t i = t; i < count; i += UT) {
+        const uint32_t k = in[i];
+        atomicOr(&W[((k >> 16) & 3u) * 2048 + ((k >> 5) & 2047u)], 1u << (k & 31u));
+    }
+    __syncthreads();
+    // (a) unique keys in ascending order: thread t owns words 8t .. 8t + 7
+    {
+        uint32_t w8[8], c = 0;
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            w8[q] = W[t * 8 + q];
+            c += __popc(w8[q]);
+        }
+        unsigned long long tot;
+        uint32_t pos = (uint32_t)scan_u64_1024(c, tmp, &tot);
+        uint32_t *o = skeys + (size_t)img * key_stride + start;
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const int word = t * 8 + q;  // = i * 2048 + (g << 3 | b >> 5)
+            const uint32_t kb = ((uint32_t)(4 * R + (word >> 11)) << 16) | ((uint32_t)(word & 2047) << 5);
+            for (uint32_t m = w8[q]; m; m &= m - 1) o[pos++] = kb | (uint32_t)__builtin_ctz(m);
+        }
+        if (t == 0) uq[(size_t)img * NPART + R] = (uint32_t)tot;
+    }
+    // (b) 4x4x4 cubes of the partition in cube-id order (see CubeEnt): thread t owns
+    // cubes (G = t / 16, B = 4 (t % 16) .. + 3); bit i*16 + j*4 + bb = (4R+i, 4G+j, 4B+bb)
+    {
+        const int G = t >> 4, B0 = (t & 15) * 4;
+        const int wsel = (G << 5) | ((t & 15) >> 1);
+        const int sh0 = (t & 1) * 16;
+        uint32_t w[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) w[i][j] = W[i * 2048 + wsel + (j << 3)];
+        unsigned long long mask[4], mine = 0;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            unsigned long long m = 0;
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    m |= (unsigned long long)((w[i][j] >> (sh0 + 4 * c)) & 15u) << (i * 16 + j * 4);
+            mask[c] = m;
+            mine += m ? (1ull << 32) + (unsigned long long)__popcll(m) : 0ull;
+        }
+        unsigned long long tot;
+        const unsigned long long pos = scan_u64_1024(mine, tmp, &tot);
+        uint32_t ci = (uint32_t)(pos >> 32), pi = (uint32_t)pos;
+        CubeEnt *ce = seg_cubes + ((size_t)img * NPART + R) * 4096;
+        uint32_t *ck = ckeys + (size_t)img * key_stride + start;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const unsigned long long m = mask[c];
+            if (!m) continue;
+            const int B = B0 + c;
+            const uint32_t n = (uint32_t)__popcll(m);
+            uint32_t sr = 4u * R * n, sg = 4u * G * n, sb = 4u * B * n;
+#pragma unroll
+            for (int i = 1; i < 4; i++) sr += i * (uint32_t)__popcll(m & (0xFFFFull << (16 * i)));
+#pragma unroll
+            for (int j = 1; j < 4; j++) sg += j * (uint32_t)__popcll(m & (0x000F000F000F000Full << (4 * j)));
+#pragma unroll
+            for (int bb = 1; bb < 4; bb++) sb += bb * (uint32_t)__popcll(m & (0x1111111111111111ull << bb));
+            CubeEnt e;
+            e.offset = start + pi;
+            e.id = ((uint32_t)R << 12) | ((uint32_t)G << 6) | (uint32_t)B;
+            e.sums = (unsigned long long)sr | ((unsigned long long)sg << 16) | ((unsigned long long)sb << 32) |
+                     ((unsigned long long)n << 48);
+            ce[ci++] = e;
+            for (unsigned long long mm = m; mm; mm &= mm - 1) {
+                const int bit = __builtin_ctzll(mm);
+                ck[pi++] = ((uint32_t)(4 * R + (bit >> 4)) << 16) | ((uint32_t)(4 * G + ((bit >> 2) & 3)) << 8) |
+                           (uint32_t)(4 * B + (bit & 3));
+            }
+        }
+        if (t == 0) cc[(size_t)img * NPART + R] = (uint32_t)(tot >> 32);
+    }
+}
+
+// grid (n): contiguous sorted keys (from the partitions' segments) and cube table
+__global__ __launch_bounds__(UT) void k_uq_gather(const uint32_t *__restrict__ skeys, long long key_stride,
+                                                  const uint32_t *__restrict__ hist, const uint32_t *__restrict__ uq,
+                                                  const uint32_t *__restrict__ cc,
+                                                  const CubeEnt *__restrict__ seg_cubes, uint32_t *__restrict__ keys,
+                                                  CubeEnt *__restrict__ cubes, long long cube_stride,
+                                                  long long *__restrict__ n_unique, int *__restrict__ n_cubes) {
+    __shared__ uint32_t pstart[NPART], ubase[NPART + 1], cbase[NPART + 1];
+    const int img = blockIdx.x, t = threadIdx.x;
+    if (t < 64) {
+        uint32_t tot;
+        pstart[t] = part_base(hist + (size_t)img * NPART, t, &tot);
+        uint32_t ut, ct;
+        ubase[t] = part_base(uq + (size_t)img * NPART, t, &ut);
+        cbase[t] = part_base(cc + (size_t)img * NPART, t, &ct);
+        if (t == 0) {
+            ubase[NPART] = ut;
+            cbase[NPART] = ct;
+            n_unique[img] = ut;
+            n_cubes[img] = (int)ct;
+        }
+    }
+    __syncthreads();
+    const uint32_t U = ubase[NPART], C = cbase[NPART];
+    const uint32_t *sk = skeys + (size_t)img * key_stride;
+    uint32_t *ok = keys + (size_t)img * key_stride;
+    for (uint32_t i = t; i < U; i += UT) {
+        int lo = 0, hi = NPART - 1;  // last partition with ubase <= i
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (ubase[mid] <= i) lo = mid;
+            else hi = mid - 1;
+        }
+        ok[i] = sk[pstart[lo] + (i - ubase[lo])];
+    }
+    const CubeEnt *sc = seg_cubes + (size_t)img * NPART * 4096;
+    CubeEnt *oc = cubes + (size_t)img * cube_stride;
+    for (uint32_t i = t; i < C; i += UT) {
+        int lo = 0, hi = NPART - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (cbase[mid] <= i) lo = mid;
+            else hi = mid - 1;
+        }
+        oc[i] = sc[(size_t)lo * 4096 + (i - cbase[lo])];
+    }
+}
+
+}  // namespace
+
+hipError_t launch_uq_keys(const uint8_t *bgr, const int8_t *noise, int n, int h, int w, uint64_t seed,
+                          int64_t index_base, int64_t key_stride, uint32_t *keys, uint32_t *hist, hipStream_t s) {
+    const long long P = (long long)h * w;
+    const long long per_block = (long long)KB * PPT * 4;
+    int bx = (int)std::min((P + per_block - 1) / per_block, 2048LL);
+    if (bx < 1) bx = 1;
+    hipLaunchKernelGGL(k_uq_keys, dim3(bx, n), dim3(KB), 0, s, bgr, noise, P, (long long)key_stride,
+                       (unsigned long long)seed, (long long)index_base, keys, hist);
+    return hipGetLastError();
+}
+
+hipError_t launch_uq_scatter(const uint32_t *keys, int n, int64_t P, int64_t key_stride, const uint32_t *hist,
+                             uint32_t *cursor, uint32_t *part, hipStream_t s) {
+    int bx = (int)std::min((P + SK * 2 - 1) / (SK * 2), (int64_t)2048);
+    if (bx < 1) bx = 1;
+    hipLaunchKernelGGL(k_uq_scatter, dim3(bx, n), dim3(KB), 0, s, keys, (long long)P, (long long)key_stride, hist,
+                       cursor, part);
+    return hipGetLastError();
+}
+
+hipError_t launch_uq_part(const uint32_t *part, int n, int64_t key_stride, const uint32_t *hist, uint32_t *skeys,
+                          uint32_t *ckeys, CubeEnt *seg_cubes, uint32_t *uq, uint32_t *cc, hipStream_t s) {
+    hipLaunchKernelGGL(k_uq_part, dim3(NPART, n), dim3(UT), 0, s, part, (long long)key_stride, hist, skeys, ckeys,
+                       seg_cubes, uq, cc);
+    return hipGetLastError();
+}
+
+hipError_t launch_uq_gather(const uint32_t *skeys, int n, int64_t key_stride, const uint32_t *hist, const uint32_t *uq,
+                            const uint32_t *cc, const CubeEnt *seg_cubes, uint32_t *keys, CubeEnt *cubes,
+                            int64_t cube_stride, int64_t *n_unique, int32_t *n_cubes, hipStream_t s) {
+    hipLaunchKernelGGL(k_uq_gather, dim3(n), dim3(UT), 0, s, skeys, (long long)key_stride, hist, uq, cc, seg_cubes,
+                       keys, cubes, (long long)cube_stride, (long long *)n_unique, (int *)n_cubes);
+    return hipGetLastError();
+}
+
+}  // namespace llfe

@@ -90,9 +90,10 @@ def test_color_unique_numpy_noise(backend, orc, h, w):
         assert np.array_equal(keys[i, : nu[i]], exp)
 
 
-def test_color_unique_philox_distribution(backend, orc):
-    """On-device noise has the distribution of int8(N(0, 0.5)): base colours spaced 8
-    apart in every channel make each noised key decode to (base, noise) uniquely."""
+def test_color_unique_device_noise_distribution(backend, orc):
+    """On-device noise has the distribution of int8(N(0, 0.5)) (21-bit tail thresholds,
+    unique.hip): base colours spaced 8 apart in every channel make each noised key
+    decode to (base, noise) uniquely."""
     v = np.arange(32) * 8 + 4
     r, g, b = np.meshgrid(v, v, v, indexing="ij")
     rgb = np.stack([r.ravel(), g.ravel(), b.ravel()], -1).astype(np.uint8)  # 32768 distinct
@@ -103,8 +104,10 @@ def test_color_unique_philox_distribution(backend, orc):
     ch = np.stack([(k >> 16) & 255, (k >> 8) & 255, k & 255], -1).astype(np.int64)
     noise = (ch % 8) - 4
     n = noise.size
-    p1 = 0.022750131948179195 - 3.167124183311986e-05
-    for val, p in [(-1, p1), (1, p1), (-2, 3.167e-05), (2, 3.167e-05)]:
+    p1 = (47711 - 66) / 2**21  # P(Z <= -2) - P(Z <= -4), quantised to 21 bits
+    p2 = 66 / 2**21
+    assert abs(p1 - (0.022750131948179195 - 3.167124183311986e-05)) < 1e-6
+    for val, p in [(-1, p1), (1, p1), (-2, p2), (2, p2)]:
         c = int((noise == val).sum())
         sd = np.sqrt(n * p * (1 - p))
         assert abs(c - n * p) <= 5 * sd + 3, (val, c, n * p)
