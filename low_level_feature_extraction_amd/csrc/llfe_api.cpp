@@ -304,6 +304,7 @@ struct llfe_ctx {
     HostBuf<unsigned long long> h_shadow_s[2];
     HostBuf<KmeansImageOut> h_kout_s[2];
     hipEvent_t chunk_done[2] = {nullptr, nullptr};
+    hipEvent_t mask_done[2] = {nullptr, nullptr};  // shapes/shadows results are on the host
     int chunk = 256;  // images per device pass (LLFE_CHUNK)
     HostBuf<KmeansImageOut> h_kout;
     // per-thread host scratch
@@ -477,18 +478,8 @@ int enqueue_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_
                              want_shd ? ctx->d_shadow.p : nullptr, want_shd ? ctx->d_shadow.p + n : nullptr, ctx->sp,
                              s));
     }
-    if (want_col) {
-        rc = color_stage(ctx, img, noise, n, h, w, seed, b->index_base + i0, s);
-        if (rc) return rc;
-        const KmeansCubes cubes{ctx->d_ckeys.p, ctx->d_cubes.p, std::min<int64_t>(key_stride, kMaxCubes),
-                                ctx->d_ncubes.p};
-        rc = kmeans_stage(ctx, ctx->d_keys.p, key_stride, ctx->d_nuniq.p, n, b->n_colors ? b->n_colors : kMaxK, seed,
-                          b->index_base + i0, cubes, s);
-        if (rc) return rc;
-        HIPCHK(ctx, ctx->h_kout_s[slot].ensure(n));
-        HIPCHK(ctx, hipMemcpyAsync(ctx->h_kout_s[slot].p, ctx->d_kout.p, sizeof(KmeansImageOut) * n,
-                                   hipMemcpyDeviceToHost, s));
-    }
+    // shapes + shadows first: their results go to the host (event mask_done) while the
+    // GPU is still in this chunk's colour stage, so contour tracing overlaps k-means
     if (want_shp) {
         HIPCHK(ctx, ctx->d_bits.ensure((size_t)n * h * wpr));
         HIPCHK(ctx, ctx->h_bits_s[slot].ensure((size_t)n * h * wpr));
@@ -502,6 +493,19 @@ int enqueue_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_
         HIPCHK(ctx, hipMemcpyAsync(ctx->h_shadow_s[slot].p, ctx->d_shadow.p, sizeof(unsigned long long) * 2 * n,
                                    hipMemcpyDeviceToHost, s));
     }
+    HIPCHK(ctx, hipEventRecord(ctx->mask_done[slot], s));
+    if (want_col) {
+        rc = color_stage(ctx, img, noise, n, h, w, seed, b->index_base + i0, s);
+        if (rc) return rc;
+        const KmeansCubes cubes{ctx->d_ckeys.p, ctx->d_cubes.p, std::min<int64_t>(key_stride, kMaxCubes),
+                                ctx->d_ncubes.p};
+        rc = kmeans_stage(ctx, ctx->d_keys.p, key_stride, ctx->d_nuniq.p, n, b->n_colors ? b->n_colors : kMaxK, seed,
+                          b->index_base + i0, cubes, s);
+        if (rc) return rc;
+        HIPCHK(ctx, ctx->h_kout_s[slot].ensure(n));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->h_kout_s[slot].p, ctx->d_kout.p, sizeof(KmeansImageOut) * n,
+                                   hipMemcpyDeviceToHost, s));
+    }
     HIPCHK(ctx, hipEventRecord(ctx->chunk_done[slot], s));
     return LLFE_OK;
 }
@@ -512,26 +516,12 @@ int finish_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, int i0, 
     const int h = b->height, w = b->width, wpr = words_per_row(w);
     const bool want_col = features & LLFE_FEATURE_COLORS, want_shp = features & LLFE_FEATURE_SHAPES,
                want_shd = features & LLFE_FEATURE_SHADOWS;
-    HIPCHK(ctx, hipEventSynchronize(ctx->chunk_done[slot]));
-    const KmeansImageOut *ko = ctx->h_kout_s[slot].p;
+    // shapes + shadows are ready first (the GPU may still be in this chunk's colours)
+    HIPCHK(ctx, hipEventSynchronize(ctx->mask_done[slot]));
     const unsigned long long *sh = ctx->h_shadow_s[slot].p;
-    if (want_col && ctx->prof.on) {
-        double kb = 0;
-        double ub = 0;
-        for (int i = 0; i < n; i++) {
-            kb += (double)ko[i].bytes;
-            ub += 8.0 * (double)ko[i].n_unique;
-        }
-        ctx->prof.add_bytes("k_kmeans", kb);
-        // unique keys written twice by k_uq_part (sorted + cube order), read + written
-        // by k_uq_gather (cube entries, <= U / 1, not counted)
-        ctx->prof.add_bytes("k_uq_part", ub);
-        ctx->prof.add_bytes("k_uq_gather", ub);
-    }
     for (int i = 0; i < n; i++) {
         llfe_image_result &r = results[i0 + i];
         std::memset(&r, 0, sizeof r);
-        if (want_col) fill_color_result(ko[i], r);
         if (want_shd) {
             r.shadow_sum = sh[i];
             r.shadow_count = sh[n + i];
@@ -556,6 +546,23 @@ int finish_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, int i0, 
             total_shapes += r.n_shapes;
         }
     }
+    HIPCHK(ctx, hipEventSynchronize(ctx->chunk_done[slot]));
+    if (want_col) {
+        const KmeansImageOut *ko = ctx->h_kout_s[slot].p;
+        for (int i = 0; i < n; i++) fill_color_result(ko[i], results[i0 + i]);
+        if (ctx->prof.on) {
+            double kb = 0, ub = 0;
+            for (int i = 0; i < n; i++) {
+                kb += (double)ko[i].bytes;
+                ub += 8.0 * (double)ko[i].n_unique;
+            }
+            ctx->prof.add_bytes("k_kmeans", kb);
+            // unique keys written twice by k_uq_part (sorted + cube order), read and
+            // written by k_uq_gather (cube entries not counted)
+            ctx->prof.add_bytes("k_uq_part", ub);
+            ctx->prof.add_bytes("k_uq_gather", ub);
+        }
+    }
     return LLFE_OK;
 }
 
@@ -574,9 +581,9 @@ int llfe_init(int device, llfe_ctx **out) {
     if (hipSetDevice(device) != hipSuccess) return LLFE_ERR_HIP;
     llfe_ctx *c = new llfe_ctx();
     c->device = device;
-    for (auto &e : c->chunk_done)
-        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
-            delete c;
+    for (hipEvent_t *e : {&c->chunk_done[0], &c->chunk_done[1], &c->mask_done[0], &c->mask_done[1]})
+        if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) {
+            llfe_destroy(c);
             return LLFE_ERR_HIP;
         }
     if (const char *ch = getenv("LLFE_CHUNK"); ch && atoi(ch) > 0) c->chunk = std::min(atoi(ch), kMaxKmeansBatch);
@@ -593,7 +600,7 @@ int llfe_init(int device, llfe_ctx **out) {
 int llfe_destroy(llfe_ctx *ctx) {
     if (!ctx) return LLFE_OK;
     (void)hipSetDevice(ctx->device);
-    for (auto e : ctx->chunk_done)
+    for (hipEvent_t e : {ctx->chunk_done[0], ctx->chunk_done[1], ctx->mask_done[0], ctx->mask_done[1]})
         if (e) (void)hipEventDestroy(e);
     delete ctx->pool;
     delete ctx;  // DevBuf / HostBuf members free themselves
