@@ -16,7 +16,7 @@ import csv, sys
 from collections import defaultdict
 tot = defaultdict(float); disp = defaultdict(set)
 for r in csv.DictReader(open(sys.argv[1])):
-    k = r["Kernel_Name"].split("(")[0].replace("llfe::(anonymous namespace)::", "")
+    k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].split("::")[-1]
     tot[(k, r["Counter_Name"])] += float(r["Counter_Value"]); disp[k].add(r["Dispatch_Id"])
 for (k, c), v in sorted(tot.items()):
     print(f"{k:28s} {c:28s} {v / len(disp[k]):18.1f}")
