@@ -26,13 +26,15 @@ import os
 import sys
 from collections import defaultdict
 
-FETCH_X2 = {"k_kmeans", "k_color_bitmap", "k_color_compact"}  # 16 B/lane streaming readers
+FETCH_X2 = {"k_kmeans", "k_uq_keys", "k_uq_scatter"}  # 16 B/lane streaming readers
 
 LOGICAL = [  # (substring of the device kernel name, logical launch)
     ("k_stencil", "k_stencil"),
     ("k_ccl_", "k_hysteresis_dilate"),
-    ("k_color_bitmap", "k_color_bitmap"),
-    ("k_color_compact", "k_color_compact"),
+    ("k_uq_keys", "k_uq_keys"),
+    ("k_uq_scatter", "k_uq_scatter"),
+    ("k_uq_part", "k_uq_part"),
+    ("k_uq_gather", "k_uq_gather"),
     ("k_kmeans", "k_kmeans"),
     ("k_resize", "k_resize"),
     ("k_reduce", "k_reduce"),
