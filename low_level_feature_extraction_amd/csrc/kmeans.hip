@@ -473,21 +473,23 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
         if (use_cubes) {
             // Margin test per 4x4x4 cube, q = its centre, k = argmin d(q, c_k):
             //   d_j(p) - d_k(p) is linear in p, so over the cube it is >= (d_j(q) - d_k(q))
-            //   - 3 L1(c_j - c_k); when the second-smallest gap at q exceeds
-            //   3 max_j L1(c_j - c_k) + 1, every colour of the cube is at least 1 closer
-            //   to c_k than to any other centre in exact arithmetic, far above the float
-            //   error of normL2Sqr (< 0.1 at these magnitudes): OpenCV labels it k.
+            //   - 3 L1(c_j - c_k); when d_j(q) - d_k(q) > 3 L1(c_j - c_k) + 1 for every
+            //   j != k, every colour of the cube is at least 1 closer to c_k than to any
+            //   other centre in exact arithmetic, far above the float error of
+            //   normL2Sqr (< 0.1 at these magnitudes): OpenCV labels it k.
+            // pairwise thresholds T[k][j] = 3 L1(c_j - c_k) + 1 (uniform); -inf where the
+            // pair needs no test (j == k, or an unused centre)
             const Cent cu = load_centres(sm.c);
-            float thr[kMaxK];
+            float thr[kMaxK][kMaxK];
 #pragma unroll
-            for (int k = 0; k < kMaxK; k++) {
-                float mx = 0.f;
+            for (int k = 0; k < kMaxK; k++)
 #pragma unroll
                 for (int j = 0; j < kMaxK; j++)
-                    if (j != k && j < K)
-                        mx = fmaxf(mx, fabsf(cu.x[j] - cu.x[k]) + fabsf(cu.y[j] - cu.y[k]) + fabsf(cu.z[j] - cu.z[k]));
-                thr[k] = 3.f * mx + 1.f;
-            }
+                    thr[k][j] = (j == k || j >= K || k >= K)
+                                    ? -__builtin_inff()
+                                    : 3.f * (fabsf(cu.x[j] - cu.x[k]) + fabsf(cu.y[j] - cu.y[k]) +
+                                             fabsf(cu.z[j] - cu.z[k])) +
+                                          1.f;
             unsigned long long fails = 0;
             CubeEnt enext;
             enext.offset = 0;
@@ -521,13 +523,15 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
                     k = dv[2] == m1 ? 2 : k;
                     k = dv[1] == m1 ? 1 : k;
                     k = dv[0] == m1 ? 0 : k;
-                    float m2 = __builtin_inff(), t = thr[0];
+                    // every other centre j must be farther by more than T[k][j] at q
+                    pass = true;
 #pragma unroll
                     for (int j = 0; j < 5; j++) {
-                        m2 = j == k ? m2 : fminf(m2, dv[j]);
-                        t = j == k ? thr[j] : t;
+                        float t = thr[0][j];
+#pragma unroll
+                        for (int kk = 1; kk < 5; kk++) t = k == kk ? thr[kk][j] : t;
+                        pass = pass && (dv[j] - m1 > t);
                     }
-                    pass = m2 - m1 > t;
                 }
                 if (pass) {
                     const unsigned long long s = e.sums;

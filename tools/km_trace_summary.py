@@ -1,0 +1,44 @@
+#!/usr/bin/env python3
+"""Summarise an LLFE_KM_TRACE file (one line per k-means attempt, see llfe_api.cpp):
+per-phase times for the "photo" (U > 300k) and "ui" classes, Lloyd time per iteration,
+Lloyd bytes per iteration relative to a plain sweep, and the kernel span / CU balance.
+
+    python tools/km_trace_summary.py gpurun_out/km_trace.txt [launch_index]
+"""
+import sys
+
+import numpy as np
+
+
+def main():
+    path = sys.argv[1]
+    launch = int(sys.argv[2]) if len(sys.argv) > 2 else -1
+    a = np.loadtxt(path, dtype=np.int64)
+    n_att = 2560 if len(a) >= 2560 else len(a)
+    nl = len(a) // n_att
+    a = a[(launch % nl) * n_att:(launch % nl + 1) * n_att]
+    img, att, U, it, t0, t1, hw, xcc, tpp, tll, by = a.T
+    ok = it > 1
+    pp = (tpp - t0) / 100.0
+    ll = (tll - tpp) / 100.0
+    cp = (t1 - tll) / 100.0
+    ph = U > 300000
+    for name, m in [("photo", ph & ok), ("ui", ~ph & ok)]:
+        if not m.any():
+            continue
+        per = (by[m] - 4 * U[m] * 6) / (it[m] - 1)
+        print(f"{name:5s} n={m.sum():4d} U={U[m].mean():9.0f} iters={it[m].mean():5.1f}  PP {pp[m].mean()/1e3:6.3f} ms"
+              f"  Lloyd {ll[m].mean()/1e3:6.3f} ms ({(ll[m] / (it[m] - 1)).mean():6.1f} us/iter,"
+              f" {np.mean(per / (4 * U[m])):.3f} of a plain sweep's bytes)  compact {cp[m].mean()/1e3:6.3f} ms")
+    dur = (t1 - t0) / 100.0
+    cu = xcc * 1000 + ((hw >> 13) & 7) * 100 + ((hw >> 12) & 1) * 16 + ((hw >> 8) & 15)
+    busy = {}
+    for k, d in zip(cu, dur):
+        busy[k] = busy.get(k, 0.0) + d
+    b = np.array(list(busy.values())) / 1e3
+    print(f"span {(t1.max() - t0.min()) / 1e5:.2f} ms; per-CU busy min/mean/max {b.min():.2f}/{b.mean():.2f}/{b.max():.2f} ms;"
+          f" longest attempts (ms): {np.round(np.sort(dur)[-4:] / 1e3, 2)}")
+
+
+if __name__ == "__main__":
+    main()
