@@ -42,16 +42,242 @@ struct __align__(16) StencilSmem {
     float hf[BHT][TW];
 };
 
+// ---------------------------------------------------------------- interior tiles
+// Tiles whose whole window lies inside the image (88 % of a 1080p frame) need no
+// border handling: every stage works on 4 consecutive pixels per thread with dword /
+// 8-byte / 16-byte LDS accesses and no index clamping.  Window columns start at
+// tx0 - 8 (4-aligned), rows at ty0 - 7.
+constexpr int FGW = TW + 16;      // gray columns   x in [tx0 - 8, tx0 + 72)
+constexpr int FBW = TW + 12;      // hb/blur columns x in [tx0 - 6, tx0 + 70)
+constexpr int FMH = TH + 2, FMW = TW + 2;
+
+struct __align__(16) FastSmem {
+    uint32_t g[GH][FGW / 4];          // gray, 4 per dword
+    uint2 hb[GH][FBW / 4];            // horizontal blur5 sums, 4 x u16 per entry
+    uint32_t blur[BHT][FBW / 4];      // blurred gray rows y in [ty0 - 5, ty0 + 37)
+    uint16_t md[FMH][FMW + 2];        // |dx|+|dy| | NMS direction << 12, tile + 1 halo
+    float4 hf[BHT][TW / 4];           // CV_32F Gauss11 row pass
+};
+
+__device__ __forceinline__ uint32_t byte_of(uint32_t w, int i) { return (w >> (8 * i)) & 255u; }
+
+__device__ void stencil_interior(FastSmem &sm, const uint8_t *__restrict__ src, int H, int W, int tx0, int ty0,
+                                 uint8_t *__restrict__ cls, uint8_t *__restrict__ blurred_out,
+                                 unsigned long long *shadow_sum, unsigned long long *shadow_cnt,
+                                 const StencilParams &prm) {
+    const int tid = threadIdx.x;
+    // 1) gray: 4 BGR pixels (12 bytes, 3 dwords) -> one dword of gray
+    for (int u = tid; u < GH * (FGW / 4); u += NT) {
+        const int row = u / (FGW / 4), q = u - row * (FGW / 4);
+        const uint32_t *p = (const uint32_t *)(src + ((size_t)(ty0 - HG + row) * W + (tx0 - 8 + 4 * q)) * 3);
+        const uint32_t d0 = p[0], d1 = p[1], d2 = p[2];
+        const uint32_t b[12] = {byte_of(d0, 0), byte_of(d0, 1), byte_of(d0, 2), byte_of(d0, 3),
+                                byte_of(d1, 0), byte_of(d1, 1), byte_of(d1, 2), byte_of(d1, 3),
+                                byte_of(d2, 0), byte_of(d2, 1), byte_of(d2, 2), byte_of(d2, 3)};
+        uint32_t o = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            o |= ((b[3 * j] * 1868u + b[3 * j + 1] * 9617u + b[3 * j + 2] * 4899u + 8192u) >> 14) << (8 * j);
+        sm.g[row][q] = o;
+    }
+    __syncthreads();
+    // 2) horizontal blur5: hb col c <-> x = tx0 - 6 + c; taps are gray cols c .. c + 4
+    for (int u = tid; u < GH * (FBW / 4); u += NT) {
+        const int row = u / (FBW / 4), q = u - row * (FBW / 4);
+        const uint32_t w0 = sm.g[row][q], w1 = sm.g[row][q + 1];
+        uint32_t b[8];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            b[i] = byte_of(w0, i);
+            b[4 + i] = byte_of(w1, i);
+        }
+        uint32_t h[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) h[j] = 16u * (b[j] + b[j + 4]) + 64u * (b[j + 1] + b[j + 3]) + 96u * b[j + 2];
+        sm.hb[row][q] = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+    }
+    __syncthreads();
+    // 3) vertical blur5 -> blur rows ly (y = ty0 - 5 + ly) from hb rows ly .. ly + 4
+    for (int u = tid; u < BHT * (FBW / 4); u += NT) {
+        const int ly = u / (FBW / 4), q = u - ly * (FBW / 4);
+        uint32_t s[4] = {0, 0, 0, 0};
+        const uint32_t kw[5] = {16u, 64u, 96u, 64u, 16u};
+#pragma unroll
+        for (int r = 0; r < 5; r++) {
+            const uint2 v = sm.hb[ly + r][q];
+            s[0] += kw[r] * (v.x & 0xFFFFu);
+            s[1] += kw[r] * (v.x >> 16);
+            s[2] += kw[r] * (v.y & 0xFFFFu);
+            s[3] += kw[r] * (v.y >> 16);
+        }
+        uint32_t o = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) o |= ((s[j] + 32768u) >> 16) << (8 * j);
+        sm.blur[ly][q] = o;
+    }
+    __syncthreads();
+    // blur byte at tile-relative (row ly, col c) where c <-> x = tx0 - 6 + c
+    auto BL = [&](int ly, int c) -> int { return (int)byte_of(sm.blur[ly][c >> 2], c & 3); };
+
+    if (blurred_out) {
+        for (int u = tid; u < TH * (TW / 4); u += NT) {
+            const int y = u / (TW / 4), q = u - y * (TW / 4);
+            uint32_t o = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) o |= (uint32_t)BL(y + 5, 4 * q + j + 6) << (8 * j);
+            *(uint32_t *)(blurred_out + (size_t)(ty0 + y) * W + tx0 + 4 * q) = o;
+        }
+    }
+
+    if (cls) {
+        // 4) Sobel (no border inside), |dx|+|dy| and the NMS direction class, for the
+        //    tile + 1 halo: md row my <-> y = ty0 - 1 + my (blur row my + 4), col mc <->
+        //    x = tx0 - 1 + mc (blur col mc + 5)
+        constexpr int TG22 = 13573;
+        for (int u = tid; u < FMH * ((FMW + 3) / 4); u += NT) {
+            const int my = u / ((FMW + 3) / 4), q = u - my * ((FMW + 3) / 4);
+            int bv[3][6];
+#pragma unroll
+            for (int r = 0; r < 3; r++) {
+                const uint32_t a = sm.blur[my + 3 + r][q + 1], b2 = sm.blur[my + 3 + r][q + 2];
+                // blur cols 4q + 4 .. 4q + 9 = mag cols 4q - 1 .. 4q + 4 around 4q .. 4q + 3
+#pragma unroll
+                for (int i = 0; i < 4; i++) bv[r][i] = (int)byte_of(a, i);
+                bv[r][4] = (int)byte_of(b2, 0);
+                bv[r][5] = (int)byte_of(b2, 1);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int mc = 4 * q + j;
+                if (mc >= FMW) break;
+                const int gx = (bv[0][j + 2] + 2 * bv[1][j + 2] + bv[2][j + 2]) - (bv[0][j] + 2 * bv[1][j] + bv[2][j]);
+                const int gy = (bv[2][j] + 2 * bv[2][j + 1] + bv[2][j + 2]) - (bv[0][j] + 2 * bv[0][j + 1] + bv[0][j + 2]);
+                const int m = abs(gx) + abs(gy);
+                const int ax = abs(gx), ay = abs(gy) << 15, tg22x = ax * TG22;
+                int dir;
+                if (ay < tg22x) dir = 0;
+                else if (ay > tg22x + (ax << 16)) dir = 1;
+                else dir = (gx ^ gy) < 0 ? 2 : 3;
+                sm.md[my][mc] = (uint16_t)(m | (dir << 12));
+            }
+        }
+        __syncthreads();
+        // 5) NMS + double threshold on 4 consecutive pixels; one dword of classes out
+        constexpr int LOW = 50, HIGH = 150;
+        for (int u = tid; u < TH * (TW / 4); u += NT) {
+            const int ty = u / (TW / 4), q = u - ty * (TW / 4);
+            uint32_t o = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int tx = 4 * q + j;
+                const int v = sm.md[ty + 1][tx + 1];
+                const int m = v & 4095, dir = v >> 12;
+                uint32_t c = 1;
+                if (m > LOW) {
+                    bool keep;
+                    if (dir == 0) {
+                        keep = m > (sm.md[ty + 1][tx] & 4095) && m >= (sm.md[ty + 1][tx + 2] & 4095);
+                    } else if (dir == 1) {
+                        keep = m > (sm.md[ty][tx + 1] & 4095) && m >= (sm.md[ty + 2][tx + 1] & 4095);
+                    } else {
+                        const int sgn = dir == 2 ? -1 : 1;
+                        keep = m > (sm.md[ty][tx + 1 - sgn] & 4095) && m > (sm.md[ty + 2][tx + 1 + sgn] & 4095);
+                    }
+                    if (keep) c = m > HIGH ? 2u : 0u;
+                }
+                o |= c << (8 * j);
+            }
+            *(uint32_t *)(cls + (size_t)(ty0 + ty) * W + tx0 + 4 * q) = o;
+        }
+    }
+
+    if (shadow_sum) {
+        // 6) CV_32F row pass (fma chain left -> right) for 4 consecutive x = tx0 + 4q + j:
+        //    taps are blur cols 4q + 1 + j .. 4q + 11 + j (dwords q .. q + 3)
+        for (int u = tid; u < BHT * (TW / 4); u += NT) {
+            const int ly = u / (TW / 4), q = u - ly * (TW / 4);
+            float bvf[16];
+#pragma unroll
+            for (int d = 0; d < 4; d++) {
+                const uint32_t w = sm.blur[ly][q + d];
+#pragma unroll
+                for (int i = 0; i < 4; i++) bvf[4 * d + i] = (float)byte_of(w, i);
+            }
+            float out[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                float s = 0.0f;
+#pragma unroll
+                for (int k = 0; k < 11; k++) s = __builtin_fmaf(bvf[1 + j + k], prm.k11[k], s);
+                out[j] = s;
+            }
+            sm.hf[ly][q] = make_float4(out[0], out[1], out[2], out[3]);
+        }
+        __syncthreads();
+        // 7) column pass (centre, then symmetric pairs inner -> outer), cvRound, mask
+        unsigned long long lsum = 0, lcnt = 0;
+        for (int u = tid; u < TH * (TW / 4); u += NT) {
+            const int ty = u / (TW / 4), q = u - ty * (TW / 4);
+            const int ly = ty + 5;
+            const float4 c0 = sm.hf[ly][q];
+            float s[4] = {__builtin_fmaf(c0.x, prm.k11[5], 0.0f), __builtin_fmaf(c0.y, prm.k11[5], 0.0f),
+                          __builtin_fmaf(c0.z, prm.k11[5], 0.0f), __builtin_fmaf(c0.w, prm.k11[5], 0.0f)};
+#pragma unroll
+            for (int d = 1; d <= 5; d++) {
+                const float4 a = sm.hf[ly + d][q], b = sm.hf[ly - d][q];
+                s[0] = __builtin_fmaf(a.x + b.x, prm.k11[5 + d], s[0]);
+                s[1] = __builtin_fmaf(a.y + b.y, prm.k11[5 + d], s[1]);
+                s[2] = __builtin_fmaf(a.z + b.z, prm.k11[5 + d], s[2]);
+                s[3] = __builtin_fmaf(a.w + b.w, prm.k11[5 + d], s[3]);
+            }
+            const uint32_t bw = sm.blur[ly][q + 1], bw2 = sm.blur[ly][q + 2];
+            // blur cols for x = tx0 + 4q + j are 4q + 6 + j: bytes 2, 3 of dword q + 1, 0, 1 of q + 2
+            const int bv[4] = {(int)byte_of(bw, 2), (int)byte_of(bw, 3), (int)byte_of(bw2, 0), (int)byte_of(bw2, 1)};
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                int mean = (int)__builtin_rintf(s[j]);
+                mean = clampi(mean, 0, 255);
+                if (bv[j] - mean <= -2) {
+                    lsum += (unsigned)bv[j];
+                    lcnt += 1;
+                }
+            }
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            lsum += __shfl_xor(lsum, off);
+            lcnt += __shfl_xor(lcnt, off);
+        }
+        if ((tid & 63) == 0 && lcnt) {
+            atomicAdd(shadow_sum, lsum);
+            atomicAdd(shadow_cnt, lcnt);
+        }
+    }
+}
+
+union StencilShared {
+    StencilSmem g;
+    FastSmem f;
+};
+
 __global__ __launch_bounds__(NT) void k_stencil(const uint8_t *__restrict__ bgr, int H, int W, int ntx, int nty,
                                                 uint8_t *__restrict__ cls, uint8_t *__restrict__ blurred_out,
                                                 unsigned long long *__restrict__ shadow_sum,
                                                 unsigned long long *__restrict__ shadow_cnt, StencilParams prm) {
-    __shared__ StencilSmem sm;
+    __shared__ StencilShared shm;
     const int tid = threadIdx.x;
     const int img = blockIdx.y;
     const int t = blockIdx.x;
     const int tx0 = (t % ntx) * TW, ty0 = (t / ntx) * TH;
     const uint8_t *src = bgr + (size_t)img * H * W * 3;
+    const bool aligned = (((uintptr_t)bgr | (uintptr_t)cls | (uintptr_t)blurred_out) & 3) == 0 && (W & 3) == 0;
+    if (aligned && tx0 >= 8 && ty0 >= HG && tx0 + TW + 8 <= W && ty0 + TH + HG <= H) {
+        stencil_interior(shm.f, src, H, W, tx0, ty0, cls ? cls + (size_t)img * H * W : nullptr,
+                         blurred_out ? blurred_out + (size_t)img * H * W : nullptr,
+                         shadow_sum ? shadow_sum + img : nullptr, shadow_cnt ? shadow_cnt + img : nullptr, prm);
+        return;
+    }
+    StencilSmem &sm = shm.g;
 
     // 1) BGR window -> gray (Y = (1868 B + 9617 G + 4899 R + 2^13) >> 14)
     for (int i = tid; i < GH * GW; i += NT) {
