@@ -128,7 +128,6 @@ __device__ __forceinline__ int label5p(uint32_t key, const CentP &c) {
 }
 
 constexpr int PF = 4;  // steps of 16-B key loads kept in flight per wave
-constexpr int FQ = 8;  // boundary cubes labelled per round of the pruned sweep (16: no gain)
 
 // the 4 keys of lane `lane` in 256-point step `s` (zeros past the full steps)
 __device__ __forceinline__ uint4 load_step(const uint32_t *pts, int s, int se_full, int lane) {
@@ -165,6 +164,15 @@ struct KmSmem {
     int ci[3];
     int flag;
     unsigned long long fail_pts;  // keys read point by point in this Lloyd sweep
+    // cube-based k-means++ (pp_cubes)
+    unsigned long long psum[3][kParts];  // per trial and red-quarter partition: sum of T_j
+    unsigned long long pD[kParts];       // per partition: sum of D (the winning trial)
+    unsigned long long pex[3];
+    unsigned long long S[3];
+    uint32_t pbase[kParts + 1];          // first sorted key of each partition
+    int pj[3];
+    int icc[kMaxK][3];                   // chosen centres (integer colours)
+    unsigned long long sel_pts;          // colours the selection scans read
 };
 
 __device__ __forceinline__ Cent load_centres(const float (*c)[3]) {
@@ -182,6 +190,371 @@ __device__ __forceinline__ int moved_label(const KmSmem &sm, int i, int l) {
     for (int m = 0; m < sm.n_moved; m++)
         if (sm.moved_idx[m] == i) l = sm.moved_lbl[m];
     return l;
+}
+
+// ------------------------------------------------------------ cube-based k-means++
+// k-means++ centres are data points, so every distance it sums is an exact integer and
+// whole cubes can be summed in closed form: for a cube with origin o, n colours o + u
+// (u in [0,3]^3), S_u = sum u and S_u2 = sum |u|^2,
+//     sum |o + u - c|^2 = n |o - c|^2 + 2 (o - c) . S_u + S_u2.
+// d(p, a) - d(p, b) is linear in p, so its extremes over the cube are at corners:
+//     min = f(o) - 6 sum_d max(a_d - b_d, 0),  max = f(o) + 6 sum_d max(b_d - a_d, 0),
+// f(o) = d(o, a) - d(o, b).  A cube is "owned" by chosen centre k when no other chosen
+// centre is ever strictly closer (then D = d(., c_k) on it), and a trial t is decided on
+// it when it is never strictly closer than c_k (T = D) or always at least as close
+// (T = d(., t)).  Undecided cubes are summed colour by colour (enumerated from the
+// occupancy mask); the totals and therefore every choice are bit-identical to the
+// plain sweep.
+//
+// The selection prefix(D, i) >= p runs in np.unique order: the red-quarter partitions
+// are contiguous ranges of the sorted keys and unions of whole cubes (cube id = R << 12
+// | ...), so the partition holding p comes from per-partition cube totals and only that
+// partition's sorted keys are scanned.
+__device__ __forceinline__ int d2i(int x, int y, int z, int cx, int cy, int cz) {
+    const int a = x - cx, b = y - cy, c = z - cz;
+    return a * a + b * b + c * c;
+}
+
+struct ICent {
+    int x[kMaxK], y[kMaxK], z[kMaxK];
+};
+
+// d(p, a) >= d(p, b) for every p of the cube at origin o
+__device__ __forceinline__ bool never_closer(int ox, int oy, int oz, int ax, int ay, int az, int bx, int by, int bz) {
+    const int f = d2i(ox, oy, oz, ax, ay, az) - d2i(ox, oy, oz, bx, by, bz);
+    return f - 6 * (max(ax - bx, 0) + max(ay - by, 0) + max(az - bz, 0)) >= 0;
+}
+// d(p, a) <= d(p, b) for every p of the cube at origin o
+__device__ __forceinline__ bool always_closer(int ox, int oy, int oz, int ax, int ay, int az, int bx, int by, int bz) {
+    const int f = d2i(ox, oy, oz, ax, ay, az) - d2i(ox, oy, oz, bx, by, bz);
+    return f + 6 * (max(bx - ax, 0) + max(by - ay, 0) + max(bz - az, 0)) <= 0;
+}
+
+struct CubeGeo {  // origin, count, sums of u = colour - origin and of |u|^2
+    int ox, oy, oz, n, sx, sy, sz, s2;
+};
+
+// the colour of mask bit `bit` in the cube `id` (bit = i*16 + j*4 + b)
+__device__ __forceinline__ uint32_t cube_key(uint32_t id, int bit) {
+    return ((((id >> 12) & 63u) * 4u + (uint32_t)(bit >> 4)) << 16) |
+           ((((id >> 6) & 63u) * 4u + (uint32_t)((bit >> 2) & 3)) << 8) | ((id & 63u) * 4u + (uint32_t)(bit & 3));
+}
+__device__ __forceinline__ CubeGeo cube_geo(const CubeEnt &e) {
+    CubeGeo g;
+    g.ox = (int)((e.id >> 12) & 63u) * 4;
+    g.oy = (int)((e.id >> 6) & 63u) * 4;
+    g.oz = (int)(e.id & 63u) * 4;
+    g.n = (int)(e.sums & 127u);
+    g.sx = (int)((e.sums >> 7) & 255u);
+    g.sy = (int)((e.sums >> 15) & 255u);
+    g.sz = (int)(e.sums >> 23);
+    g.s2 = (int)(e.id >> 18);
+    return g;
+}
+__device__ __forceinline__ uint32_t cube_sum(const CubeGeo &g, int cx, int cy, int cz) {
+    const int ax = g.ox - cx, ay = g.oy - cy, az = g.oz - cz;
+    return (uint32_t)(g.n * (ax * ax + ay * ay + az * az) + 2 * (ax * g.sx + ay * g.sy + az * g.sz) + g.s2);
+}
+
+__device__ __forceinline__ int unpack_r(uint32_t k) { return (int)((k >> 16) & 255u); }
+__device__ __forceinline__ int unpack_g(uint32_t k) { return (int)((k >> 8) & 255u); }
+__device__ __forceinline__ int unpack_b(uint32_t k) { return (int)(k & 255u); }
+
+// D(p) = min over the first kk chosen centres (kk >= 1)
+__device__ __forceinline__ int dmin_chosen(int x, int y, int z, const ICent &ch, int kk) {
+    int d = d2i(x, y, z, ch.x[0], ch.y[0], ch.z[0]);
+#pragma unroll
+    for (int m = 1; m < kMaxK; m++)
+        if (m < kk) d = min(d, d2i(x, y, z, ch.x[m], ch.y[m], ch.z[m]));
+    return d;
+}
+
+__device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, int K, uint64_t &rng,
+                         const CubeEnt *__restrict__ ctab, int C, int cb,
+                         int cend, const uint32_t *__restrict__ part_uq, unsigned long long &bytes,
+                         uint32_t &pp_pts, uint32_t &pp_sel) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    if (wid == 0) {
+        const uint32_t v = part_uq[lane];
+        uint32_t x = v;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(x, off);
+            if (lane >= off) x += y;
+        }
+        sm.pbase[lane] = x - v;
+        if (lane == 63) sm.pbase[kParts] = x;
+    }
+    if (tid == 0) {
+        sm.fail_pts = 0;
+        sm.sel_pts = 0;
+    }
+    if (tid < kMaxK * 3) (&sm.icc[0][0])[tid] = 0;
+    {
+        const uint32_t q0 = pts[cvrng_next(rng) % (uint32_t)N];
+        if (tid == 0) {
+            sm.icc[0][0] = unpack_r(q0);
+            sm.icc[0][1] = unpack_g(q0);
+            sm.icc[0][2] = unpack_b(q0);
+        }
+    }
+    unsigned long long sum0 = 0;
+    for (int kk = 0; kk < K; kk++) {
+        __syncthreads();
+        ICent ch;  // chosen centres 0 .. kk-1 (uniform)
+#pragma unroll
+        for (int m = 0; m < kMaxK; m++) {
+            ch.x[m] = __builtin_amdgcn_readfirstlane(sm.icc[m][0]);
+            ch.y[m] = __builtin_amdgcn_readfirstlane(sm.icc[m][1]);
+            ch.z[m] = __builtin_amdgcn_readfirstlane(sm.icc[m][2]);
+        }
+        int tx[3], ty[3], tz[3];
+        if (kk == 0) {
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                tx[j] = ch.x[0];
+                ty[j] = ch.y[0];
+                tz[j] = ch.z[0];
+            }
+        } else {
+            double p[3];
+#pragma unroll
+            for (int j = 0; j < 3; j++) p[j] = cvrng_double(rng) * (double)sum0;
+            // ---- partition holding prefix(D) >= p_j
+            if (wid == 0) {
+                const unsigned long long v = sm.pD[lane];
+                unsigned long long x = v;
+#pragma unroll
+                for (int off = 1; off < 64; off <<= 1) {
+                    const unsigned long long y = __shfl_up(x, off);
+                    if (lane >= off) x += y;
+                }
+#pragma unroll
+                for (int j = 0; j < 3; j++) {
+                    const unsigned long long bal = __ballot((double)x >= p[j]);
+                    const int P = bal ? (int)__builtin_ctzll(bal) : 0;
+                    const unsigned long long ex = __shfl(x - v, P);
+                    if (lane == 0) {
+                        sm.pj[j] = !(p[j] > 0) ? -2 : (bal ? P : -1);
+                        sm.pex[j] = ex;
+                    }
+                }
+            }
+            __syncthreads();
+            // ---- waves 0..2 scan their partition's sorted keys for the first crossing
+            if (wid < 3) {
+                const int j = wid;
+                const double pj = j == 0 ? p[0] : (j == 1 ? p[1] : p[2]);
+                const int P = sm.pj[j];
+                int ci = P == -2 ? 0 : N - 1;
+                if (P >= 0) {
+                    const uint32_t a = sm.pbase[P], b = sm.pbase[P + 1];
+                    unsigned long long e = sm.pex[j];
+                    int found = -1;
+                    unsigned long long scanned = 0;
+                    for (uint32_t s0 = a; s0 < b && found < 0; s0 += STEP) {
+                        scanned += min((uint32_t)STEP, b - s0);
+                        const uint32_t i0 = s0 + (uint32_t)lane * 4;
+                        uint32_t dv[4], ls = 0;
+#pragma unroll
+                        for (int jj = 0; jj < 4; jj++) {
+                            dv[jj] = 0;
+                            if (i0 + jj < b) {
+                                const uint32_t k = pts[i0 + jj];
+                                dv[jj] = (uint32_t)dmin_chosen(unpack_r(k), unpack_g(k), unpack_b(k), ch, kk);
+                            }
+                            ls += dv[jj];
+                        }
+                        unsigned long long x = ls;
+#pragma unroll
+                        for (int off = 1; off < 64; off <<= 1) {
+                            const unsigned long long y = __shfl_up(x, off);
+                            if (lane >= off) x += y;
+                        }
+                        unsigned long long ee = e + x - ls;
+                        int hit = -1;
+#pragma unroll
+                        for (int jj = 0; jj < 4; jj++) {
+                            ee += dv[jj];
+                            if (hit < 0 && (double)ee >= pj) hit = jj;
+                        }
+                        const unsigned long long bal = __ballot(hit >= 0);
+                        if (bal) {
+                            const int first = (int)__builtin_ctzll(bal);
+                            found = (int)(s0 + (uint32_t)first * 4) + __shfl(hit, first);
+                        }
+                        e += __shfl(x, 63);
+                    }
+                    if (found >= 0) ci = min(found, N - 1);
+                    if (lane == 0) atomicAdd(&sm.sel_pts, scanned);
+                }
+                if (lane == 0) sm.pj[j] = ci;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                const uint32_t k = pts[sm.pj[j]];
+                tx[j] = unpack_r(k);
+                ty[j] = unpack_g(k);
+                tz[j] = unpack_b(k);
+            }
+        }
+        // ---- trial sums T_j = sum min(D, d(., t_j)) per partition (kk == 0: sum d(., c0))
+        if (tid < 3 * kParts) (&sm.psum[0][0])[tid] = 0;
+        __syncthreads();
+        unsigned long long acc0 = 0, acc1 = 0, acc2 = 0, fails = 0;
+        int Pcur = -1;
+        CubeEnt enext;
+        enext.mask = 0;
+        enext.id = 0;
+        enext.sums = 0;
+        if (cb + lane < cend) enext = ctab[cb + lane];
+        for (int base = cb; base < cend; base += 64) {
+            const int cidx = base + lane;
+            const bool valid = cidx < cend;
+            const CubeEnt e = enext;
+            if (cidx + 64 < cend) enext = ctab[cidx + 64];
+            const CubeGeo g = cube_geo(e);
+            const int P = valid ? (int)((e.id >> 12) & 63u) : kParts;
+            uint32_t v0 = 0, v1 = 0, v2 = 0;
+            bool fail = false;
+            if (valid) {
+                if (kk == 0) {
+                    v0 = cube_sum(g, tx[0], ty[0], tz[0]);
+                } else {
+                    // owner candidate: nearest chosen centre to the cube centre o + 1.5
+                    const int qx = 2 * g.ox + 3, qy = 2 * g.oy + 3, qz = 2 * g.oz + 3;
+                    int k = 0, bd = d2i(qx, qy, qz, 2 * ch.x[0], 2 * ch.y[0], 2 * ch.z[0]);
+#pragma unroll
+                    for (int m = 1; m < kMaxK; m++) {
+                        if (m >= kk) break;
+                        const int d = d2i(qx, qy, qz, 2 * ch.x[m], 2 * ch.y[m], 2 * ch.z[m]);
+                        if (d < bd) {
+                            bd = d;
+                            k = m;
+                        }
+                    }
+                    int kx = ch.x[0], ky = ch.y[0], kz = ch.z[0];
+#pragma unroll
+                    for (int m = 1; m < kMaxK; m++) {
+                        kx = k == m ? ch.x[m] : kx;
+                        ky = k == m ? ch.y[m] : ky;
+                        kz = k == m ? ch.z[m] : kz;
+                    }
+                    bool owned = true;
+#pragma unroll
+                    for (int m = 0; m < kMaxK; m++) {
+                        if (m >= kk) break;
+                        if (m != k) owned = owned && never_closer(g.ox, g.oy, g.oz, ch.x[m], ch.y[m], ch.z[m], kx, ky, kz);
+                    }
+                    const uint32_t ds = cube_sum(g, kx, ky, kz);
+                    uint32_t vv[3];
+                    bool dec = owned;
+#pragma unroll
+                    for (int j = 0; j < 3; j++) {
+                        const bool A = never_closer(g.ox, g.oy, g.oz, tx[j], ty[j], tz[j], kx, ky, kz);
+                        const bool B = always_closer(g.ox, g.oy, g.oz, tx[j], ty[j], tz[j], kx, ky, kz);
+                        dec = dec && (A || B);
+                        vv[j] = A ? ds : cube_sum(g, tx[j], ty[j], tz[j]);
+                    }
+                    v0 = vv[0];
+                    v1 = vv[1];
+                    v2 = vv[2];
+                    fail = !dec;
+                }
+            }
+            // lanes hold ascending cube ids: visit the batch's partitions in order
+            int Pseg = __shfl(P, 0);
+            for (;;) {
+                if (Pseg != Pcur) {
+                    if (Pcur >= 0) {
+                        const unsigned long long a0 = wave_sum(acc0), a1 = wave_sum(acc1), a2 = wave_sum(acc2);
+                        if (lane == 0) {
+                            atomicAdd(&sm.psum[0][Pcur], a0);
+                            atomicAdd(&sm.psum[1][Pcur], a1);
+                            atomicAdd(&sm.psum[2][Pcur], a2);
+                        }
+                    }
+                    acc0 = acc1 = acc2 = 0;
+                    Pcur = Pseg;
+                }
+                const bool mine = P == Pseg;
+                if (mine && !fail) {
+                    acc0 += v0;
+                    acc1 += v1;
+                    acc2 += v2;
+                }
+                // undecided cubes, one per round: lane = mask bit = colour of the cube
+                unsigned long long fm = __ballot(mine && fail);
+                while (fm) {
+                    const int src = __builtin_ctzll(fm);
+                    fm &= fm - 1;
+                    const unsigned long long m = __shfl(e.mask, src);
+                    const uint32_t id = (uint32_t)__shfl((int)e.id, src);
+                    if ((m >> lane) & 1ull) {
+                        const uint32_t kq = cube_key(id, lane);
+                        const int x = unpack_r(kq), y = unpack_g(kq), z = unpack_b(kq);
+                        const int D = dmin_chosen(x, y, z, ch, kk);
+                        acc0 += (uint32_t)min(D, d2i(x, y, z, tx[0], ty[0], tz[0]));
+                        acc1 += (uint32_t)min(D, d2i(x, y, z, tx[1], ty[1], tz[1]));
+                        acc2 += (uint32_t)min(D, d2i(x, y, z, tx[2], ty[2], tz[2]));
+                    }
+                    fails += (unsigned long long)__popcll(m);
+                }
+                const unsigned long long rest = __ballot(P > Pseg && P < kParts);
+                if (!rest) break;
+                Pseg = __shfl(P, (int)__builtin_ctzll(rest));
+            }
+        }
+        if (Pcur >= 0) {
+            const unsigned long long a0 = wave_sum(acc0), a1 = wave_sum(acc1), a2 = wave_sum(acc2);
+            if (lane == 0) {
+                atomicAdd(&sm.psum[0][Pcur], a0);
+                atomicAdd(&sm.psum[1][Pcur], a1);
+                atomicAdd(&sm.psum[2][Pcur], a2);
+            }
+        }
+        if (lane == 0 && fails) atomicAdd(&sm.fail_pts, fails);
+        __syncthreads();
+        if (wid == 0) {
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                const unsigned long long s = wave_sum(sm.psum[j][lane]);
+                if (lane == 0) sm.S[j] = s;
+            }
+        }
+        __syncthreads();
+        int best = 0;
+        if (kk > 0) {
+            double bs = 1.7976931348623157e308;
+            for (int j = 0; j < 3; j++)
+                if ((double)sm.S[j] < bs) {
+                    bs = (double)sm.S[j];
+                    best = j;
+                }
+        }
+        sum0 = sm.S[best];
+        if (tid < kParts) sm.pD[tid] = sm.psum[best][tid];
+        if (tid == 0 && kk > 0) {
+            sm.icc[kk][0] = best == 0 ? tx[0] : (best == 1 ? tx[1] : tx[2]);
+            sm.icc[kk][1] = best == 0 ? ty[0] : (best == 1 ? ty[1] : ty[2]);
+            sm.icc[kk][2] = best == 0 ? tz[0] : (best == 1 ? tz[1] : tz[2]);
+        }
+    }
+    __syncthreads();
+    if (tid < kMaxK * 3) {
+        const int k = tid / 3, j = tid % 3;
+        sm.cc[k][j] = k < K ? (float)sm.icc[k][j] : kFar;
+    }
+    if (tid == 0) {
+        // K passes over the cube table + colours read one by one (undecided cubes and
+        // the partition scans)
+        bytes += 16ull * (unsigned long long)C * (unsigned long long)K + 4ull * sm.sel_pts;
+        pp_pts = (uint32_t)sm.fail_pts;
+        pp_sel = (uint32_t)sm.sel_pts;
+        sm.fail_pts = 0;
+    }
+    __syncthreads();
 }
 
 __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys, long long key_stride,
@@ -211,6 +584,8 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
             o->compactness = 0.0;
             o->iters = 0;
             o->bytes = 0;
+            o->pp_pts = 0;
+            o->n_cubes = 0;
             o->t_end = wall_clock64();
         }
         return;
@@ -225,13 +600,14 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
     uint32_t *ss = scratch + ((size_t)img * kAttempts + att) * (size_t)scratch_stride;
     // cube-pruned Lloyd sweeps (when the cube table was built): waves own contiguous
     // ranges of cubes
-    const bool use_cubes = cubes.ckeys != nullptr;
+    const bool use_cubes = cubes.cubes != nullptr;
     const int C = use_cubes ? cubes.n_cubes[img] : 0;
     const CubeEnt *ctab = use_cubes ? cubes.cubes + (size_t)img * cubes.cube_stride : nullptr;
-    const uint32_t *ckp = use_cubes ? cubes.ckeys + (size_t)img * key_stride : nullptr;
     const int Cw = (C + KW - 1) / KW;
     const int cb = min(C, wid * Cw), cend = min(C, cb + Cw);
-    unsigned long long bytes = 4ull * (unsigned long long)N * (unsigned long long)(K + 1);  // PP + compactness
+    uint32_t pp_pts = 0, pp_sel = 0;
+    // compactness + (plain path) k-means++; the cube path adds what its passes read
+    unsigned long long bytes = 4ull * (unsigned long long)N * (unsigned long long)(use_cubes ? 1 : K + 1);
     if (tid == 0) sm.fail_pts = 0;
 #define SSLOT(slot) (ss + (size_t)(slot) * (size_t)M)
 
@@ -240,6 +616,9 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
     for (int q = 0, skip = att * (1 + 6 * (K - 1)); q < skip; q++) cvrng_next(rng);
 
     // ------------------------------------------------ k-means++ (generateCentersPP)
+    if (use_cubes) {
+        pp_cubes(sm, pts, N, K, rng, ctab, C, cb, cend, cubes.part_uq + (size_t)img * kParts, bytes, pp_pts, pp_sel);
+    } else {
     int cur = 0;
     {
         const uint32_t c0 = cvrng_next(rng) % (uint32_t)N;
@@ -452,6 +831,7 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
         __syncthreads();
     }
 
+    }  // k-means++
     if (tid == 0) o->t_pp = wall_clock64();
     // ------------------------------------------------ Lloyd iterations
     if (tid < kMaxK * 3) {
@@ -492,7 +872,7 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
                                           1.f;
             unsigned long long fails = 0;
             CubeEnt enext;
-            enext.offset = 0;
+            enext.mask = 0;
             enext.id = 0;
             enext.sums = 0;
             if (cb + lane < cend) enext = ctab[cb + lane];
@@ -504,7 +884,7 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
                 bool pass = false;
                 int k = 0;
                 if (valid) {
-                    const float qx = (float)(e.id >> 12) * 4.f + 1.5f, qy = (float)((e.id >> 6) & 63u) * 4.f + 1.5f,
+                    const float qx = (float)((e.id >> 12) & 63u) * 4.f + 1.5f, qy = (float)((e.id >> 6) & 63u) * 4.f + 1.5f,
                                 qz = (float)(e.id & 63u) * 4.f + 1.5f;
                     const f2 px = f2{qx, qx}, py = f2{qy, qy}, pz = f2{qz, qz};
                     f2 d[3];
@@ -534,40 +914,28 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
                     }
                 }
                 if (pass) {
-                    const unsigned long long s = e.sums;
-                    atomicAdd(&sm.accA[k][tid], (s & 0xFFFFull) | (((s >> 16) & 0xFFFFull) << 32));
-                    atomicAdd(&sm.accB[k][tid], ((s >> 32) & 0xFFFFull) | ((s >> 48) << 32));
+                    const CubeGeo g = cube_geo(e);
+                    atomicAdd(&sm.accA[k][tid], (unsigned long long)(g.n * g.ox + g.sx) |
+                                                    ((unsigned long long)(g.n * g.oy + g.sy) << 32));
+                    atomicAdd(&sm.accB[k][tid], (unsigned long long)(g.n * g.oz + g.sz) |
+                                                    ((unsigned long long)g.n << 32));
                 }
-                // cubes straddling a boundary: one key per lane, FQ cubes per round so
-                // that FQ independent key loads are in flight (a cube at a time would
-                // serialise one memory latency per cube)
+                // cubes straddling a boundary, one per round: lane = mask bit = colour
+                // (no key loads: the colours are enumerated from the occupancy mask)
                 unsigned long long fm = __ballot(valid && !pass);
-                const uint32_t cnt_mine = (uint32_t)(e.sums >> 48);
                 while (fm) {
-                    uint32_t off[FQ], cnt[FQ], kq[FQ];
-#pragma unroll
-                    for (int u = 0; u < FQ; u++) {
-                        cnt[u] = 0;
-                        off[u] = 0;
-                        if (fm) {
-                            const int src = __builtin_ctzll(fm);
-                            fm &= fm - 1;
-                            off[u] = (uint32_t)__shfl((int)e.offset, src);
-                            cnt[u] = (uint32_t)__shfl((int)cnt_mine, src);
-                        }
+                    const int src = __builtin_ctzll(fm);
+                    fm &= fm - 1;
+                    const unsigned long long m = __shfl(e.mask, src);
+                    const uint32_t id = (uint32_t)__shfl((int)e.id, src);
+                    if ((m >> lane) & 1ull) {
+                        const uint32_t kq = cube_key(id, lane);
+                        const int l = label5p(kq, c);
+                        atomicAdd(&sm.accA[l][tid], (unsigned long long)((kq >> 16) & 255u) |
+                                                        ((unsigned long long)((kq >> 8) & 255u) << 32));
+                        atomicAdd(&sm.accB[l][tid], (unsigned long long)(kq & 255u) | (1ull << 32));
                     }
-#pragma unroll
-                    for (int u = 0; u < FQ; u++) kq[u] = (uint32_t)lane < cnt[u] ? ckp[off[u] + lane] : 0u;
-#pragma unroll
-                    for (int u = 0; u < FQ; u++) {
-                        if ((uint32_t)lane < cnt[u]) {
-                            const int l = label5p(kq[u], c);
-                            atomicAdd(&sm.accA[l][tid], (unsigned long long)((kq[u] >> 16) & 255u) |
-                                                            ((unsigned long long)((kq[u] >> 8) & 255u) << 32));
-                            atomicAdd(&sm.accB[l][tid], (unsigned long long)(kq[u] & 255u) | (1ull << 32));
-                        }
-                        fails += cnt[u];
-                    }
+                    fails += (unsigned long long)__popcll(m);
                 }
             }
             if (lane == 0 && fails) atomicAdd(&sm.fail_pts, fails);
@@ -614,7 +982,7 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
         __syncthreads();
         if (tid == 0) {
             if (use_cubes) {
-                bytes += 16ull * (unsigned long long)C + 4ull * sm.fail_pts;
+                bytes += 16ull * (unsigned long long)C;  // boundary colours come from the masks
                 sm.fail_pts = 0;
             } else {
                 bytes += 4ull * (unsigned long long)N;
@@ -770,6 +1138,9 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
             o->compactness = compactness;
             o->iters = iter;
             o->bytes = bytes;
+            o->pp_pts = pp_pts;
+            o->pad = (int32_t)pp_sel;
+            o->n_cubes = (uint32_t)C;
             o->t_end = wall_clock64();
             for (int k = 0; k < kMaxK; k++) {
                 for (int j = 0; j < 3; j++) o->centers[k][j] = k < K ? sm.c[k][j] : 0.f;

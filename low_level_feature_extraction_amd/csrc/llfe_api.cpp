@@ -206,7 +206,7 @@ struct Work {
     DevBuf<unsigned long long> d_shadow;
     DevBuf<int> d_order, d_parent, d_nroots;
     DevBuf<uint16_t> d_lab, d_roots;
-    DevBuf<uint32_t> d_raw, d_keys, d_kscratch, d_ckeys, d_pmeta;
+    DevBuf<uint32_t> d_raw, d_keys, d_kscratch, d_pmeta;
     DevBuf<CubeEnt> d_segcubes, d_cubes;
     DevBuf<int32_t> d_ncubes;
     DevBuf<int64_t> d_nuniq;
@@ -401,7 +401,6 @@ int color_stage(llfe_ctx *ctx, Work &W, const uint8_t *img, const int8_t *noise,
     const int64_t cube_stride = std::min<int64_t>(key_stride, kMaxCubes);
     HIPCHK(ctx, W.d_raw.ensure((size_t)n * key_stride));
     HIPCHK(ctx, W.d_keys.ensure((size_t)n * key_stride));
-    HIPCHK(ctx, W.d_ckeys.ensure((size_t)n * key_stride));
     HIPCHK(ctx, W.d_segcubes.ensure((size_t)n * kParts * kCubesPerPart));
     HIPCHK(ctx, W.d_cubes.ensure((size_t)n * cube_stride));
     HIPCHK(ctx, W.d_pmeta.ensure((size_t)n * kParts * 4));
@@ -416,7 +415,7 @@ int color_stage(llfe_ctx *ctx, Work &W, const uint8_t *img, const int8_t *noise,
           launch_uq_scatter(W.d_raw.p, n, P, key_stride, hist, cursor, W.d_keys.p, s));
     // the partitions' sorted unique keys overwrite the (dead) raw keys
     TIMED(ctx, s, "k_uq_part", (double)n * P * 4,
-          launch_uq_part(W.d_keys.p, n, key_stride, hist, W.d_raw.p, W.d_ckeys.p, W.d_segcubes.p, uq, cc,
+          launch_uq_part(W.d_keys.p, n, key_stride, hist, W.d_raw.p, W.d_segcubes.p, uq, cc,
                          s));
     TIMED(ctx, s, "k_uq_gather", 0,
           launch_uq_gather(W.d_raw.p, n, key_stride, hist, uq, cc, W.d_segcubes.p, W.d_keys.p, W.d_cubes.p,
@@ -447,9 +446,9 @@ int kmeans_stage(llfe_ctx *ctx, Work &W, const uint32_t *keys, int64_t key_strid
             for (int i = 0; i < n; i++)
                 for (int a = 0; a < kAttempts; a++) {
                     const KmeansAttemptOut &o = att[(size_t)i * kAttempts + a];
-                    fprintf(f, "%d %d %lld %d %llu %llu %u %u %llu %llu %llu\n", i, a, (long long)nu[i], o.iters,
+                    fprintf(f, "%d %d %lld %d %llu %llu %u %u %llu %llu %llu %u %u %d\n", i, a, (long long)nu[i], o.iters,
                             (unsigned long long)o.t_start, (unsigned long long)o.t_end, o.hw_id, o.xcc_id,
-                            (unsigned long long)o.t_pp, (unsigned long long)o.t_lloyd, (unsigned long long)o.bytes);
+                            (unsigned long long)o.t_pp, (unsigned long long)o.t_lloyd, (unsigned long long)o.bytes, o.pp_pts, o.n_cubes, o.pad);
                 }
             fclose(f);
         }
@@ -513,8 +512,8 @@ int enqueue_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_
     if (want_col) {
         rc = color_stage(ctx, W, img, noise, n, h, w, seed, b->index_base + i0, s);
         if (rc) return rc;
-        const KmeansCubes cubes{W.d_ckeys.p, W.d_cubes.p, std::min<int64_t>(key_stride, kMaxCubes),
-                                W.d_ncubes.p};
+        const KmeansCubes cubes{W.d_cubes.p, std::min<int64_t>(key_stride, kMaxCubes), W.d_ncubes.p,
+                                W.d_pmeta.p + (size_t)2 * n * kParts};
         rc = kmeans_stage(ctx, W, W.d_keys.p, key_stride, W.d_nuniq.p, n, b->n_colors ? b->n_colors : kMaxK, seed,
                           b->index_base + i0, cubes, s);
         if (rc) return rc;
@@ -791,7 +790,7 @@ int llfe_kmeans(llfe_ctx *ctx, const uint32_t *keys, int64_t key_stride, const i
     Work &W = ctx->ws[0];
     HIPCHK(ctx, W.d_nuniq.ensure(n));
     HIPCHK(ctx, hipMemcpyAsync(W.d_nuniq.p, n_points, sizeof(int64_t) * n, hipMemcpyHostToDevice, s));
-    const KmeansCubes none{nullptr, nullptr, 0, nullptr};  // plain sweeps over caller-supplied keys
+    const KmeansCubes none{nullptr, 0, nullptr, nullptr};  // plain sweeps over caller-supplied keys
     int rc = kmeans_stage(ctx, W, keys, key_stride, W.d_nuniq.p, n, n_colors, seed, index_base, none, s);
     if (rc) return rc;
     HIPCHK(ctx, ctx->h_kout.ensure(n));

@@ -57,6 +57,7 @@ struct KmeansAttemptOut {
     // workgroup timeline (s_memrealtime, 100 MHz) and placement, for LLFE_KM_TRACE
     uint64_t t_start, t_pp, t_lloyd, t_end;  // start, k-means++ done, Lloyd done, end
     uint32_t hw_id, xcc_id;
+    uint32_t pp_pts, n_cubes;  // colours k-means++ read one by one; cube count
 };
 
 struct KmeansImageOut {
@@ -69,27 +70,29 @@ struct KmeansImageOut {
     uint64_t bytes;  // algorithmic bytes read, summed over the attempts (roofline)
 };
 
-// Lloyd pruning by 4x4x4 colour cubes: the unique keys regrouped cube by cube, with a
-// per-cube entry holding where its keys start and their exact coordinate sums.
-// A cube whose whole box provably has one label (margin test) is accumulated from its
-// sums; the others are labelled point by point -- the labels are OpenCV's either way.
+// k-means pruning by 4x4x4 colour cubes: one 16-byte entry per occupied cube holds its
+// occupancy mask and the exact sums of its colours.  A cube whose whole box provably
+// has one label (margin test) is accumulated from its sums; the colours of the others
+// are enumerated from the mask and labelled one by one -- OpenCV's labels either way.
 struct CubeEnt {
-    uint32_t offset;  // first key of the cube in the cube-ordered key array
-    uint32_t id;      // R << 12 | G << 6 | B (cube = [4R, 4R+3] x [4G, 4G+3] x [4B, 4B+3])
-    uint64_t sums;    // sum r | sum g << 16 | sum b << 32 | count << 48
+    uint64_t mask;  // bit i*16 + j*4 + b: colour (4R + i, 4G + j, 4B + b) is present
+    uint32_t id;    // R << 12 | G << 6 | B (cube = [4R, 4R+3] x [4G, 4G+3] x [4B, 4B+3]) in bits 0..17,
+                    // sum over the cube's colours u = colour - origin of |u|^2 (<= 1728) in bits 18..28
+    uint32_t sums;  // count (<= 64) | sum u_r << 7 | sum u_g << 15 | sum u_b << 23 (each <= 192)
 };
+static_assert(sizeof(CubeEnt) == 16, "CubeEnt is one 16-byte load");
 constexpr int kMaxCubes = 1 << 18;
 struct KmeansCubes {
-    const uint32_t *ckeys;  // per image (key_stride): keys in cube order (nullptr: no pruning)
-    const CubeEnt *cubes;   // per image (cube_stride) entries in cube-id order
+    const CubeEnt *cubes;   // per image (cube_stride) entries in cube-id order (nullptr: no pruning)
     int64_t cube_stride;
     const int32_t *n_cubes;
+    const uint32_t *part_uq;  // per image: unique colours per red-quarter partition (kParts)
 };
 // Unique colours (unique.hip), all per image with stride key_stride (u32 keys):
 //   keys:    pixels -> noised keys into `raw`, partition histogram `hist` (n x 64, zeroed)
 //   scatter: raw -> `part` grouped by partition (`cursor` n x 64, zeroed)
 //   part:    per (image, partition): sorted unique keys -> `skeys` (may alias raw),
-//            cube-ordered keys -> `ckeys`, cube entries -> `seg_cubes` (n x 64 x 4096),
+//            cube entries -> `seg_cubes` (n x 64 x 4096),
 //            counts -> uq, cc (n x 64)
 //   gather:  contiguous sorted keys -> `keys` (may alias part), cube table -> `cubes`,
 //            n_unique, n_cubes
@@ -98,7 +101,7 @@ hipError_t launch_uq_keys(const uint8_t *bgr, const int8_t *noise, int n, int h,
 hipError_t launch_uq_scatter(const uint32_t *raw, int n, int64_t P, int64_t key_stride, const uint32_t *hist,
                              uint32_t *cursor, uint32_t *part, hipStream_t s);
 hipError_t launch_uq_part(const uint32_t *part, int n, int64_t key_stride, const uint32_t *hist, uint32_t *skeys,
-                          uint32_t *ckeys, CubeEnt *seg_cubes, uint32_t *uq, uint32_t *cc, hipStream_t s);
+                          CubeEnt *seg_cubes, uint32_t *uq, uint32_t *cc, hipStream_t s);
 hipError_t launch_uq_gather(const uint32_t *skeys, int n, int64_t key_stride, const uint32_t *hist, const uint32_t *uq,
                             const uint32_t *cc, const CubeEnt *seg_cubes, uint32_t *keys, CubeEnt *cubes,
                             int64_t cube_stride, int64_t *n_unique, int32_t *n_cubes, hipStream_t s);

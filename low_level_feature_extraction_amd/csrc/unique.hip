@@ -12,10 +12,10 @@
 //   k_uq_scatter  counting sort of the keys by R (block-local LDS sort, 64 global
 //                 cursors per image, coalesced runs out)
 //   k_uq_part     one 1024-thread workgroup per (image, R): LDS bitmap of the partition's
-//                 4 x 256 x 256 colours -> its sorted unique keys, its cubes and the cube-
-//                 ordered keys (written in place of the partition)
+//                 4 x 256 x 256 colours -> its sorted unique keys (written in place of the
+//                 partition) and its 4x4x4 cubes (occupancy mask + exact sums, CubeEnt)
 //   k_uq_gather   per image: prefix over the partitions, contiguous sorted keys + cube
-//                 table (cube offsets keep pointing into the partitioned cube keys)
+//                 table
 #include <algorithm>
 
 #include "llfe_internal.h"
@@ -244,11 +244,11 @@ __device__ __forceinline__ unsigned long long scan_u64_1024(unsigned long long v
 }
 
 // grid (64, n).  Reads the partition's keys from `part`, writes (in place of those
-// keys, so capacity is the partition size) the sorted unique keys to `skeys` and the
-// cube-ordered keys to `ckeys`, and up to 4096 cube entries to `seg_cubes`.
+// keys, so capacity is the partition size) the sorted unique keys to `skeys`, and up
+// to 4096 cube entries to `seg_cubes`.
 __global__ __launch_bounds__(UT) void k_uq_part(const uint32_t *__restrict__ part, long long key_stride,
                                                 const uint32_t *__restrict__ hist, uint32_t *__restrict__ skeys,
-                                                uint32_t *__restrict__ ckeys, CubeEnt *__restrict__ seg_cubes,
+                                                CubeEnt *__restrict__ seg_cubes,
                                                 uint32_t *__restrict__ uq, uint32_t *__restrict__ cc) {
     __shared__ __attribute__((aligned(16))) uint32_t W[4 * 2048];  // rows r = 4R + i, word g << 3 | b >> 5
     __shared__ unsigned long long tmp[UT / 64];
@@ -318,39 +318,43 @@ __global__ __launch_bounds__(UT) void k_uq_part(const uint32_t *__restrict__ par
                 for (int j = 0; j < 4; j++)
                     m |= (unsigned long long)((w[i][j] >> (sh0 + 4 * c)) & 15u) << (i * 16 + j * 4);
             mask[c] = m;
-            mine += m ? (1ull << 32) + (unsigned long long)__popcll(m) : 0ull;
+            mine += m ? 1ull : 0ull;
         }
         unsigned long long tot;
-        const unsigned long long pos = scan_u64_1024(mine, tmp, &tot);
-        uint32_t ci = (uint32_t)(pos >> 32), pi = (uint32_t)pos;
+        uint32_t ci = (uint32_t)scan_u64_1024(mine, tmp, &tot);
         CubeEnt *ce = seg_cubes + ((size_t)img * NPART + R) * 4096;
-        uint32_t *ck = ckeys + (size_t)img * key_stride + start;
 #pragma unroll
         for (int c = 0; c < 4; c++) {
             const unsigned long long m = mask[c];
             if (!m) continue;
             const int B = B0 + c;
             const uint32_t n = (uint32_t)__popcll(m);
-            uint32_t sr = 4u * R * n, sg = 4u * G * n, sb = 4u * B * n;
+            uint32_t sr = 0, sg = 0, sb = 0, su2 = 0;  // over u = colour - cube origin
 #pragma unroll
-            for (int i = 1; i < 4; i++) sr += i * (uint32_t)__popcll(m & (0xFFFFull << (16 * i)));
-#pragma unroll
-            for (int j = 1; j < 4; j++) sg += j * (uint32_t)__popcll(m & (0x000F000F000F000Full << (4 * j)));
-#pragma unroll
-            for (int bb = 1; bb < 4; bb++) sb += bb * (uint32_t)__popcll(m & (0x1111111111111111ull << bb));
-            CubeEnt e;
-            e.offset = start + pi;
-            e.id = ((uint32_t)R << 12) | ((uint32_t)G << 6) | (uint32_t)B;
-            e.sums = (unsigned long long)sr | ((unsigned long long)sg << 16) | ((unsigned long long)sb << 32) |
-                     ((unsigned long long)n << 48);
-            ce[ci++] = e;
-            for (unsigned long long mm = m; mm; mm &= mm - 1) {
-                const int bit = __builtin_ctzll(mm);
-                ck[pi++] = ((uint32_t)(4 * R + (bit >> 4)) << 16) | ((uint32_t)(4 * G + ((bit >> 2) & 3)) << 8) |
-                           (uint32_t)(4 * B + (bit & 3));
+            for (int i = 1; i < 4; i++) {
+                const uint32_t c = (uint32_t)__popcll(m & (0xFFFFull << (16 * i)));
+                sr += i * c;
+                su2 += i * i * c;
             }
+#pragma unroll
+            for (int j = 1; j < 4; j++) {
+                const uint32_t c = (uint32_t)__popcll(m & (0x000F000F000F000Full << (4 * j)));
+                sg += j * c;
+                su2 += j * j * c;
+            }
+#pragma unroll
+            for (int bb = 1; bb < 4; bb++) {
+                const uint32_t c = (uint32_t)__popcll(m & (0x1111111111111111ull << bb));
+                sb += bb * c;
+                su2 += bb * bb * c;
+            }
+            CubeEnt e;
+            e.mask = m;
+            e.id = ((uint32_t)R << 12) | ((uint32_t)G << 6) | (uint32_t)B | (su2 << 18);
+            e.sums = n | (sr << 7) | (sg << 15) | (sb << 23);
+            ce[ci++] = e;
         }
-        if (t == 0) cc[(size_t)img * NPART + R] = (uint32_t)(tot >> 32);
+        if (t == 0) cc[(size_t)img * NPART + R] = (uint32_t)tot;
     }
 }
 
@@ -425,8 +429,8 @@ hipError_t launch_uq_scatter(const uint32_t *keys, int n, int64_t P, int64_t key
 }
 
 hipError_t launch_uq_part(const uint32_t *part, int n, int64_t key_stride, const uint32_t *hist, uint32_t *skeys,
-                          uint32_t *ckeys, CubeEnt *seg_cubes, uint32_t *uq, uint32_t *cc, hipStream_t s) {
-    hipLaunchKernelGGL(k_uq_part, dim3(NPART, n), dim3(UT), 0, s, part, (long long)key_stride, hist, skeys, ckeys,
+                          CubeEnt *seg_cubes, uint32_t *uq, uint32_t *cc, hipStream_t s) {
+    hipLaunchKernelGGL(k_uq_part, dim3(NPART, n), dim3(UT), 0, s, part, (long long)key_stride, hist, skeys,
                        seg_cubes, uq, cc);
     return hipGetLastError();
 }
