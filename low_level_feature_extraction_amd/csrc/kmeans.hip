@@ -173,6 +173,8 @@ struct KmSmem {
     int pj[3];
     int icc[kMaxK][3];                   // chosen centres (integer colours)
     unsigned long long sel_pts;          // colours the selection scans read
+    unsigned long long wchunk[3][KW];    // per trial: sum of D over each wave's chunk
+    unsigned long long qtot;             // sum of |p|^2 over all colours (exact)
 };
 
 __device__ __forceinline__ Cent load_centres(const float (*c)[3]) {
@@ -272,7 +274,7 @@ __device__ __forceinline__ int dmin_chosen(int x, int y, int z, const ICent &ch,
 __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, int K, uint64_t &rng,
                          const CubeEnt *__restrict__ ctab, int C, int cb,
                          int cend, const uint32_t *__restrict__ part_uq, unsigned long long &bytes,
-                         uint32_t &pp_pts, uint32_t &pp_sel) {
+                         uint32_t &pp_pts, uint32_t &pp_sel, uint64_t &t_sel) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     if (wid == 0) {
         const uint32_t v = part_uq[lane];
@@ -288,6 +290,7 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
     if (tid == 0) {
         sm.fail_pts = 0;
         sm.sel_pts = 0;
+        sm.qtot = 0;
     }
     if (tid < kMaxK * 3) (&sm.icc[0][0])[tid] = 0;
     {
@@ -298,7 +301,7 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
             sm.icc[0][2] = unpack_b(q0);
         }
     }
-    unsigned long long sum0 = 0;
+    unsigned long long sum0 = 0, qacc = 0;  // qacc: sum |p|^2 over the lane's cubes
     for (int kk = 0; kk < K; kk++) {
         __syncthreads();
         ICent ch;  // chosen centres 0 .. kk-1 (uniform)
@@ -317,6 +320,7 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
                 tz[j] = ch.z[0];
             }
         } else {
+            const uint64_t tsel0 = wall_clock64();
             double p[3];
 #pragma unroll
             for (int j = 0; j < 3; j++) p[j] = cvrng_double(rng) * (double)sum0;
@@ -341,7 +345,32 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
                 }
             }
             __syncthreads();
-            // ---- waves 0..2 scan their partition's sorted keys for the first crossing
+            // ---- the partition's sorted keys in KW wave chunks: chunk sums of D ...
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                const int P = sm.pj[j];
+                if (P < 0) continue;
+                const uint32_t a = sm.pbase[P], b = sm.pbase[P + 1];
+                const uint32_t len = (b - a + KW - 1) / KW;
+                const uint32_t wa = min(b, a + (uint32_t)wid * len), wb = min(b, wa + len);
+                uint32_t ls = 0;
+                for (uint32_t s0 = wa; s0 < wb; s0 += STEP) {
+                    const uint32_t i0 = s0 + (uint32_t)lane * 4;
+#pragma unroll
+                    for (int jj = 0; jj < 4; jj++)
+                        if (i0 + jj < wb) {
+                            const uint32_t k = pts[i0 + jj];
+                            ls += (uint32_t)dmin_chosen(unpack_r(k), unpack_g(k), unpack_b(k), ch, kk);
+                        }
+                }
+                const unsigned long long ws = wave_sum((unsigned long long)ls);
+                if (lane == 0) {
+                    sm.wchunk[j][wid] = ws;
+                    atomicAdd(&sm.sel_pts, (unsigned long long)(wb - wa));
+                }
+            }
+            __syncthreads();
+            // ... then waves 0..2 find the chunk holding p_j and the first crossing in it
             if (wid < 3) {
                 const int j = wid;
                 const double pj = j == 0 ? p[0] : (j == 1 ? p[1] : p[2]);
@@ -349,17 +378,24 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
                 int ci = P == -2 ? 0 : N - 1;
                 if (P >= 0) {
                     const uint32_t a = sm.pbase[P], b = sm.pbase[P + 1];
+                    const uint32_t len = (b - a + KW - 1) / KW;
                     unsigned long long e = sm.pex[j];
+                    int w = 0;
+                    for (; w < KW - 1; w++) {
+                        if ((double)(e + sm.wchunk[j][w]) >= pj) break;
+                        e += sm.wchunk[j][w];
+                    }
+                    const uint32_t wa = min(b, a + (uint32_t)w * len), wb = min(b, wa + len);
                     int found = -1;
                     unsigned long long scanned = 0;
-                    for (uint32_t s0 = a; s0 < b && found < 0; s0 += STEP) {
-                        scanned += min((uint32_t)STEP, b - s0);
+                    for (uint32_t s0 = wa; s0 < wb && found < 0; s0 += STEP) {
+                        scanned += min((uint32_t)STEP, wb - s0);
                         const uint32_t i0 = s0 + (uint32_t)lane * 4;
                         uint32_t dv[4], ls = 0;
 #pragma unroll
                         for (int jj = 0; jj < 4; jj++) {
                             dv[jj] = 0;
-                            if (i0 + jj < b) {
+                            if (i0 + jj < wb) {
                                 const uint32_t k = pts[i0 + jj];
                                 dv[jj] = (uint32_t)dmin_chosen(unpack_r(k), unpack_g(k), unpack_b(k), ch, kk);
                             }
@@ -391,6 +427,7 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
                 if (lane == 0) sm.pj[j] = ci;
             }
             __syncthreads();
+            t_sel += wall_clock64() - tsel0;
 #pragma unroll
             for (int j = 0; j < 3; j++) {
                 const uint32_t k = pts[sm.pj[j]];
@@ -421,6 +458,7 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
             if (valid) {
                 if (kk == 0) {
                     v0 = cube_sum(g, tx[0], ty[0], tz[0]);
+                    qacc += cube_sum(g, 0, 0, 0);
                 } else {
                     // owner candidate: nearest chosen centre to the cube centre o + 1.5
                     const int qx = 2 * g.ox + 3, qy = 2 * g.oy + 3, qz = 2 * g.oz + 3;
@@ -541,6 +579,8 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
             sm.icc[kk][2] = best == 0 ? tz[0] : (best == 1 ? tz[1] : tz[2]);
         }
     }
+    qacc = wave_sum(qacc);
+    if (lane == 0) atomicAdd(&sm.qtot, qacc);
     __syncthreads();
     if (tid < kMaxK * 3) {
         const int k = tid / 3, j = tid % 3;
@@ -586,6 +626,8 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
             o->bytes = 0;
             o->pp_pts = 0;
             o->n_cubes = 0;
+            o->t_sel = 0;
+            o->ll_pts = 0;
             o->t_end = wall_clock64();
         }
         return;
@@ -606,8 +648,9 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
     const int Cw = (C + KW - 1) / KW;
     const int cb = min(C, wid * Cw), cend = min(C, cb + Cw);
     uint32_t pp_pts = 0, pp_sel = 0;
-    // compactness + (plain path) k-means++; the cube path adds what its passes read
-    unsigned long long bytes = 4ull * (unsigned long long)N * (unsigned long long)(use_cubes ? 1 : K + 1);
+    uint64_t t_sel = 0, ll_pts = 0;
+    // plain path: k-means++ + compactness passes; the cube path adds what its passes read
+    unsigned long long bytes = use_cubes ? 0ull : 4ull * (unsigned long long)N * (unsigned long long)(K + 1);
     if (tid == 0) sm.fail_pts = 0;
 #define SSLOT(slot) (ss + (size_t)(slot) * (size_t)M)
 
@@ -617,7 +660,7 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
 
     // ------------------------------------------------ k-means++ (generateCentersPP)
     if (use_cubes) {
-        pp_cubes(sm, pts, N, K, rng, ctab, C, cb, cend, cubes.part_uq + (size_t)img * kParts, bytes, pp_pts, pp_sel);
+        pp_cubes(sm, pts, N, K, rng, ctab, C, cb, cend, cubes.part_uq + (size_t)img * kParts, bytes, pp_pts, pp_sel, t_sel);
     } else {
     int cur = 0;
     {
@@ -983,6 +1026,7 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
         if (tid == 0) {
             if (use_cubes) {
                 bytes += 16ull * (unsigned long long)C;  // boundary colours come from the masks
+                ll_pts += sm.fail_pts;
                 sm.fail_pts = 0;
             } else {
                 bytes += 4ull * (unsigned long long)N;
@@ -1105,7 +1149,27 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
 
     if (tid == 0) o->t_lloyd = wall_clock64();
     // ------------------------------------------------ compactness with the last labels
-    {
+    if (use_cubes) {
+        // sum_k sum_{p in k} |p - c_k|^2 = sum_p |p|^2 - sum_k (2 c_k . S_k - n_k |c_k|^2)
+        // with the last assignment's exact sums S_k, n_k: no pass over the colours.  (OpenCV
+        // sums float normL2Sqr per colour; the two differ by float rounding, ~1e-7
+        // relative -- compactness only ranks the attempts.)
+        if (tid == 0) {
+            double acc = (double)sm.qtot;
+            for (int k = 0; k < K; k++) {
+                double cs = 0.0, c2 = 0.0;
+                for (int j = 0; j < 3; j++) {
+                    const double cj = (double)sm.c[k][j];
+                    cs += cj * (double)sm.sums[k][j];
+                    c2 += cj * cj;
+                }
+                acc -= 2.0 * cs - (double)sm.counts[k] * c2;
+            }
+            sm.dred[0] = acc;
+            for (int w = 1; w < KW; w++) sm.dred[w] = 0.0;
+        }
+        __syncthreads();
+    } else {
         const Cent cp = load_centres(sm.cprev);
         const Cent cn = load_centres(sm.c);
         const bool moved = sm.n_moved > 0;
@@ -1132,6 +1196,8 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
         acc = wave_sum(acc);
         if (lane == 0) sm.dred[wid] = acc;
         __syncthreads();
+    }
+    {
         if (tid == 0) {
             double compactness = 0.0;
             for (int w = 0; w < KW; w++) compactness += sm.dred[w];
@@ -1140,6 +1206,8 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
             o->bytes = bytes;
             o->pp_pts = pp_pts;
             o->pad = (int32_t)pp_sel;
+            o->t_sel = t_sel;
+            o->ll_pts = ll_pts;
             o->n_cubes = (uint32_t)C;
             o->t_end = wall_clock64();
             for (int k = 0; k < kMaxK; k++) {

@@ -58,6 +58,8 @@ struct KmeansAttemptOut {
     uint64_t t_start, t_pp, t_lloyd, t_end;  // start, k-means++ done, Lloyd done, end
     uint32_t hw_id, xcc_id;
     uint32_t pp_pts, n_cubes;  // colours k-means++ read one by one; cube count
+    uint64_t t_sel;            // k-means++ time in the selection scans (ticks)
+    uint64_t ll_pts;           // colours Lloyd labelled one by one (all sweeps)
 };
 
 struct KmeansImageOut {

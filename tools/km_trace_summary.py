@@ -21,6 +21,8 @@ def main():
     z = np.zeros_like(U)
     pp_pts, ncub = (a.T[11], a.T[12]) if a.shape[1] >= 13 else (z, z)
     pp_sel = a.T[13] if a.shape[1] >= 14 else z
+    t_sel = a.T[14] / 100.0 if a.shape[1] >= 15 else z
+    ll_pts = a.T[15] if a.shape[1] >= 16 else z
     ok = it > 1
     pp = (tpp - t0) / 100.0
     ll = (tll - tpp) / 100.0
@@ -29,13 +31,13 @@ def main():
     for name, m in [("photo", ph & ok), ("ui", ~ph & ok)]:
         if not m.any():
             continue
-        per = (by[m] - 4 * U[m] * 6) / (it[m] - 1)
         print(f"{name:5s} n={m.sum():4d} U={U[m].mean():9.0f} iters={it[m].mean():5.1f}  PP {pp[m].mean()/1e3:6.3f} ms"
               f"  Lloyd {ll[m].mean()/1e3:6.3f} ms ({(ll[m] / (it[m] - 1)).mean():6.1f} us/iter,"
-              f" {np.mean(per / (4 * U[m])):.3f} of a plain sweep's bytes)  compact {cp[m].mean()/1e3:6.3f} ms")
+              f" {np.mean(ll_pts[m] / (it[m] - 1) / U[m]):.3f} of the colours labelled one by one)  compact {cp[m].mean()/1e3:6.3f} ms")
         if ncub[m].any():
             print(f"      cubes/U {np.mean(ncub[m] / U[m]):.3f}  k-means++ colours read one by one / U"
-                  f" {np.mean(pp_pts[m] / U[m]):.3f} (undecided cubes) + {np.mean(pp_sel[m] / U[m]):.3f} (selection)")
+                  f" {np.mean(pp_pts[m] / U[m]):.3f} (undecided cubes) + {np.mean(pp_sel[m] / U[m]):.3f} (selection);"
+                  f" selection time {t_sel[m].mean() / 1e3:.3f} ms")
     dur = (t1 - t0) / 100.0
     cu = xcc * 1000 + ((hw >> 13) & 7) * 100 + ((hw >> 12) & 1) * 16 + ((hw >> 8) & 15)
     busy = {}
