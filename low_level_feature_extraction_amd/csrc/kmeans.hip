@@ -258,6 +258,50 @@ __device__ __forceinline__ uint32_t cube_sum(const CubeGeo &g, int cx, int cy, i
     return (uint32_t)(g.n * (ax * ax + ay * ay + az * az) + 2 * (ax * g.sx + ay * g.sy + az * g.sz) + g.s2);
 }
 
+// Boundary colours are packed densely into the wave's lanes before they are labelled:
+// the colours of cube (m, id) go to lanes [fill, fill + popc(m)) of pk (ds_permute
+// push; lane b's rank among the set bits comes from mbcnt).  fill + popc(m) <= 64.
+__device__ __forceinline__ void pack_cube(uint32_t &pk, int fill, unsigned long long m, uint32_t id, int lane) {
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    const int n = __popcll(m);
+    const bool has = (m >> lane) & 1ull;
+    // lanes without a colour push into a lane outside [fill, fill + n) (ignored)
+    const int dst = has ? fill + (int)rank : (fill > 0 ? 0 : 63);
+    const uint32_t v = (uint32_t)__builtin_amdgcn_ds_permute(dst * 4, (int)cube_key(id, lane));
+    if (lane >= fill && lane < fill + n) pk = v;
+}
+
+// The cube table is streamed 64 entries per wave step with the next CPF steps' 16-B
+// loads in flight (3 measured no faster: the sweeps are VALU-bound).
+constexpr int CPF = 1;
+struct CubeRing {
+    CubeEnt r[CPF];
+    __device__ __forceinline__ void init(const CubeEnt *t, int cb, int cend, int lane) {
+#pragma unroll
+        for (int q = 0; q < CPF; q++) {
+            r[q].mask = 0;
+            r[q].id = 0;
+            r[q].sums = 0;
+            if (cb + q * 64 + lane < cend) r[q] = t[cb + q * 64 + lane];
+        }
+    }
+    // entry `ci` (this lane's cube of the current step); loads the step CPF ahead
+    __device__ __forceinline__ CubeEnt next(const CubeEnt *t, int ci, int cend) {
+        const CubeEnt e = r[0];
+#pragma unroll
+        for (int q = 0; q + 1 < CPF; q++) r[q] = r[q + 1];
+        if (ci + CPF * 64 < cend) r[CPF - 1] = t[ci + CPF * 64];
+        return e;
+    }
+};
+
+// the uniform mask / id of the cube in lane `src`
+__device__ __forceinline__ unsigned long long lane_mask(const CubeEnt &e, int src) {
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)e.mask, src);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(e.mask >> 32), src);
+    return ((unsigned long long)hi << 32) | lo;
+}
+
 __device__ __forceinline__ int unpack_r(uint32_t k) { return (int)((k >> 16) & 255u); }
 __device__ __forceinline__ int unpack_g(uint32_t k) { return (int)((k >> 8) & 255u); }
 __device__ __forceinline__ int unpack_b(uint32_t k) { return (int)(k & 255u); }
@@ -441,16 +485,24 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
         __syncthreads();
         unsigned long long acc0 = 0, acc1 = 0, acc2 = 0, fails = 0;
         int Pcur = -1;
-        CubeEnt enext;
-        enext.mask = 0;
-        enext.id = 0;
-        enext.sums = 0;
-        if (cb + lane < cend) enext = ctab[cb + lane];
+        uint32_t pk = 0;  // packed boundary colours in lanes [0, fill)
+        int fill = 0;
+        auto flush_pk = [&]() {
+            if (lane < fill) {
+                const int x = unpack_r(pk), y = unpack_g(pk), z = unpack_b(pk);
+                const int D = dmin_chosen(x, y, z, ch, kk);
+                acc0 += (uint32_t)min(D, d2i(x, y, z, tx[0], ty[0], tz[0]));
+                acc1 += (uint32_t)min(D, d2i(x, y, z, tx[1], ty[1], tz[1]));
+                acc2 += (uint32_t)min(D, d2i(x, y, z, tx[2], ty[2], tz[2]));
+            }
+            fill = 0;
+        };
+        CubeRing ring;
+        ring.init(ctab, cb, cend, lane);
         for (int base = cb; base < cend; base += 64) {
             const int cidx = base + lane;
             const bool valid = cidx < cend;
-            const CubeEnt e = enext;
-            if (cidx + 64 < cend) enext = ctab[cidx + 64];
+            const CubeEnt e = ring.next(ctab, cidx, cend);
             const CubeGeo g = cube_geo(e);
             const int P = valid ? (int)((e.id >> 12) & 63u) : kParts;
             uint32_t v0 = 0, v1 = 0, v2 = 0;
@@ -506,6 +558,7 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
             for (;;) {
                 if (Pseg != Pcur) {
                     if (Pcur >= 0) {
+                        flush_pk();
                         const unsigned long long a0 = wave_sum(acc0), a1 = wave_sum(acc1), a2 = wave_sum(acc2);
                         if (lane == 0) {
                             atomicAdd(&sm.psum[0][Pcur], a0);
@@ -522,22 +575,19 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
                     acc1 += v1;
                     acc2 += v2;
                 }
-                // undecided cubes, one per round: lane = mask bit = colour of the cube
+                // undecided cubes: their colours (enumerated from the occupancy mask)
+                // packed densely into the lanes, summed 64 at a time
                 unsigned long long fm = __ballot(mine && fail);
                 while (fm) {
                     const int src = __builtin_ctzll(fm);
                     fm &= fm - 1;
-                    const unsigned long long m = __shfl(e.mask, src);
-                    const uint32_t id = (uint32_t)__shfl((int)e.id, src);
-                    if ((m >> lane) & 1ull) {
-                        const uint32_t kq = cube_key(id, lane);
-                        const int x = unpack_r(kq), y = unpack_g(kq), z = unpack_b(kq);
-                        const int D = dmin_chosen(x, y, z, ch, kk);
-                        acc0 += (uint32_t)min(D, d2i(x, y, z, tx[0], ty[0], tz[0]));
-                        acc1 += (uint32_t)min(D, d2i(x, y, z, tx[1], ty[1], tz[1]));
-                        acc2 += (uint32_t)min(D, d2i(x, y, z, tx[2], ty[2], tz[2]));
-                    }
-                    fails += (unsigned long long)__popcll(m);
+                    const unsigned long long m = lane_mask(e, src);
+                    const uint32_t id = __builtin_amdgcn_readlane(e.id, src);
+                    const int n = __popcll(m);
+                    if (fill + n > 64) flush_pk();
+                    pack_cube(pk, fill, m, id, lane);
+                    fill += n;
+                    fails += (unsigned long long)n;
                 }
                 const unsigned long long rest = __ballot(P > Pseg && P < kParts);
                 if (!rest) break;
@@ -545,6 +595,7 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
             }
         }
         if (Pcur >= 0) {
+            flush_pk();
             const unsigned long long a0 = wave_sum(acc0), a1 = wave_sum(acc1), a2 = wave_sum(acc2);
             if (lane == 0) {
                 atomicAdd(&sm.psum[0][Pcur], a0);
@@ -628,6 +679,7 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
             o->n_cubes = 0;
             o->t_sel = 0;
             o->ll_pts = 0;
+            o->t_sw = 0;
             o->t_end = wall_clock64();
         }
         return;
@@ -885,7 +937,9 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
 
     int iter = 1;
     const double eps2 = 0.2 * 0.2;
+    uint64_t t_sw = 0;  // (trace) time in the labelling sweeps
     for (;;) {
+        const uint64_t tsw0 = wall_clock64();
         const CentP c = pack_centres(load_centres(sm.c));
 #pragma unroll
         for (int k = 0; k < kMaxK; k++) {
@@ -914,16 +968,23 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
                                              fabsf(cu.z[j] - cu.z[k])) +
                                           1.f;
             unsigned long long fails = 0;
-            CubeEnt enext;
-            enext.mask = 0;
-            enext.id = 0;
-            enext.sums = 0;
-            if (cb + lane < cend) enext = ctab[cb + lane];
+            uint32_t pk = 0;  // packed boundary colours in lanes [0, fill)
+            int fill = 0;
+            auto label_pk = [&]() {
+                if (lane < fill) {
+                    const int l = label5p(pk, c);
+                    atomicAdd(&sm.accA[l][tid], (unsigned long long)((pk >> 16) & 255u) |
+                                                    ((unsigned long long)((pk >> 8) & 255u) << 32));
+                    atomicAdd(&sm.accB[l][tid], (unsigned long long)(pk & 255u) | (1ull << 32));
+                }
+                fill = 0;
+            };
+            CubeRing ring;
+            ring.init(ctab, cb, cend, lane);
             for (int base = cb; base < cend; base += 64) {
                 const int ci = base + lane;
                 const bool valid = ci < cend;
-                const CubeEnt e = enext;  // this batch's entry; the next batch's is loaded
-                if (ci + 64 < cend) enext = ctab[ci + 64];  // behind the labelling below
+                const CubeEnt e = ring.next(ctab, ci, cend);
                 bool pass = false;
                 int k = 0;
                 if (valid) {
@@ -963,24 +1024,23 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
                     atomicAdd(&sm.accB[k][tid], (unsigned long long)(g.n * g.oz + g.sz) |
                                                     ((unsigned long long)g.n << 32));
                 }
-                // cubes straddling a boundary, one per round: lane = mask bit = colour
-                // (no key loads: the colours are enumerated from the occupancy mask)
+                // cubes straddling a boundary: their colours (enumerated from the
+                // occupancy mask, no key loads) packed densely into the lanes and
+                // labelled 64 at a time
                 unsigned long long fm = __ballot(valid && !pass);
                 while (fm) {
                     const int src = __builtin_ctzll(fm);
                     fm &= fm - 1;
-                    const unsigned long long m = __shfl(e.mask, src);
-                    const uint32_t id = (uint32_t)__shfl((int)e.id, src);
-                    if ((m >> lane) & 1ull) {
-                        const uint32_t kq = cube_key(id, lane);
-                        const int l = label5p(kq, c);
-                        atomicAdd(&sm.accA[l][tid], (unsigned long long)((kq >> 16) & 255u) |
-                                                        ((unsigned long long)((kq >> 8) & 255u) << 32));
-                        atomicAdd(&sm.accB[l][tid], (unsigned long long)(kq & 255u) | (1ull << 32));
-                    }
-                    fails += (unsigned long long)__popcll(m);
+                    const unsigned long long m = lane_mask(e, src);
+                    const uint32_t id = __builtin_amdgcn_readlane(e.id, src);
+                    const int n = __popcll(m);
+                    if (fill + n > 64) label_pk();
+                    pack_cube(pk, fill, m, id, lane);
+                    fill += n;
+                    fails += (unsigned long long)n;
                 }
             }
+            label_pk();
             if (lane == 0 && fails) atomicAdd(&sm.fail_pts, fails);
         } else {
         // The sweep is load-latency bound: keep the next PF steps' 16-B loads in flight
@@ -1023,6 +1083,7 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
         }
         }  // point sweep
         __syncthreads();
+        t_sw += wall_clock64() - tsw0;
         if (tid == 0) {
             if (use_cubes) {
                 bytes += 16ull * (unsigned long long)C;  // boundary colours come from the masks
@@ -1208,6 +1269,7 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
             o->pad = (int32_t)pp_sel;
             o->t_sel = t_sel;
             o->ll_pts = ll_pts;
+            o->t_sw = t_sw;
             o->n_cubes = (uint32_t)C;
             o->t_end = wall_clock64();
             for (int k = 0; k < kMaxK; k++) {

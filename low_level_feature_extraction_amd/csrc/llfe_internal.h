@@ -60,6 +60,7 @@ struct KmeansAttemptOut {
     uint32_t pp_pts, n_cubes;  // colours k-means++ read one by one; cube count
     uint64_t t_sel;            // k-means++ time in the selection scans (ticks)
     uint64_t ll_pts;           // colours Lloyd labelled one by one (all sweeps)
+    uint64_t t_sw;             // Lloyd time in the labelling sweeps (ticks)
 };
 
 struct KmeansImageOut {

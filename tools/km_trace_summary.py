@@ -23,6 +23,7 @@ def main():
     pp_sel = a.T[13] if a.shape[1] >= 14 else z
     t_sel = a.T[14] / 100.0 if a.shape[1] >= 15 else z
     ll_pts = a.T[15] if a.shape[1] >= 16 else z
+    t_sw = a.T[16] / 100.0 if a.shape[1] >= 17 else z
     ok = it > 1
     pp = (tpp - t0) / 100.0
     ll = (tll - tpp) / 100.0
@@ -37,7 +38,7 @@ def main():
         if ncub[m].any():
             print(f"      cubes/U {np.mean(ncub[m] / U[m]):.3f}  k-means++ colours read one by one / U"
                   f" {np.mean(pp_pts[m] / U[m]):.3f} (undecided cubes) + {np.mean(pp_sel[m] / U[m]):.3f} (selection);"
-                  f" selection time {t_sel[m].mean() / 1e3:.3f} ms")
+                  f" selection time {t_sel[m].mean() / 1e3:.3f} ms; Lloyd sweeps {t_sw[m].mean() / 1e3:.3f} ms")
     dur = (t1 - t0) / 100.0
     cu = xcc * 1000 + ((hw >> 13) & 7) * 100 + ((hw >> 12) & 1) * 16 + ((hw >> 8) & 15)
     busy = {}
