@@ -40,7 +40,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
     objs = []
     hipcc = _hipcc()
     common = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", f"-I{os.path.join(ROOT, 'include')}",
-              "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
+              "-Wall", "-Wno-unused-function", "-Wno-unused-variable",
+              *os.environ.get("LLFE_EXTRA_FLAGS", "").split()]  # (experiments only)
     tmpdir = os.path.join(PKG, "build")
     os.makedirs(tmpdir, exist_ok=True)
     procs = []
