@@ -162,6 +162,19 @@ int llfe_resize_lanczos_pil(llfe_ctx *ctx, const uint8_t *src, int32_t h, int32_
  * ceil(h/fy) x ceil(w/fx) x ch bytes. */
 int llfe_reduce_pil(llfe_ctx *ctx, const uint8_t *src, int32_t h, int32_t w, int32_t ch, int32_t fx, int32_t fy,
                     uint8_t *dst, llfe_stream stream);
+/* cv2.resize(src, (out_w, out_h), interpolation=...) on a device u8 HWC image (ch <= 4)
+ * -- the downscale of validate_and_preprocess_image (app/services/analyze/utils.py:
+ * 118-143): LLFE_CV_INTER_AREA for "auto", LLFE_CV_INTER_LANCZOS4 for "high_quality",
+ * LLFE_CV_INTER_LINEAR for "performance".  dst holds out_h x out_w x ch bytes. */
+#define LLFE_CV_INTER_LINEAR 1
+#define LLFE_CV_INTER_AREA 3
+#define LLFE_CV_INTER_LANCZOS4 4
+int llfe_resize_cv(llfe_ctx *ctx, const uint8_t *src, int32_t h, int32_t w, int32_t ch, uint8_t *dst, int32_t out_h,
+                   int32_t out_w, int32_t interpolation, llfe_stream stream);
+/* validate_and_preprocess_image's size rule (utils.py:118-143, Python float
+ * semantics): returns 1 with (out_w, out_h, interpolation) when `mode` (LLFE_PRE_*)
+ * resizes a w x h image, 0 when it does not. Host only. */
+int llfe_preprocess_size(int32_t w, int32_t h, int32_t mode, int32_t *out_w, int32_t *out_h, int32_t *interpolation);
 /* PIL Image.thumbnail size rule (preserve_aspect_ratio): returns 1 and the new size
  * when a resize happens, 0 when (w, h) already fits (max_w, max_h). Host only. */
 int llfe_thumbnail_size(int32_t w, int32_t h, int32_t max_w, int32_t max_h, int32_t *out_w, int32_t *out_h);

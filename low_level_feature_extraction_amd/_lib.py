@@ -98,6 +98,9 @@ SIGNATURES = {
     "llfe_resize_lanczos_pil": (C.c_int, [_vp, _vp, _i32, _i32, _i32, _vp, _i32, _i32, _vp, _vp]),
     "llfe_reduce_pil": (C.c_int, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp]),
     "llfe_thumbnail_size": (C.c_int, [_i32, _i32, _i32, _i32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "llfe_resize_cv": (C.c_int, [_vp, _vp, _i32, _i32, _i32, _vp, _i32, _i32, _i32, _vp]),
+    "llfe_preprocess_size": (C.c_int, [_i32, _i32, _i32, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                       C.POINTER(C.c_int32)]),
     "llfe_thumbnail_pil": (C.c_int, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _i64, C.POINTER(C.c_int32),
                                      C.POINTER(C.c_int32), _vp]),
     "llfe_find_contours":(C.c_int, [_vp, _i32, _i32, _vp, _i64, _vp, _i32, C.POINTER(C.c_int64)]),

@@ -301,6 +301,23 @@ class Backend:
                                             self._stream(x)))
         return out
 
+    def resize_cv(self, image, out_w, out_h, interpolation):
+        """cv2.resize(image, (out_w, out_h), interpolation) of one H x W [x C] uint8 image
+        (validate_and_preprocess_image, utils.py:118-143); interpolation is an OpenCV
+        code or one of "linear" / "area" / "lanczos4"."""
+        torch = _torch()
+        code = CV_INTER[interpolation] if isinstance(interpolation, str) else int(interpolation)
+        x = image if _is_torch(image) else torch.from_numpy(np.ascontiguousarray(image, np.uint8))
+        x = x.to(f"cuda:{self.device}").contiguous()
+        squeeze = x.dim() == 2
+        if squeeze:
+            x = x[:, :, None]
+        h, w, ch = x.shape
+        out = torch.empty((out_h, out_w, ch), dtype=torch.uint8, device=x.device)
+        self._chk(self._lib.llfe_resize_cv(self.ctx, x.data_ptr(), h, w, ch, out.data_ptr(), out_h, out_w, code,
+                                           self._stream(x)))
+        return out[:, :, 0] if squeeze else out
+
     def thumbnail_pil(self, image, max_w=1920, max_h=1080):
         """PIL thumbnail((max_w, max_h), LANCZOS) of one H x W x C uint8 image."""
         torch = _torch()
@@ -316,6 +333,23 @@ class Backend:
                                                out.numel(), C.byref(oh), C.byref(ow), self._stream(x)))
         out = out[: oh.value * ow.value * ch].view(oh.value, ow.value, ch)
         return out[:, :, 0] if squeeze else out
+
+
+CV_INTER = {"linear": 1, "area": 3, "lanczos4": 4}
+PRE_MODES = {"none": 0, "auto": 1, "high_quality": 2, "performance": 3}
+_INTER_NAME = {1: "INTER_LINEAR", 3: "INTER_AREA", 4: "INTER_LANCZOS4"}
+
+
+def preprocess_size(w, h, mode):
+    """validate_and_preprocess_image's size rule (utils.py:118-143) through the ABI:
+    -> (new_w, new_h, interpolation code) or None when the mode does not resize."""
+    if mode not in PRE_MODES:
+        return None
+    ow, oh, it = C.c_int32(0), C.c_int32(0), C.c_int32(0)
+    rc = L.lib().llfe_preprocess_size(w, h, PRE_MODES[mode], C.byref(ow), C.byref(oh), C.byref(it))
+    if rc < 0:
+        raise L.LlfeError(rc, "invalid preprocessing geometry")
+    return (ow.value, oh.value, it.value) if rc == 1 else None
 
 
 def thumbnail_size(w, h, max_w=1920, max_h=1080):

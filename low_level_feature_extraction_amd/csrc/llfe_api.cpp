@@ -906,6 +906,48 @@ int llfe_thumbnail_pil(llfe_ctx *ctx, const uint8_t *src, int32_t h, int32_t w, 
     return llfe_resize_lanczos_pil(ctx, src, h, w, ch, dst, oh, ow, nullptr, stream);
 }
 
+// cv2.resize (validate_and_preprocess_image, utils.py:118-143); tables built on the host
+// exactly as OpenCV builds them, one kernel evaluates the output (cvresize.hip)
+int llfe_resize_cv(llfe_ctx *ctx, const uint8_t *src, int32_t h, int32_t w, int32_t ch, uint8_t *dst, int32_t out_h,
+                   int32_t out_w, int32_t interpolation, llfe_stream stream) {
+    if (!ctx || !src || !dst || h <= 0 || w <= 0 || ch <= 0 || out_h <= 0 || out_w <= 0) return LLFE_ERR_INVALID;
+    if (ch > 4) return ctx->fail(LLFE_ERR_UNSUPPORTED, "llfe_resize_cv: ch > 4");
+    CvResizePlan plan;
+    if (cv_resize_plan(h, w, ch, out_h, out_w, interpolation, plan) != 0)
+        return ctx->fail(LLFE_ERR_UNSUPPORTED, "llfe_resize_cv: interpolation %d not supported", interpolation);
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = (hipStream_t)stream;
+    const int32_t *dtab = nullptr;
+    if (!plan.tab.empty()) {
+        HIPCHK(ctx, ctx->d_coef.ensure(plan.tab.size()));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->d_coef.p, plan.tab.data(), plan.tab.size() * sizeof(int32_t),
+                                   hipMemcpyHostToDevice, s));
+        dtab = ctx->d_coef.p;
+    }
+    HIPCHK(ctx, launch_cv_resize(plan, src, dst, dtab, s));
+    HIPCHK(ctx, hipStreamSynchronize(s));  // the host table dies here
+    return LLFE_OK;
+}
+
+int llfe_preprocess_size(int32_t w, int32_t h, int32_t mode, int32_t *out_w, int32_t *out_h, int32_t *interpolation) {
+    if (w <= 0 || h <= 0 || !out_w || !out_h || !interpolation) return LLFE_ERR_INVALID;
+    int max_dim, interp;
+    switch (mode) {
+    case LLFE_PRE_AUTO: max_dim = 2000, interp = LLFE_CV_INTER_AREA; break;
+    case LLFE_PRE_HIGH_QUALITY: max_dim = 4000, interp = LLFE_CV_INTER_LANCZOS4; break;
+    case LLFE_PRE_PERFORMANCE: max_dim = 1000, interp = LLFE_CV_INTER_LINEAR; break;
+    case LLFE_PRE_NONE: return 0;
+    default: return LLFE_ERR_INVALID;
+    }
+    const int m = std::max(w, h);
+    if (m <= max_dim) return 0;
+    const double scale = (double)max_dim / m;  // Python: max_dim / max(h, w)
+    *out_w = (int32_t)(w * scale);             // int(w * scale): truncation toward 0
+    *out_h = (int32_t)(h * scale);
+    *interpolation = interp;
+    return 1;
+}
+
 int llfe_reduce_pil(llfe_ctx *ctx, const uint8_t *src, int32_t h, int32_t w, int32_t ch, int32_t fx, int32_t fy,
                     uint8_t *dst, llfe_stream stream) {
     if (!ctx || !src || !dst || h <= 0 || w <= 0 || ch <= 0 || fx <= 0 || fy <= 0) return LLFE_ERR_INVALID;

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 namespace llfe {
 
 // ---------------------------------------------------------------- stencils
@@ -127,5 +129,20 @@ hipError_t launch_resize_v(const uint8_t *src, int src_w, int ch, uint8_t *dst, 
                            const int32_t *coeffs, int ksize, hipStream_t s);
 hipError_t launch_reduce(const uint8_t *src, int src_w, int ch, int x0, int y0, int x1, int y1, int fx, int fy,
                          uint8_t *dst, int out_w, int out_h, hipStream_t s);
+
+// cv2.resize for the preprocessing modes (cvresize.hip); OpenCV interpolation codes
+constexpr int kCvInterLinear = 1, kCvInterArea = 3, kCvInterLanczos4 = 4;
+struct CvResizePlan {
+    enum Kind { COPY, AREA_FAST, AREA, GENERIC } kind = COPY;
+    int h = 0, w = 0, cn = 0, oh = 0, ow = 0;
+    int fx = 1, fy = 1;                      // AREA_FAST integer factors
+    int ks = 2, xmin = 0, xmax = 0, x_vec = 0;  // GENERIC: taps, border columns, vector stop
+    std::vector<int32_t> tab;                // coefficient tables (x part, then y part)
+    int64_t ytab_off = 0;
+};
+// host: OpenCV's tables for (h, w, cn) -> (oh, ow); 0 ok, -1 unsupported
+int cv_resize_plan(int h, int w, int cn, int oh, int ow, int interp, CvResizePlan &p);
+hipError_t launch_cv_resize(const CvResizePlan &p, const uint8_t *src, uint8_t *dst, const int32_t *d_tab,
+                            hipStream_t s);
 
 }  // namespace llfe

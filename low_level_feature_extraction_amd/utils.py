@@ -8,10 +8,10 @@ mode-dependent downscale of utils.py:118-143:
     high_quality  -> INTER_LANCZOS4 when max(h, w) > 4000
     performance   -> INTER_LINEAR   when max(h, w) > 1000
 
-with new_size = (int(w * s), int(h * s)), s = max_dim / max(h, w).  No BASELINE
-configuration triggers a resize (1920 < 2000, 3840 < 4000).  The OpenCV fixed-point
-resize kernels are not part of this backend yet: an input that needs one raises
-HTTPException(400) naming the mode instead of silently resizing on the CPU.
+with new_size = (int(w * s), int(h * s)), s = max_dim / max(h, w) (the size rule is
+llfe_preprocess_size in the C ABI).  The resize itself runs on the GPU
+(llfe_resize_cv: OpenCV's fixed-point / area tables, csrc/cvresize.hip).  No BASELINE
+configuration triggers a resize (1920 < 2000, 3840 < 4000).
 """
 from __future__ import annotations
 
@@ -35,28 +35,30 @@ class PreprocessingMode(str, Enum):
     PERFORMANCE = "performance"
 
 
-class UnsupportedResize(NotImplementedError):
-    pass
+_CODE = {"INTER_LINEAR": 1, "INTER_AREA": 3, "INTER_LANCZOS4": 4}
 
 
 def preprocess_size(w: int, h: int, preprocessing: str):
-    """-> (new_w, new_h, interpolation) or None (utils.py:118-143)."""
-    if preprocessing not in _LIMITS:
+    """-> (new_w, new_h, interpolation name) or None (utils.py:118-143)."""
+    from . import backend
+
+    plan = backend.preprocess_size(w, h, preprocessing)
+    if plan is None:
         return None
-    max_dim, interp = _LIMITS[preprocessing]
-    if max(h, w) > max_dim:
-        scale = max_dim / max(h, w)
-        return int(w * scale), int(h * scale), interp
-    return None
+    return plan[0], plan[1], _LIMITS[preprocessing][1]
 
 
-def preprocess_decoded(image: np.ndarray, preprocessing: str) -> np.ndarray:
+def preprocess_decoded(image: np.ndarray, preprocessing: str, device: int = 0) -> np.ndarray:
+    """The mode resize of utils.py:118-143 on a decoded BGR image (GPU; the HIP
+    extension must be present -- there is no CPU fallback)."""
     h, w = image.shape[:2]
     plan = preprocess_size(w, h, preprocessing)
     if plan is None:
         return image
-    raise UnsupportedResize(f"cv2.resize {plan[2]} ({w}x{h} -> {plan[0]}x{plan[1]}) for preprocessing="
-                            f"{preprocessing!r} is not implemented by the MI355X backend")
+    from .backend import Backend
+
+    out = Backend.get(device).resize_cv(image, plan[0], plan[1], _CODE[plan[2]])
+    return out.cpu().numpy()
 
 
 def _http_exception(status_code: int, detail: str):

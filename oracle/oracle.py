@@ -436,6 +436,32 @@ def preprocess_size(w, h, mode):
     return None
 
 
+CV_INTER = {"linear": 1, "area": 3, "lanczos4": 4}
+
+
+def cv_resize(img, out_w, out_h, interp):
+    """cv2.resize(img, (out_w, out_h), interpolation=INTER_<interp>) on u8 (H, W[, C]),
+    restated in llfe_oracle.c (utils.py:118-143)."""
+    img = np.ascontiguousarray(img, np.uint8)
+    squeeze = img.ndim == 2
+    if squeeze:
+        img = img[:, :, None]
+    h, w, ch = img.shape
+    out = np.empty((out_h, out_w, ch), np.uint8)
+    code = CV_INTER[interp] if isinstance(interp, str) else int(interp)
+    if lib().orc_cv_resize(_p(img), h, w, ch, _p(out), out_h, out_w, code) != 0:
+        raise ValueError(f"cv_resize: unsupported {interp!r} {w}x{h} -> {out_w}x{out_h}")
+    return out[:, :, 0] if squeeze else out
+
+
+def preprocess(img, mode):
+    """validate_and_preprocess_image's resize step on a decoded BGR image."""
+    plan = preprocess_size(img.shape[1], img.shape[0], mode)
+    if plan is None:
+        return img
+    return cv_resize(img, plan[0], plan[1], plan[2])
+
+
 # --------------------------------------------------------------------------- seeds
 MASK64 = (1 << 64) - 1
 

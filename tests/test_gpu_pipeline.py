@@ -189,3 +189,53 @@ def test_auto_process_image_dropin():
     assert np.array_equal(ImageProcessor.auto_process_image(small.getvalue()), rgb[:100, :100, ::-1])
     with pytest.raises(ValueError):
         ImageProcessor.auto_process_image(b"junk")
+
+
+# --------------------------------------------------------------------------- cv2.resize modes
+# validate_and_preprocess_image (utils.py:118-143): the GPU resize (llfe_resize_cv) against
+# the oracle's OpenCV restatement, bit-exact.  Sizes cover AREA 2x / 3x (resizeAreaFast_),
+# fractional AREA (resizeArea_), LINEAR (incl. the exact-2x -> AREA rule and the vector /
+# scalar vertical split), LANCZOS4, grey and 4-channel images.
+CV_RESIZE_CASES = [
+    (3000, 4000, 1500, 2000, "area"), (1440, 2560, 1125, 2000, "area"), (2400, 6000, 800, 2000, "area"),
+    (1080, 1920, 562, 1000, "linear"), (2000, 1500, 1000, 750, "linear"), (1201, 1333, 900, 1000, "linear"),
+    (4000, 6000, 2666, 4000, "lanczos4"), (4500, 4100, 4000, 3644, "lanczos4"), (97, 131, 40, 57, "lanczos4"),
+    (97, 131, 40, 57, "area"), (97, 131, 40, 57, "linear"), (9, 7, 3, 2, "area"),
+]
+
+
+@pytest.mark.parametrize("h,w,oh,ow,interp", CV_RESIZE_CASES)
+def test_cv_resize_vs_oracle(backend, orc, h, w, oh, ow, interp):
+    rng = np.random.default_rng(h * 31 + w)
+    img = synth.synth_numpy(3, h, w, seed=5, kind="photo") if h * w > 10000 else rng.integers(
+        0, 256, (h, w, 3), dtype=np.uint8)
+    got = backend.resize_cv(img, ow, oh, interp).cpu().numpy()
+    exp = orc.cv_resize(img, ow, oh, interp)
+    assert got.shape == exp.shape
+    assert np.array_equal(got, exp), int((got != exp).sum())
+
+
+@pytest.mark.parametrize("ch", [1, 4])
+def test_cv_resize_channels(backend, orc, ch):
+    img = np.random.default_rng(ch).integers(0, 256, (333, 517, ch), dtype=np.uint8)
+    for interp, (ow, oh) in [("area", (200, 129)), ("linear", (250, 161)), ("lanczos4", (300, 193)),
+                             ("area", (172, 111))]:
+        got = backend.resize_cv(img if ch > 1 else img[:, :, 0], ow, oh, interp).cpu().numpy()
+        exp = orc.cv_resize(img if ch > 1 else img[:, :, 0], ow, oh, interp)
+        assert np.array_equal(got, exp), (interp, int((got != exp).sum()))
+
+
+def test_validate_and_preprocess_image_resizes_on_gpu(orc):
+    import asyncio
+
+    from PIL import Image
+
+    from low_level_feature_extraction_amd.utils import validate_and_preprocess_image
+
+    rgb = synth.synth_numpy(1, 1300, 2200, seed=3)[:, :, ::-1].copy()
+    buf = io.BytesIO()
+    Image.fromarray(rgb).save(buf, format="PNG")
+    bgr = rgb[:, :, ::-1]
+    for mode in ("auto", "performance", "high_quality", "none"):
+        out = asyncio.run(validate_and_preprocess_image(buf.getvalue(), "r", mode))
+        assert np.array_equal(out, orc.preprocess(np.ascontiguousarray(bgr), mode)), mode

@@ -373,3 +373,167 @@ def test_preprocess_and_seed_helpers(orc):
     assert orc.image_rng_state(0, 0) == orc.splitmix64(0) != 0
     assert orc.splitmix64(0) == 0xE220A8397B1DCDAF
     assert math.isclose(orc.thumbnail_size(3840, 2160)[0], 1920)
+
+
+# --------------------------------------------------------------------------- cv2.resize
+# utils.py:118-143 (validate_and_preprocess_image): AREA / LANCZOS4 / LINEAR downscales.
+# A second restatement in NumPy (float32 scalars for OpenCV's float steps, int64 for its
+# fixed point) checked bit-exactly against llfe_oracle.c, plus hand-derived answers.
+def _np_area_tab(ssize, dsize, scale):
+    tab = []
+    for dx in range(dsize):
+        f1 = dx * scale
+        f2 = f1 + scale
+        cell = min(scale, ssize - f1)
+        s1, s2 = math.ceil(f1), math.floor(f2)
+        s2 = min(s2, ssize - 1)
+        s1 = min(s1, s2)
+        if s1 - f1 > 1e-3:
+            tab.append((dx, s1 - 1, np.float32((s1 - f1) / cell)))
+        for s in range(s1, s2):
+            tab.append((dx, s, np.float32(1.0 / cell)))
+        if f2 - s2 > 1e-3:
+            tab.append((dx, s2, np.float32(min(min(f2 - s2, 1.0), cell) / cell)))
+    return tab
+
+
+def _np_lanczos4(x):
+    x = np.float32(x)
+    s45 = 0.70710678118654752440084436210485
+    cs = [(1, 0), (-s45, -s45), (0, 1), (s45, -s45), (-1, 0), (s45, s45), (0, -1), (-s45, s45)]
+    y0 = -float(np.float32(x + np.float32(3))) * math.pi * 0.25
+    s0, c0 = math.sin(y0), math.cos(y0)
+    c = []
+    tot = np.float32(0)
+    for i in range(8):
+        yi = np.float32(np.float32(x + np.float32(3)) - np.float32(i))
+        if abs(yi) >= np.float32(1e-6):
+            y = -float(yi) * math.pi * 0.25
+            v = np.float32((cs[i][0] * s0 + cs[i][1] * c0) / (y * y))
+        else:
+            v = np.float32(1e30)
+        c.append(v)
+        tot = np.float32(tot + v)
+    inv = np.float32(np.float32(1) / tot)
+    return [np.float32(v * inv) for v in c]
+
+
+def _s16(v):
+    return int(np.clip(np.rint(np.float32(v)), -32768, 32767))
+
+
+def _np_cv_resize(img, ow, oh, interp):
+    h, w, cn = img.shape
+    sx_, sy_ = w / ow, h / oh  # = 1 / ((double)dsize / ssize) up to the last ulp; recomputed below
+    inv_x, inv_y = ow / w, oh / h
+    scale_x, scale_y = 1.0 / inv_x, 1.0 / inv_y
+    ix, iy = int(round(scale_x)), int(round(scale_y))
+    fast = abs(scale_x - ix) < 2.220446049250313e-16 and abs(scale_y - iy) < 2.220446049250313e-16
+    if interp == "linear" and fast and ix == 2 and iy == 2:
+        interp = "area"
+    if interp == "area":
+        if fast:
+            out = np.zeros((oh, ow, cn), np.uint8)
+            for dy in range(oh):
+                for dx in range(ow):
+                    blk = img[dy * iy:(dy + 1) * iy, dx * ix:(dx + 1) * ix].astype(np.int64)
+                    s = blk.sum(axis=(0, 1))
+                    if ix == 2 and iy == 2:
+                        out[dy, dx] = (s + 2) >> 2
+                    else:
+                        out[dy, dx] = np.clip(np.rint(s.astype(np.float32) * np.float32(1.0 / np.float32(ix * iy))),
+                                              0, 255)
+            return out
+        S = img.astype(np.float32)
+        buf = np.zeros((h, ow, cn), np.float32)
+        for dx, sx, a in _np_area_tab(w, ow, scale_x):
+            buf[:, dx] = buf[:, dx] + S[:, sx] * a
+        acc = np.zeros((oh, ow, cn), np.float32)
+        for dy, sy, b in _np_area_tab(h, oh, scale_y):
+            acc[dy] = acc[dy] + b * buf[sy]
+        return np.clip(np.rint(acc), 0, 255).astype(np.uint8)
+    ks = 8 if interp == "lanczos4" else 2
+
+    def coeffs(d, scale, n):
+        f = np.float32((d + 0.5) * scale - 0.5)
+        s = math.floor(f)
+        f = np.float32(f - np.float32(s))
+        if ks == 2 and s >= n - 1:
+            s, f = n - 1, np.float32(0)
+        c = _np_lanczos4(f) if ks == 8 else [np.float32(1) - f, f]
+        return s, [_s16(np.float32(v * np.float32(2048))) for v in c]
+
+    xs = [coeffs(dx, scale_x, w) for dx in range(ow)]
+    ys = [coeffs(dy, scale_y, h) for dy in range(oh)]
+    I = img.astype(np.int64)
+    # horizontal pass for every source row: (h, ow, cn)
+    hor = np.zeros((h, ow, cn), np.int64)
+    for dx, (sx, a) in enumerate(xs):
+        for j in range(ks):
+            col = min(max(sx - (ks // 2 - 1) + j, 0), w - 1)
+            hor[:, dx] += I[:, col] * a[j]
+    width = ow * cn
+    x_vec = 0
+    while x_vec <= width - 16:
+        x_vec += 16
+    while x_vec < width - 8:
+        x_vec += 8
+    out = np.zeros((oh, ow * cn), np.int64)
+    for dy, (sy, b) in enumerate(ys):
+        rows = [hor[min(max(sy - (ks // 2 - 1) + k, 0), h - 1)].reshape(-1) for k in range(ks)]
+        if ks == 8:
+            v = sum(r * bk for r, bk in zip(rows, b))
+            out[dy] = (v + (1 << 21)) >> 22
+        else:
+            scal = (rows[0] * b[0] + rows[1] * b[1] + (1 << 21)) >> 22
+            t = ((np.clip(rows[0] >> 4, -32768, 32767) * b[0]) >> 16) + ((np.clip(rows[1] >> 4, -32768, 32767) * b[1]) >> 16)
+            vec = (np.clip(t, -32768, 32767) + 2) >> 2
+            idx = np.arange(width)
+            out[dy] = np.where(idx < x_vec, vec, scal)
+    return np.clip(out, 0, 255).astype(np.uint8).reshape(oh, ow, cn)
+
+
+RESIZE_CASES = [  # (h, w, oh, ow): exact 2x, 3x, fractional, tall, wide, odd
+    (40, 60, 20, 30), (45, 66, 15, 22), (97, 131, 40, 57), (120, 50, 77, 32), (33, 200, 9, 61),
+    (64, 64, 21, 21), (101, 103, 100, 102), (18, 26, 7, 13),
+]
+
+
+@pytest.mark.parametrize("interp", ["area", "linear", "lanczos4"])
+@pytest.mark.parametrize("h,w,oh,ow", RESIZE_CASES)
+def test_cv_resize_numpy_restatement(orc, interp, h, w, oh, ow):
+    img = _rng(h * 7 + w).integers(0, 256, (h, w, 3), dtype=np.uint8)
+    if interp != "area":
+        img = np.stack([_smooth_image(h + w + c, h, w) for c in range(3)], -1)
+    got = orc.cv_resize(img, ow, oh, interp)
+    exp = _np_cv_resize(img, ow, oh, interp)
+    assert np.array_equal(got, exp)
+
+
+def test_cv_resize_known_answers(orc):
+    # INTER_AREA 2x2 (and INTER_LINEAR at exactly 2x, which OpenCV runs as AREA):
+    # (a + b + c + d + 2) >> 2 -- 1+2+3+4 = 10 -> 3, 0+0+0+2 = 2 -> 1, 255*4 -> 255
+    x = np.array([[1, 2, 0, 0, 255, 255], [3, 4, 0, 2, 255, 255]], np.uint8)[:, :, None]
+    assert orc.cv_resize(x, 3, 1, "area")[:, :, 0].tolist() == [[3, 1, 255]]
+    assert orc.cv_resize(x, 3, 1, "linear")[:, :, 0].tolist() == [[3, 1, 255]]
+    # INTER_AREA 3x3: cvRound(sum * (1.f / 9)); 13 / 9 = 1.44 -> 1, 14 / 9 = 1.56 -> 2
+    y = np.zeros((3, 6), np.uint8)
+    y[0, 0], y[0, 1] = 9, 4
+    y[0, 3], y[2, 5] = 9, 5
+    assert orc.cv_resize(y[:, :, None], 2, 1, "area")[:, :, 0].tolist() == [[1, 2]]
+    # INTER_LINEAR at 4x: fx = 4 dx + 1.5 -> taps (4dx + 1, 4dx + 2) with 1024 / 1024
+    z = np.tile(np.arange(16, dtype=np.uint8) * 10, (4, 1))[:, :, None]
+    assert orc.cv_resize(z, 4, 1, "linear")[:, :, 0].tolist() == [[15, 55, 95, 135]]
+    # constant images stay constant for every mode and size
+    for interp in ("area", "linear", "lanczos4"):
+        c = np.full((37, 53, 3), 201, np.uint8)
+        assert (orc.cv_resize(c, 17, 11, interp) == 201).all()
+    # LANCZOS4 at integer phase (fx = 0) is a copy of the centre tap
+    assert _np_lanczos4(0.0)[3] == np.float32(1.0)
+
+
+def test_cv_resize_preprocess_modes(orc):
+    img = _rng(3).integers(0, 256, (1100, 700, 3), dtype=np.uint8)
+    assert orc.preprocess(img, "auto") is img and orc.preprocess(img, "none") is img
+    out = orc.preprocess(img, "performance")
+    assert out.shape == (1000, int(700 * (1000 / 1100)), 3)
