@@ -318,6 +318,12 @@ struct llfe_ctx {
     HostBuf<KmeansImageOut> h_kout_s[2];
     hipEvent_t chunk_done[2] = {nullptr, nullptr};
     hipEvent_t mask_done[2] = {nullptr, nullptr};  // shapes/shadows results are on the host
+    // the mask / shadow D2H runs on its own stream so the colour stage starts right after
+    // the hysteresis kernels; mask_ready[slot] orders it after them, and a workspace is
+    // not overwritten before the D2H that last read it (w_mask_slot) has finished
+    hipStream_t copy_stream = nullptr;
+    hipEvent_t mask_ready[2] = {nullptr, nullptr};
+    int w_mask_slot[2] = {-1, -1};
     int chunk = 256;  // images per device pass (LLFE_CHUNK)
     HostBuf<KmeansImageOut> h_kout;
     // per-thread host scratch
@@ -485,6 +491,8 @@ int enqueue_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_
     const int8_t *noise;
     int rc = stage_input(ctx, W, b, i0, n, &img, &noise, s);
     if (rc) return rc;
+    // d_shadow / d_bits of this workspace may still be in the previous chunk's D2H
+    if (ctx->w_mask_slot[q] >= 0) HIPCHK(ctx, hipStreamWaitEvent(s, ctx->mask_done[ctx->w_mask_slot[q]], 0));
     if (want_shp || want_shd) {
         HIPCHK(ctx, W.d_shadow.ensure(2 * (size_t)n));
         if (want_shp) HIPCHK(ctx, W.d_cls.ensure((size_t)n * P));
@@ -501,15 +509,23 @@ int enqueue_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_
         HIPCHK(ctx, ctx->h_bits_s[slot].ensure((size_t)n * h * wpr));
         rc = run_hysteresis_dilate(ctx, W, n, h, w, W.d_bits.p, nullptr, s);
         if (rc) return rc;
-        HIPCHK(ctx, hipMemcpyAsync(ctx->h_bits_s[slot].p, W.d_bits.p, sizeof(uint64_t) * n * h * wpr,
-                                   hipMemcpyDeviceToHost, s));
     }
-    if (want_shd) {
-        HIPCHK(ctx, ctx->h_shadow_s[slot].ensure(2 * (size_t)n));
-        HIPCHK(ctx, hipMemcpyAsync(ctx->h_shadow_s[slot].p, W.d_shadow.p, sizeof(unsigned long long) * 2 * n,
-                                   hipMemcpyDeviceToHost, s));
+    if (want_shd) HIPCHK(ctx, ctx->h_shadow_s[slot].ensure(2 * (size_t)n));
+    if (want_shp || want_shd) {
+        hipStream_t cs = ctx->copy_stream;
+        HIPCHK(ctx, hipEventRecord(ctx->mask_ready[slot], s));
+        HIPCHK(ctx, hipStreamWaitEvent(cs, ctx->mask_ready[slot], 0));
+        if (want_shp)
+            HIPCHK(ctx, hipMemcpyAsync(ctx->h_bits_s[slot].p, W.d_bits.p, sizeof(uint64_t) * n * h * wpr,
+                                       hipMemcpyDeviceToHost, cs));
+        if (want_shd)
+            HIPCHK(ctx, hipMemcpyAsync(ctx->h_shadow_s[slot].p, W.d_shadow.p, sizeof(unsigned long long) * 2 * n,
+                                       hipMemcpyDeviceToHost, cs));
+        HIPCHK(ctx, hipEventRecord(ctx->mask_done[slot], cs));
+        ctx->w_mask_slot[q] = slot;
+    } else {
+        HIPCHK(ctx, hipEventRecord(ctx->mask_done[slot], s));
     }
-    HIPCHK(ctx, hipEventRecord(ctx->mask_done[slot], s));
     if (want_col) {
         rc = color_stage(ctx, W, img, noise, n, h, w, seed, b->index_base + i0, s);
         if (rc) return rc;
@@ -598,13 +614,13 @@ int llfe_init(int device, llfe_ctx **out) {
     llfe_ctx *c = new llfe_ctx();
     c->device = device;
     for (hipEvent_t *e : {&c->chunk_done[0], &c->chunk_done[1], &c->mask_done[0], &c->mask_done[1], &c->start_ev,
-                          &c->stream_done[0], &c->stream_done[1]})
+                          &c->stream_done[0], &c->stream_done[1], &c->mask_ready[0], &c->mask_ready[1]})
         if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) {
             llfe_destroy(c);
             return LLFE_ERR_HIP;
         }
-    for (hipStream_t &st : c->streams)
-        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+    for (hipStream_t *st : {&c->streams[0], &c->streams[1], &c->copy_stream})
+        if (hipStreamCreateWithFlags(st, hipStreamNonBlocking) != hipSuccess) {
             llfe_destroy(c);
             return LLFE_ERR_HIP;
         }
@@ -623,12 +639,12 @@ int llfe_init(int device, llfe_ctx **out) {
 int llfe_destroy(llfe_ctx *ctx) {
     if (!ctx) return LLFE_OK;
     (void)hipSetDevice(ctx->device);
-    for (hipStream_t st : ctx->streams)
+    for (hipStream_t st : {ctx->streams[0], ctx->streams[1], ctx->copy_stream})
         if (st) (void)hipStreamSynchronize(st);
     for (hipEvent_t e : {ctx->chunk_done[0], ctx->chunk_done[1], ctx->mask_done[0], ctx->mask_done[1], ctx->start_ev,
-                         ctx->stream_done[0], ctx->stream_done[1]})
+                         ctx->stream_done[0], ctx->stream_done[1], ctx->mask_ready[0], ctx->mask_ready[1]})
         if (e) (void)hipEventDestroy(e);
-    for (hipStream_t st : ctx->streams)
+    for (hipStream_t st : {ctx->streams[0], ctx->streams[1], ctx->copy_stream})
         if (st) (void)hipStreamDestroy(st);
     delete ctx->pool;
     delete ctx;  // DevBuf / HostBuf members free themselves
