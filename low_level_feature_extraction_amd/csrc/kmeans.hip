@@ -258,17 +258,36 @@ __device__ __forceinline__ uint32_t cube_sum(const CubeGeo &g, int cx, int cy, i
     return (uint32_t)(g.n * (ax * ax + ay * ay + az * az) + 2 * (ax * g.sx + ay * g.sy + az * g.sz) + g.s2);
 }
 
+// per lane: bit `lane` of the wave-uniform 64-bit mask m ? a : b -- one v_cndmask_b32
+// reading m as a lane mask from an SGPR pair
+__device__ __forceinline__ uint32_t lane_sel(unsigned long long m, uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, %2, %1, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+    return r;
+}
+
+// the colour of mask bit `lane` relative to its cube's origin (bit = i*16 + j*4 + b)
+__device__ __forceinline__ uint32_t lane_offset(int lane) {
+    return ((uint32_t)(lane >> 4) << 16) | ((uint32_t)((lane >> 2) & 3) << 8) | (uint32_t)(lane & 3);
+}
+__device__ __forceinline__ uint32_t cube_origin_key(uint32_t id) {
+    return ((((id >> 12) & 63u) * 4u) << 16) | ((((id >> 6) & 63u) * 4u) << 8) | ((id & 63u) * 4u);
+}
+
 // Boundary colours are packed densely into the wave's lanes before they are labelled:
 // the colours of cube (m, id) go to lanes [fill, fill + popc(m)) of pk (ds_permute
-// push; lane b's rank among the set bits comes from mbcnt).  fill + popc(m) <= 64.
-__device__ __forceinline__ void pack_cube(uint32_t &pk, int fill, unsigned long long m, uint32_t id, int lane) {
+// push; lane b's rank among the set bits comes from mbcnt).  fill + popc(m) <= 64;
+// m and id are wave-uniform (SGPRs).
+__device__ __forceinline__ uint32_t lane_off_rel(int fill) { return (uint32_t)(__lane_id() - fill); }
+__device__ __forceinline__ void pack_cube(uint32_t &pk, int fill, unsigned long long m, uint32_t id,
+                                          uint32_t lane_off) {
     const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
     const int n = __popcll(m);
-    const bool has = (m >> lane) & 1ull;
     // lanes without a colour push into a lane outside [fill, fill + n) (ignored)
-    const int dst = has ? fill + (int)rank : (fill > 0 ? 0 : 63);
-    const uint32_t v = (uint32_t)__builtin_amdgcn_ds_permute(dst * 4, (int)cube_key(id, lane));
-    if (lane >= fill && lane < fill + n) pk = v;
+    const uint32_t dst = lane_sel(m, (uint32_t)fill + rank, fill > 0 ? 0u : 63u);
+    const uint32_t v = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst * 4u), (int)(cube_origin_key(id) | lane_off));
+    const uint32_t rel = lane_off_rel(fill);
+    pk = rel < (uint32_t)n ? v : pk;
 }
 
 // The cube table is streamed 64 entries per wave step with the next CPF steps' 16-B
@@ -486,6 +505,7 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
         unsigned long long acc0 = 0, acc1 = 0, acc2 = 0, fails = 0;
         int Pcur = -1;
         uint32_t pk = 0;  // packed boundary colours in lanes [0, fill)
+        const uint32_t loff = lane_offset(lane);
         int fill = 0;
         auto flush_pk = [&]() {
             if (lane < fill) {
@@ -585,7 +605,7 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
                     const uint32_t id = __builtin_amdgcn_readlane(e.id, src);
                     const int n = __popcll(m);
                     if (fill + n > 64) flush_pk();
-                    pack_cube(pk, fill, m, id, lane);
+                    pack_cube(pk, fill, m, id, loff);
                     fill += n;
                     fails += (unsigned long long)n;
                 }
@@ -969,6 +989,7 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
                                           1.f;
             unsigned long long fails = 0;
             uint32_t pk = 0;  // packed boundary colours in lanes [0, fill)
+            const uint32_t loff = lane_offset(lane);
             int fill = 0;
             auto label_pk = [&]() {
                 if (lane < fill) {
@@ -1035,7 +1056,7 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
                     const uint32_t id = __builtin_amdgcn_readlane(e.id, src);
                     const int n = __popcll(m);
                     if (fill + n > 64) label_pk();
-                    pack_cube(pk, fill, m, id, lane);
+                    pack_cube(pk, fill, m, id, loff);
                     fill += n;
                     fails += (unsigned long long)n;
                 }
