@@ -1023,20 +1023,22 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
                     }
                     const float dv[5] = {d[0].x, d[0].y, d[1].x, d[1].y, d[2].x};
                     const float m1 = fminf(fminf(fminf(dv[0], dv[1]), fminf(dv[2], dv[3])), dv[4]);
-                    k = 4;
-                    k = dv[3] == m1 ? 3 : k;
-                    k = dv[2] == m1 ? 2 : k;
-                    k = dv[1] == m1 ? 1 : k;
-                    k = dv[0] == m1 ? 0 : k;
-                    // every other centre j must be farther by more than T[k][j] at q
-                    pass = true;
-#pragma unroll
-                    for (int j = 0; j < 5; j++) {
-                        float t = thr[0][j];
-#pragma unroll
-                        for (int kk = 1; kk < 5; kk++) t = k == kk ? thr[kk][j] : t;
-                        pass = pass && (dv[j] - m1 > t);
-                    }
+                    // k = first minimum; every other centre j must be farther by more than
+                    // T[k][j] at q.  T is symmetric and dv[k] = m1, so the test per pair
+                    // (a, b) is |dv[a] - dv[b]| > T[a][b]: ten compares into lane masks,
+                    // combined per k with scalar mask logic
+                    const bool e0 = dv[0] == m1, e1 = dv[1] == m1, e2 = dv[2] == m1, e3 = dv[3] == m1;
+                    const bool is0 = e0, is1 = !e0 && e1, is2 = !e0 && !e1 && e2, is3 = !e0 && !e1 && !e2 && e3,
+                               is4 = !(e0 || e1 || e2 || e3);
+                    const bool o01 = fabsf(dv[0] - dv[1]) > thr[0][1], o02 = fabsf(dv[0] - dv[2]) > thr[0][2],
+                               o03 = fabsf(dv[0] - dv[3]) > thr[0][3], o04 = fabsf(dv[0] - dv[4]) > thr[0][4],
+                               o12 = fabsf(dv[1] - dv[2]) > thr[1][2], o13 = fabsf(dv[1] - dv[3]) > thr[1][3],
+                               o14 = fabsf(dv[1] - dv[4]) > thr[1][4], o23 = fabsf(dv[2] - dv[3]) > thr[2][3],
+                               o24 = fabsf(dv[2] - dv[4]) > thr[2][4], o34 = fabsf(dv[3] - dv[4]) > thr[3][4];
+                    pass = (is0 && o01 && o02 && o03 && o04) || (is1 && o01 && o12 && o13 && o14) ||
+                           (is2 && o02 && o12 && o23 && o24) || (is3 && o03 && o13 && o23 && o34) ||
+                           (is4 && o04 && o14 && o24 && o34);
+                    k = is0 ? 0 : (is1 ? 1 : (is2 ? 2 : (is3 ? 3 : 4)));
                 }
                 if (pass) {
                     const CubeGeo g = cube_geo(e);
