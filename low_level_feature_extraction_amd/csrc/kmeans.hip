@@ -128,6 +128,7 @@ __device__ __forceinline__ int label5p(uint32_t key, const CentP &c) {
 }
 
 constexpr int PF = 4;  // steps of 16-B key loads kept in flight per wave
+constexpr int kStage = 128;  // per-wave LDS ring of boundary colours awaiting labelling
 
 // the 4 keys of lane `lane` in 256-point step `s` (zeros past the full steps)
 __device__ __forceinline__ uint4 load_step(const uint32_t *pts, int s, int se_full, int lane) {
@@ -174,6 +175,7 @@ struct KmSmem {
     int icc[kMaxK][3];                   // chosen centres (integer colours)
     unsigned long long sel_pts;          // colours the selection scans read
     unsigned long long wchunk[3][KW];    // per trial: sum of D over each wave's chunk
+    uint32_t stage[KW][kStage + 64];     // per-wave ring of boundary colours (+ a dummy row)
     unsigned long long qtot;             // sum of |p|^2 over all colours (exact)
 };
 
@@ -988,17 +990,24 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
                                              fabsf(cu.z[j] - cu.z[k])) +
                                           1.f;
             unsigned long long fails = 0;
-            uint32_t pk = 0;  // packed boundary colours in lanes [0, fill)
+            // boundary colours: each undecided cube's lanes (lane = mask bit) store their
+            // colour into this wave's LDS ring at head + rank (a dummy slot per lane when
+            // the bit is clear); 64 staged colours at a time are read back densely and
+            // labelled.  Stores are fire-and-forget, so cubes do not serialise on LDS
+            // latency the way a register permute would.
+            uint32_t *stg = sm.stage[wid];
             const uint32_t loff = lane_offset(lane);
-            int fill = 0;
-            auto label_pk = [&]() {
-                if (lane < fill) {
-                    const int l = label5p(pk, c);
-                    atomicAdd(&sm.accA[l][tid], (unsigned long long)((pk >> 16) & 255u) |
-                                                    ((unsigned long long)((pk >> 8) & 255u) << 32));
-                    atomicAdd(&sm.accB[l][tid], (unsigned long long)(pk & 255u) | (1ull << 32));
+            int head = 0, tail = 0;  // wave-uniform ring counters
+            auto label_stage = [&](int count) {
+                __builtin_amdgcn_wave_barrier();
+                if (lane < count) {
+                    const uint32_t kq = stg[(tail + lane) & (kStage - 1)];
+                    const int l = label5p(kq, c);
+                    atomicAdd(&sm.accA[l][tid], (unsigned long long)((kq >> 16) & 255u) |
+                                                    ((unsigned long long)((kq >> 8) & 255u) << 32));
+                    atomicAdd(&sm.accB[l][tid], (unsigned long long)(kq & 255u) | (1ull << 32));
                 }
-                fill = 0;
+                tail += count;
             };
             CubeRing ring;
             ring.init(ctab, cb, cend, lane);
@@ -1050,20 +1059,27 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
                 // cubes straddling a boundary: their colours (enumerated from the
                 // occupancy mask, no key loads) packed densely into the lanes and
                 // labelled 64 at a time
+#ifdef LLFE_EXP_NO_BOUNDARY
+                unsigned long long fm = 0;
+#else
                 unsigned long long fm = __ballot(valid && !pass);
+#endif
                 while (fm) {
                     const int src = __builtin_ctzll(fm);
                     fm &= fm - 1;
                     const unsigned long long m = lane_mask(e, src);
                     const uint32_t id = __builtin_amdgcn_readlane(e.id, src);
+                    const uint32_t rank =
+                        __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    const uint32_t slot = lane_sel(m, ((uint32_t)head + rank) & (kStage - 1), kStage + lane);
+                    stg[slot] = cube_origin_key(id) | loff;
                     const int n = __popcll(m);
-                    if (fill + n > 64) label_pk();
-                    pack_cube(pk, fill, m, id, loff);
-                    fill += n;
+                    head += n;
                     fails += (unsigned long long)n;
+                    if (head - tail >= 64) label_stage(64);
                 }
             }
-            label_pk();
+            if (head > tail) label_stage(head - tail);
             if (lane == 0 && fails) atomicAdd(&sm.fail_pts, fails);
         } else {
         // The sweep is load-latency bound: keep the next PF steps' 16-B loads in flight
