@@ -3,7 +3,7 @@
 # crash/timeout) one bench line.  Outputs under gpurun_out/.
 set -u
 mkdir -p gpurun_out
-timeout -k 10 1200 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
 rc=$?
 tail -30 gpurun_out/gpu_tests.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest exit $rc: stopping"; exit $rc; fi
