@@ -285,6 +285,8 @@ struct Profiler {
     }
 };
 
+size_t shadow_tiles(int n, int h, int w) { return (size_t)n * tiles_x(w) * tiles_y(h); }
+
 int default_threads() {
     const char *e = getenv("LLFE_HOST_THREADS");
     if (e && atoi(e) > 0) return atoi(e);
@@ -494,13 +496,12 @@ int enqueue_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_
     // d_shadow / d_bits of this workspace may still be in the previous chunk's D2H
     if (ctx->w_mask_slot[q] >= 0) HIPCHK(ctx, hipStreamWaitEvent(s, ctx->mask_done[ctx->w_mask_slot[q]], 0));
     if (want_shp || want_shd) {
-        HIPCHK(ctx, W.d_shadow.ensure(2 * (size_t)n));
+        HIPCHK(ctx, W.d_shadow.ensure(2 * (size_t)n + shadow_tiles(n, h, w)));
         if (want_shp) HIPCHK(ctx, W.d_cls.ensure((size_t)n * P));
-        if (want_shd) HIPCHK(ctx, hipMemsetAsync(W.d_shadow.p, 0, sizeof(unsigned long long) * 2 * n, s));
         TIMED(ctx, s, "k_stencil", (double)n * P * (3 + (want_shp ? 1 : 0)),
               launch_stencil(img, n, h, w, want_shp ? W.d_cls.p : nullptr, nullptr,
-                             want_shd ? W.d_shadow.p : nullptr, want_shd ? W.d_shadow.p + n : nullptr, ctx->sp,
-                             s));
+                             want_shd ? W.d_shadow.p : nullptr, want_shd ? W.d_shadow.p + n : nullptr,
+                             (uint2 *)(W.d_shadow.p + 2 * n), ctx->sp, s));
     }
     // shapes + shadows first: their results go to the host (event mask_done) while the
     // GPU is still in this chunk's colour stage, so contour tracing overlaps k-means
@@ -726,7 +727,7 @@ int llfe_gray_blur5(llfe_ctx *ctx, const uint8_t *bgr, uint8_t *blurred, int32_t
                     llfe_stream stream) {
     if (!ctx || !valid_dims(n, h, w) || !bgr || !blurred) return LLFE_ERR_INVALID;
     HIPCHK(ctx, hipSetDevice(ctx->device));
-    HIPCHK(ctx, launch_stencil(bgr, n, h, w, nullptr, blurred, nullptr, nullptr, ctx->sp, (hipStream_t)stream));
+    HIPCHK(ctx, launch_stencil(bgr, n, h, w, nullptr, blurred, nullptr, nullptr, nullptr, ctx->sp, (hipStream_t)stream));
     HIPCHK(ctx, hipStreamSynchronize((hipStream_t)stream));
     return LLFE_OK;
 }
@@ -735,7 +736,7 @@ int llfe_edge_classes(llfe_ctx *ctx, const uint8_t *bgr, uint8_t *classes, int32
                       llfe_stream stream) {
     if (!ctx || !valid_dims(n, h, w) || !bgr || !classes) return LLFE_ERR_INVALID;
     HIPCHK(ctx, hipSetDevice(ctx->device));
-    HIPCHK(ctx, launch_stencil(bgr, n, h, w, classes, nullptr, nullptr, nullptr, ctx->sp, (hipStream_t)stream));
+    HIPCHK(ctx, launch_stencil(bgr, n, h, w, classes, nullptr, nullptr, nullptr, nullptr, ctx->sp, (hipStream_t)stream));
     HIPCHK(ctx, hipStreamSynchronize((hipStream_t)stream));
     return LLFE_OK;
 }
@@ -747,7 +748,7 @@ int llfe_shape_mask(llfe_ctx *ctx, const uint8_t *bgr, uint8_t *mask, int32_t n,
     hipStream_t s = (hipStream_t)stream;
     Work &W = ctx->ws[0];  // stage entry points run on the caller's stream, slot 0
     HIPCHK(ctx, W.d_cls.ensure((size_t)n * h * w));
-    HIPCHK(ctx, launch_stencil(bgr, n, h, w, W.d_cls.p, nullptr, nullptr, nullptr, ctx->sp, s));
+    HIPCHK(ctx, launch_stencil(bgr, n, h, w, W.d_cls.p, nullptr, nullptr, nullptr, nullptr, ctx->sp, s));
     int rc = run_hysteresis_dilate(ctx, W, n, h, w, nullptr, mask, s);
     if (rc) return rc;
     HIPCHK(ctx, hipStreamSynchronize(s));
@@ -761,9 +762,9 @@ int llfe_shadow_stats(llfe_ctx *ctx, const uint8_t *bgr, uint64_t *sums, uint64_
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t s = (hipStream_t)stream;
     Work &W = ctx->ws[0];
-    HIPCHK(ctx, W.d_shadow.ensure(2 * (size_t)n));
-    HIPCHK(ctx, hipMemsetAsync(W.d_shadow.p, 0, sizeof(unsigned long long) * 2 * n, s));
-    HIPCHK(ctx, launch_stencil(bgr, n, h, w, nullptr, nullptr, W.d_shadow.p, W.d_shadow.p + n, ctx->sp, s));
+    HIPCHK(ctx, W.d_shadow.ensure(2 * (size_t)n + shadow_tiles(n, h, w)));
+    HIPCHK(ctx, launch_stencil(bgr, n, h, w, nullptr, nullptr, W.d_shadow.p, W.d_shadow.p + n,
+                               (uint2 *)(W.d_shadow.p + 2 * n), ctx->sp, s));
     HIPCHK(ctx, hipMemcpyAsync(sums, W.d_shadow.p, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, s));
     HIPCHK(ctx, hipMemcpyAsync(counts, W.d_shadow.p + n, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, s));
     HIPCHK(ctx, hipStreamSynchronize(s));

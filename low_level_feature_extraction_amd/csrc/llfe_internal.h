@@ -21,9 +21,10 @@ struct StencilParams {
 //   cls (may be null): n x h x w u8, 0 weak / 1 suppressed / 2 strong
 //   blurred (may be null): n x h x w u8 (parity of GaussianBlur 5x5)
 //   shadow_sum/shadow_cnt (may be null): per image u64 accumulators (zeroed by caller)
+// shadow_sum / shadow_cnt (when non-null) need tile_part scratch of n * tiles_x(w) * tiles_y(h)
 hipError_t launch_stencil(const uint8_t *bgr, int n, int h, int w, uint8_t *cls, uint8_t *blurred,
-                          unsigned long long *shadow_sum, unsigned long long *shadow_cnt, const StencilParams &p,
-                          hipStream_t s);
+                          unsigned long long *shadow_sum, unsigned long long *shadow_cnt, uint2 *tile_part,
+                          const StencilParams &p, hipStream_t s);
 
 // Canny hysteresis as connected components + dilate(3x3) + bit-pack (hysteresis.hip).
 // Workspace: lab n*h*w u16; parent/sroot/roots over hysteresis_ids() entries; nroots

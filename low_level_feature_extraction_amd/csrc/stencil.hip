@@ -34,14 +34,6 @@ __device__ __forceinline__ int reflect101(int p, int len) {
     return p;
 }
 
-struct __align__(16) StencilSmem {
-    uint8_t gray[GH][GW];
-    uint16_t hb[GH][BWD];
-    uint8_t blur[BHT][BWD];
-    uint16_t mag[MH][MW];
-    float hf[BHT][TW];
-};
-
 // ---------------------------------------------------------------- interior tiles
 // Tiles whose whole window lies inside the image (88 % of a 1080p frame) need no
 // border handling: every stage works on 4 consecutive pixels per thread with dword /
@@ -53,69 +45,106 @@ constexpr int FMH = TH + 2, FMW = TW + 2;
 
 struct __align__(16) FastSmem {
     uint32_t g[GH][FGW / 4];          // gray, 4 per dword
-    uint2 hb[GH][FBW / 4];            // horizontal blur5 sums, 4 x u16 per entry
+    uint2 hb[GH][FBW / 4];            // horizontal blur5 sums (unscaled taps), 4 x u16 per entry
     uint32_t blur[BHT][FBW / 4];      // blurred gray rows y in [ty0 - 5, ty0 + 37)
     uint16_t md[FMH][FMW + 2];        // |dx|+|dy| | NMS direction << 12, tile + 1 halo
     float4 hf[BHT][TW / 4];           // CV_32F Gauss11 row pass
+    uint2 red[NT / 64];               // per-wave shadow (sum, count)
 };
 
 __device__ __forceinline__ uint32_t byte_of(uint32_t w, int i) { return (w >> (8 * i)) & 255u; }
 
-__device__ void stencil_interior(FastSmem &sm, const uint8_t *__restrict__ src, int H, int W, int tx0, int ty0,
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+__device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+
+template <bool BORDER>
+__device__ void stencil_tile(FastSmem &sm, const uint8_t *__restrict__ src, int H, int W, int tx0, int ty0,
                                  uint8_t *__restrict__ cls, uint8_t *__restrict__ blurred_out,
-                                 unsigned long long *shadow_sum, unsigned long long *shadow_cnt,
+                                 uint2 *tile_part,
                                  const StencilParams &prm) {
     const int tid = threadIdx.x;
-    // 1) gray: 4 BGR pixels (12 bytes, 3 dwords) -> one dword of gray
+    // 1) gray: 4 BGR pixels (12 bytes, 3 dwords) -> one dword of gray.  Per pixel the
+    //    (B, G) pair is one v_perm into packed u16 and Y = dot2((B, G), (1868, 9617)) +
+    //    4899 R + 2^13, >> 14 (exact: every term is an integer < 2^32).
+    if (BORDER) {
+        // window pixels outside the image take the gray of their REFLECT_101 image
+        // pixel: exact for the blur5 taps (<= 2 outside); deeper values are replaced
+        // after stage 3 (REPLICATE of the blurred image)
+        for (int u = tid; u < GH * FGW; u += NT) {
+            const int row = u / FGW, c = u - row * FGW;
+            const int Y = reflect101(ty0 - HG + row, H), X = reflect101(tx0 - 8 + c, W);
+            const uint8_t *q = src + ((size_t)Y * W + X) * 3;
+            ((uint8_t *)sm.g[row])[c] = (uint8_t)((q[0] * 1868u + q[1] * 9617u + q[2] * 4899u + 8192u) >> 14);
+        }
+    } else
     for (int u = tid; u < GH * (FGW / 4); u += NT) {
         const int row = u / (FGW / 4), q = u - row * (FGW / 4);
         const uint32_t *p = (const uint32_t *)(src + ((size_t)(ty0 - HG + row) * W + (tx0 - 8 + 4 * q)) * 3);
         const uint32_t d0 = p[0], d1 = p[1], d2 = p[2];
-        const uint32_t b[12] = {byte_of(d0, 0), byte_of(d0, 1), byte_of(d0, 2), byte_of(d0, 3),
-                                byte_of(d1, 0), byte_of(d1, 1), byte_of(d1, 2), byte_of(d1, 3),
-                                byte_of(d2, 0), byte_of(d2, 1), byte_of(d2, 2), byte_of(d2, 3)};
-        uint32_t o = 0;
-#pragma unroll
-        for (int j = 0; j < 4; j++)
-            o |= ((b[3 * j] * 1868u + b[3 * j + 1] * 9617u + b[3 * j + 2] * 4899u + 8192u) >> 14) << (8 * j);
-        sm.g[row][q] = o;
+        // v_perm selector bytes: 0-3 = second operand, 4-7 = first operand, 0x0c = 0
+        const u16x2 bg0 = as_u16x2(__builtin_amdgcn_perm(0u, d0, 0x0c010c00u));
+        const u16x2 bg1 = as_u16x2(__builtin_amdgcn_perm(d1, d0, 0x0c040c03u));
+        const u16x2 bg2 = as_u16x2(__builtin_amdgcn_perm(0u, d1, 0x0c030c02u));
+        const u16x2 bg3 = as_u16x2(__builtin_amdgcn_perm(0u, d2, 0x0c020c01u));
+        const u16x2 wbg = {1868, 9617};
+        const uint32_t y0 = __builtin_amdgcn_udot2(bg0, wbg, byte_of(d0, 2) * 4899u + 8192u, false) >> 14;
+        const uint32_t y1 = __builtin_amdgcn_udot2(bg1, wbg, byte_of(d1, 1) * 4899u + 8192u, false) >> 14;
+        const uint32_t y2 = __builtin_amdgcn_udot2(bg2, wbg, byte_of(d2, 0) * 4899u + 8192u, false) >> 14;
+        const uint32_t y3 = __builtin_amdgcn_udot2(bg3, wbg, byte_of(d2, 3) * 4899u + 8192u, false) >> 14;
+        sm.g[row][q] = y0 | (y1 << 8) | (y2 << 16) | (y3 << 24);
     }
     __syncthreads();
-    // 2) horizontal blur5: hb col c <-> x = tx0 - 6 + c; taps are gray cols c .. c + 4
+    // 2) horizontal blur5 in packed u16 with the unscaled taps [1, 4, 6, 4, 1] (sum of a
+    //    row <= 16 * 255): hb col c <-> x = tx0 - 6 + c; taps are gray cols c .. c + 4.
+    //    (the 8U blur is (sum_ij w_i w_j g + 128) >> 8, so both passes fit in 16 bits)
     for (int u = tid; u < GH * (FBW / 4); u += NT) {
         const int row = u / (FBW / 4), q = u - row * (FBW / 4);
         const uint32_t w0 = sm.g[row][q], w1 = sm.g[row][q + 1];
-        uint32_t b[8];
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            b[i] = byte_of(w0, i);
-            b[4 + i] = byte_of(w1, i);
-        }
-        uint32_t h[4];
-#pragma unroll
-        for (int j = 0; j < 4; j++) h[j] = 16u * (b[j] + b[j + 4]) + 64u * (b[j + 1] + b[j + 3]) + 96u * b[j + 2];
-        sm.hb[row][q] = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+        const u16x2 b01 = as_u16x2(__builtin_amdgcn_perm(0u, w0, 0x0c010c00u));
+        const u16x2 b12 = as_u16x2(__builtin_amdgcn_perm(0u, w0, 0x0c020c01u));
+        const u16x2 b23 = as_u16x2(__builtin_amdgcn_perm(0u, w0, 0x0c030c02u));
+        const u16x2 b34 = as_u16x2(__builtin_amdgcn_perm(w1, w0, 0x0c040c03u));
+        const u16x2 b45 = as_u16x2(__builtin_amdgcn_perm(0u, w1, 0x0c010c00u));
+        const u16x2 b56 = as_u16x2(__builtin_amdgcn_perm(0u, w1, 0x0c020c01u));
+        const u16x2 b67 = as_u16x2(__builtin_amdgcn_perm(0u, w1, 0x0c030c02u));
+        const u16x2 four = {4, 4}, six = {6, 6};
+        const u16x2 h01 = (b12 + b34) * four + (b01 + b45) + b23 * six;
+        const u16x2 h23 = (b34 + b56) * four + (b23 + b67) + b45 * six;
+        sm.hb[row][q] = make_uint2(as_u32(h01), as_u32(h23));
     }
     __syncthreads();
     // 3) vertical blur5 -> blur rows ly (y = ty0 - 5 + ly) from hb rows ly .. ly + 4
     for (int u = tid; u < BHT * (FBW / 4); u += NT) {
         const int ly = u / (FBW / 4), q = u - ly * (FBW / 4);
-        uint32_t s[4] = {0, 0, 0, 0};
-        const uint32_t kw[5] = {16u, 64u, 96u, 64u, 16u};
+        u16x2 s01 = {128, 128}, s23 = {128, 128};
+        const uint16_t kw[5] = {1, 4, 6, 4, 1};
 #pragma unroll
         for (int r = 0; r < 5; r++) {
             const uint2 v = sm.hb[ly + r][q];
-            s[0] += kw[r] * (v.x & 0xFFFFu);
-            s[1] += kw[r] * (v.x >> 16);
-            s[2] += kw[r] * (v.y & 0xFFFFu);
-            s[3] += kw[r] * (v.y >> 16);
+            const u16x2 k = {kw[r], kw[r]};
+            s01 = as_u16x2(v.x) * k + s01;
+            s23 = as_u16x2(v.y) * k + s23;
         }
-        uint32_t o = 0;
-#pragma unroll
-        for (int j = 0; j < 4; j++) o |= ((s[j] + 32768u) >> 16) << (8 * j);
-        sm.blur[ly][q] = o;
+        const u16x2 e8 = {8, 8};
+        s01 = s01 >> e8;
+        s23 = s23 >> e8;
+        sm.blur[ly][q] = __builtin_amdgcn_perm(as_u32(s23), as_u32(s01), 0x06040200u);
     }
     __syncthreads();
+    if (BORDER) {
+        // blurred values outside the image: REPLICATE (Sobel's and the CV_32F Gauss11's
+        // border on the blurred image)
+        for (int u = tid; u < BHT * FBW; u += NT) {
+            const int ly = u / FBW, c = u - ly * FBW, Y = ty0 - 5 + ly, X = tx0 - 6 + c;
+            if ((unsigned)Y >= (unsigned)H || (unsigned)X >= (unsigned)W) {
+                const int sy = clampi(Y, 0, H - 1) - (ty0 - 5), sx = clampi(X, 0, W - 1) - (tx0 - 6);
+                ((uint8_t *)sm.blur[ly])[c] = ((const uint8_t *)sm.blur[sy])[sx];
+            }
+        }
+        __syncthreads();
+    }
     // blur byte at tile-relative (row ly, col c) where c <-> x = tx0 - 6 + c
     auto BL = [&](int ly, int c) -> int { return (int)byte_of(sm.blur[ly][c >> 2], c & 3); };
 
@@ -125,7 +154,13 @@ __device__ void stencil_interior(FastSmem &sm, const uint8_t *__restrict__ src, 
             uint32_t o = 0;
 #pragma unroll
             for (int j = 0; j < 4; j++) o |= (uint32_t)BL(y + 5, 4 * q + j + 6) << (8 * j);
-            *(uint32_t *)(blurred_out + (size_t)(ty0 + y) * W + tx0 + 4 * q) = o;
+            if (BORDER) {
+                const int Y = ty0 + y, X = tx0 + 4 * q;
+                if (Y < H)
+                    for (int j = 0; j < 4 && X + j < W; j++) blurred_out[(size_t)Y * W + X + j] = (uint8_t)(o >> (8 * j));
+            } else {
+                *(uint32_t *)(blurred_out + (size_t)(ty0 + y) * W + tx0 + 4 * q) = o;
+            }
         }
     }
 
@@ -158,7 +193,8 @@ __device__ void stencil_interior(FastSmem &sm, const uint8_t *__restrict__ src, 
                 if (ay < tg22x) dir = 0;
                 else if (ay > tg22x + (ax << 16)) dir = 1;
                 else dir = (gx ^ gy) < 0 ? 2 : 3;
-                sm.md[my][mc] = (uint16_t)(m | (dir << 12));
+                const bool out = BORDER && ((unsigned)(ty0 - 1 + my) >= (unsigned)H || (unsigned)(tx0 - 1 + mc) >= (unsigned)W);
+                sm.md[my][mc] = out ? (uint16_t)0 : (uint16_t)(m | (dir << 12));  // Canny: no magnitude outside
             }
         }
         __syncthreads();
@@ -187,261 +223,153 @@ __device__ void stencil_interior(FastSmem &sm, const uint8_t *__restrict__ src, 
                 }
                 o |= c << (8 * j);
             }
-            *(uint32_t *)(cls + (size_t)(ty0 + ty) * W + tx0 + 4 * q) = o;
+            if (BORDER) {
+                const int Y = ty0 + ty, X = tx0 + 4 * q;
+                if (Y < H)
+                    for (int j = 0; j < 4 && X + j < W; j++) cls[(size_t)Y * W + X + j] = (uint8_t)(o >> (8 * j));
+            } else {
+                *(uint32_t *)(cls + (size_t)(ty0 + ty) * W + tx0 + 4 * q) = o;
+            }
         }
     }
 
-    if (shadow_sum) {
-        // 6) CV_32F row pass (fma chain left -> right) for 4 consecutive x = tx0 + 4q + j:
-        //    taps are blur cols 4q + 1 + j .. 4q + 11 + j (dwords q .. q + 3)
-        for (int u = tid; u < BHT * (TW / 4); u += NT) {
-            const int ly = u / (TW / 4), q = u - ly * (TW / 4);
-            float bvf[16];
+    if (tile_part) {
+        // 6) CV_32F row pass (fma chain left -> right) for 4 consecutive x = tx0 + 4q + j
+        //    on two rows at once (packed FP32: lane 0 = row ly, lane 1 = row ly + 1; each
+        //    lane is the same fma chain as the scalar form): taps are blur cols
+        //    4q + 1 + j .. 4q + 11 + j (dwords q .. q + 3)
+        for (int u = tid; u < (BHT / 2) * (TW / 4); u += NT) {
+            const int lp = u / (TW / 4), q = u - lp * (TW / 4), ly = 2 * lp;
+            f32x2 bv[16];
 #pragma unroll
             for (int d = 0; d < 4; d++) {
-                const uint32_t w = sm.blur[ly][q + d];
+                const uint32_t wa = sm.blur[ly][q + d], wb = sm.blur[ly + 1][q + d];
 #pragma unroll
-                for (int i = 0; i < 4; i++) bvf[4 * d + i] = (float)byte_of(w, i);
+                for (int i = 0; i < 4; i++) bv[4 * d + i] = f32x2{(float)byte_of(wa, i), (float)byte_of(wb, i)};
             }
-            float out[4];
+            f32x2 out[4];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                float s = 0.0f;
+                f32x2 acc = {0.0f, 0.0f};
 #pragma unroll
-                for (int k = 0; k < 11; k++) s = __builtin_fmaf(bvf[1 + j + k], prm.k11[k], s);
-                out[j] = s;
+                for (int k = 0; k < 11; k++)
+                    acc = __builtin_elementwise_fma(bv[1 + j + k], f32x2{prm.k11[k], prm.k11[k]}, acc);
+                out[j] = acc;
             }
-            sm.hf[ly][q] = make_float4(out[0], out[1], out[2], out[3]);
+            sm.hf[ly][q] = make_float4(out[0].x, out[1].x, out[2].x, out[3].x);
+            sm.hf[ly + 1][q] = make_float4(out[0].y, out[1].y, out[2].y, out[3].y);
         }
         __syncthreads();
-        // 7) column pass (centre, then symmetric pairs inner -> outer), cvRound, mask
-        unsigned long long lsum = 0, lcnt = 0;
+        // 7) column pass (centre, then symmetric pairs inner -> outer), cvRound, mask;
+        //    packed FP32 over column pairs (j, j + 1)
+        uint32_t lsum = 0, lcnt = 0;
         for (int u = tid; u < TH * (TW / 4); u += NT) {
             const int ty = u / (TW / 4), q = u - ty * (TW / 4);
             const int ly = ty + 5;
             const float4 c0 = sm.hf[ly][q];
-            float s[4] = {__builtin_fmaf(c0.x, prm.k11[5], 0.0f), __builtin_fmaf(c0.y, prm.k11[5], 0.0f),
-                          __builtin_fmaf(c0.z, prm.k11[5], 0.0f), __builtin_fmaf(c0.w, prm.k11[5], 0.0f)};
+            const f32x2 w5 = {prm.k11[5], prm.k11[5]}, z = {0.0f, 0.0f};
+            f32x2 s01 = __builtin_elementwise_fma(f32x2{c0.x, c0.y}, w5, z);
+            f32x2 s23 = __builtin_elementwise_fma(f32x2{c0.z, c0.w}, w5, z);
 #pragma unroll
             for (int d = 1; d <= 5; d++) {
                 const float4 a = sm.hf[ly + d][q], b = sm.hf[ly - d][q];
-                s[0] = __builtin_fmaf(a.x + b.x, prm.k11[5 + d], s[0]);
-                s[1] = __builtin_fmaf(a.y + b.y, prm.k11[5 + d], s[1]);
-                s[2] = __builtin_fmaf(a.z + b.z, prm.k11[5 + d], s[2]);
-                s[3] = __builtin_fmaf(a.w + b.w, prm.k11[5 + d], s[3]);
+                const f32x2 wd = {prm.k11[5 + d], prm.k11[5 + d]};
+                s01 = __builtin_elementwise_fma(f32x2{a.x, a.y} + f32x2{b.x, b.y}, wd, s01);
+                s23 = __builtin_elementwise_fma(f32x2{a.z, a.w} + f32x2{b.z, b.w}, wd, s23);
             }
+            const float sj[4] = {s01.x, s01.y, s23.x, s23.y};
             const uint32_t bw = sm.blur[ly][q + 1], bw2 = sm.blur[ly][q + 2];
             // blur cols for x = tx0 + 4q + j are 4q + 6 + j: bytes 2, 3 of dword q + 1, 0, 1 of q + 2
             const int bv[4] = {(int)byte_of(bw, 2), (int)byte_of(bw, 3), (int)byte_of(bw2, 0), (int)byte_of(bw2, 1)};
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                int mean = (int)__builtin_rintf(s[j]);
+                int mean = (int)__builtin_rintf(sj[j]);
                 mean = clampi(mean, 0, 255);
-                if (bv[j] - mean <= -2) {
+                const bool in = !BORDER || (ty0 + ty < H && tx0 + 4 * q + j < W);
+                if (in && bv[j] - mean <= -2) {
                     lsum += (unsigned)bv[j];
                     lcnt += 1;
                 }
             }
         }
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
+        for (int off = 32; off > 0; off >>= 1) {  // per wave: <= 64 x 8 x 4 x 255 < 2^32
             lsum += __shfl_xor(lsum, off);
             lcnt += __shfl_xor(lcnt, off);
         }
-        if ((tid & 63) == 0 && lcnt) {
-            atomicAdd(shadow_sum, lsum);
-            atomicAdd(shadow_cnt, lcnt);
+        // one (sum, count) per tile, no atomics: k_shadow_reduce adds the tiles up
+        if ((tid & 63) == 0) sm.red[tid >> 6] = make_uint2(lsum, lcnt);
+        __syncthreads();
+        if (tid == 0) {
+            uint2 r = sm.red[0];
+#pragma unroll
+            for (int w = 1; w < NT / 64; w++) {
+                r.x += sm.red[w].x;
+                r.y += sm.red[w].y;
+            }
+            *tile_part = r;
         }
     }
 }
 
-union StencilShared {
-    StencilSmem g;
-    FastSmem f;
-};
+// grid (n): per-image totals of the tiles' (sum, count)
+__global__ __launch_bounds__(256) void k_shadow_reduce(const uint2 *__restrict__ tile_part, int ntiles,
+                                                       unsigned long long *__restrict__ shadow_sum,
+                                                       unsigned long long *__restrict__ shadow_cnt) {
+    __shared__ unsigned long long rs[4], rc[4];
+    const int img = blockIdx.x, tid = threadIdx.x;
+    unsigned long long a = 0, b = 0;
+    for (int t = tid; t < ntiles; t += 256) {
+        const uint2 v = tile_part[(size_t)img * ntiles + t];
+        a += v.x;
+        b += v.y;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        a += __shfl_xor(a, off);
+        b += __shfl_xor(b, off);
+    }
+    if ((tid & 63) == 0) {
+        rs[tid >> 6] = a;
+        rc[tid >> 6] = b;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        shadow_sum[img] = rs[0] + rs[1] + rs[2] + rs[3];
+        shadow_cnt[img] = rc[0] + rc[1] + rc[2] + rc[3];
+    }
+}
 
 __global__ __launch_bounds__(NT) void k_stencil(const uint8_t *__restrict__ bgr, int H, int W, int ntx, int nty,
                                                 uint8_t *__restrict__ cls, uint8_t *__restrict__ blurred_out,
-                                                unsigned long long *__restrict__ shadow_sum,
-                                                unsigned long long *__restrict__ shadow_cnt, StencilParams prm) {
-    __shared__ StencilShared shm;
+                                                uint2 *__restrict__ tile_part, StencilParams prm) {
+    __shared__ FastSmem shm;
     const int tid = threadIdx.x;
     const int img = blockIdx.y;
     const int t = blockIdx.x;
     const int tx0 = (t % ntx) * TW, ty0 = (t / ntx) * TH;
     const uint8_t *src = bgr + (size_t)img * H * W * 3;
     const bool aligned = (((uintptr_t)bgr | (uintptr_t)cls | (uintptr_t)blurred_out) & 3) == 0 && (W & 3) == 0;
-    if (aligned && tx0 >= 8 && ty0 >= HG && tx0 + TW + 8 <= W && ty0 + TH + HG <= H) {
-        stencil_interior(shm.f, src, H, W, tx0, ty0, cls ? cls + (size_t)img * H * W : nullptr,
-                         blurred_out ? blurred_out + (size_t)img * H * W : nullptr,
-                         shadow_sum ? shadow_sum + img : nullptr, shadow_cnt ? shadow_cnt + img : nullptr, prm);
-        return;
-    }
-    StencilSmem &sm = shm.g;
-
-    // 1) BGR window -> gray (Y = (1868 B + 9617 G + 4899 R + 2^13) >> 14)
-    for (int i = tid; i < GH * GW; i += NT) {
-        int gy = i / GW, gx = i - gy * GW;
-        int Y = ty0 - HG + gy, X = tx0 - HG + gx;
-        uint8_t g = 0;
-        if ((unsigned)Y < (unsigned)H && (unsigned)X < (unsigned)W) {
-            const uint8_t *p = src + ((size_t)Y * W + X) * 3;
-            unsigned b = p[0], gg = p[1], r = p[2];
-            g = (uint8_t)((b * 1868u + gg * 9617u + r * 4899u + 8192u) >> 14);
-        }
-        sm.gray[gy][gx] = g;
-    }
-    __syncthreads();
-
-    // 2) horizontal blur5 (REFLECT_101) for every in-image gray row of the window,
-    //    at the (replicate-clamped) columns of the blurred region.
-    for (int i = tid; i < GH * BWD; i += NT) {
-        int gy = i / BWD, lx = i - gy * BWD;
-        int Y = ty0 - HG + gy;
-        uint16_t v = 0;
-        if ((unsigned)Y < (unsigned)H) {
-            int X = clampi(tx0 - 5 + lx, 0, W - 1);
-            int c0 = reflect101(X - 2, W) - (tx0 - HG), c1 = reflect101(X - 1, W) - (tx0 - HG);
-            int c2 = X - (tx0 - HG), c3 = reflect101(X + 1, W) - (tx0 - HG), c4 = reflect101(X + 2, W) - (tx0 - HG);
-            const uint8_t *row = sm.gray[gy];
-            v = (uint16_t)(16u * row[c0] + 64u * row[c1] + 96u * row[c2] + 64u * row[c3] + 16u * row[c4]);
-        }
-        sm.hb[gy][lx] = v;
-    }
-    __syncthreads();
-
-    // 3) vertical blur5 -> blurred region; entry (ly,lx) holds blur(clamp(ty0-5+ly), clamp(tx0-5+lx))
-    for (int i = tid; i < BHT * BWD; i += NT) {
-        int ly = i / BWD, lx = i - ly * BWD;
-        int Y = clampi(ty0 - 5 + ly, 0, H - 1);
-        int r0 = reflect101(Y - 2, H) - (ty0 - HG), r1 = reflect101(Y - 1, H) - (ty0 - HG), r2 = Y - (ty0 - HG);
-        int r3 = reflect101(Y + 1, H) - (ty0 - HG), r4 = reflect101(Y + 2, H) - (ty0 - HG);
-        uint32_t s = 16u * sm.hb[r0][lx] + 64u * sm.hb[r1][lx] + 96u * sm.hb[r2][lx] + 64u * sm.hb[r3][lx] +
-                     16u * sm.hb[r4][lx];
-        uint32_t v = (s + 32768u) >> 16;
-        sm.blur[ly][lx] = (uint8_t)(v > 255u ? 255u : v);
-    }
-    __syncthreads();
-
-    if (blurred_out) {
-        for (int i = tid; i < TH * TW; i += NT) {
-            int y = i / TW, x = i - y * TW;
-            int Y = ty0 + y, X = tx0 + x;
-            if (Y < H && X < W) blurred_out[((size_t)img * H + Y) * W + X] = sm.blur[y + 5][x + 5];
-        }
-    }
-
-    // blurred value at in-image global (Y, X) with |Y-ty0|,|X-tx0| in range
-#define BLUR(Y, X) ((int)sm.blur[(Y) - (ty0 - 5)][(X) - (tx0 - 5)])
-
-    if (cls) {
-        // 4) |dx|+|dy| on the tile + 1 halo (0 outside the image: Canny's mag border)
-        for (int i = tid; i < MH * MW; i += NT) {
-            int my = i / MW, mx = i - my * MW;
-            int y = ty0 - 1 + my, x = tx0 - 1 + mx;
-            uint16_t m = 0;
-            if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W) {
-                int ym = max(y - 1, 0), yp = min(y + 1, H - 1), xm = max(x - 1, 0), xp = min(x + 1, W - 1);
-                int gx = (BLUR(ym, xp) + 2 * BLUR(y, xp) + BLUR(yp, xp)) - (BLUR(ym, xm) + 2 * BLUR(y, xm) + BLUR(yp, xm));
-                int gy = (BLUR(yp, xm) + 2 * BLUR(yp, x) + BLUR(yp, xp)) - (BLUR(ym, xm) + 2 * BLUR(ym, x) + BLUR(ym, xp));
-                m = (uint16_t)(abs(gx) + abs(gy));
-            }
-            sm.mag[my][mx] = m;
-        }
-        __syncthreads();
-
-        // 5) non-maximum suppression + double threshold (50, 150) -> class
-        constexpr int TG22 = 13573, LOW = 50, HIGH = 150;
-        for (int i = tid; i < TH * TW; i += NT) {
-            int ty = i / TW, tx = i - ty * TW;
-            int y = ty0 + ty, x = tx0 + tx;
-            if (y >= H || x >= W) continue;
-            int m = sm.mag[ty + 1][tx + 1];
-            uint8_t v = 1;
-            if (m > LOW) {
-                int ym = max(y - 1, 0), yp = min(y + 1, H - 1), xm = max(x - 1, 0), xp = min(x + 1, W - 1);
-                int xs = (BLUR(ym, xp) + 2 * BLUR(y, xp) + BLUR(yp, xp)) - (BLUR(ym, xm) + 2 * BLUR(y, xm) + BLUR(yp, xm));
-                int ys = (BLUR(yp, xm) + 2 * BLUR(yp, x) + BLUR(yp, xp)) - (BLUR(ym, xm) + 2 * BLUR(ym, x) + BLUR(ym, xp));
-                int ax = abs(xs);
-                int ay = abs(ys) << 15;
-                int tg22x = ax * TG22;
-                bool keep;
-                if (ay < tg22x) {
-                    keep = m > sm.mag[ty + 1][tx] && m >= sm.mag[ty + 1][tx + 2];
-                } else {
-                    int tg67x = tg22x + (ax << 16);
-                    if (ay > tg67x) {
-                        keep = m > sm.mag[ty][tx + 1] && m >= sm.mag[ty + 2][tx + 1];
-                    } else {
-                        int sgn = (xs ^ ys) < 0 ? -1 : 1;
-                        keep = m > sm.mag[ty][tx + 1 - sgn] && m > sm.mag[ty + 2][tx + 1 + sgn];
-                    }
-                }
-                if (keep) v = m > HIGH ? 2 : 0;
-            }
-            cls[((size_t)img * H + y) * W + x] = v;
-        }
-    }
-
-    if (shadow_sum) {
-        // 6) CV_32F row pass of the 11x11 Gaussian (REPLICATE): fma chain left->right
-        for (int i = tid; i < BHT * TW; i += NT) {
-            int ly = i / TW, tx = i - ly * TW;
-            int x = min(tx0 + tx, W - 1);
-            const uint8_t *row = sm.blur[ly];
-            float s = 0.0f;
-#pragma unroll
-            for (int j = 0; j < 11; j++) {
-                int c = clampi(x + j - 5, 0, W - 1) - (tx0 - 5);
-                s = __builtin_fmaf((float)row[c], prm.k11[j], s);
-            }
-            sm.hf[ly][tx] = s;
-        }
-        __syncthreads();
-        // 7) column pass: centre first, then symmetric pairs inner->outer; cvRound
-        unsigned long long lsum = 0, lcnt = 0;
-        for (int i = tid; i < TH * TW; i += NT) {
-            int ty = i / TW, tx = i - ty * TW;
-            int y = ty0 + ty, x = tx0 + tx;
-            if (y >= H || x >= W) continue;
-            int ly = y - (ty0 - 5);
-            float s = __builtin_fmaf(sm.hf[ly][tx], prm.k11[5], 0.0f);
-#pragma unroll
-            for (int d = 1; d <= 5; d++) {
-                float a = sm.hf[min(y + d, H - 1) - (ty0 - 5)][tx];
-                float b = sm.hf[max(y - d, 0) - (ty0 - 5)][tx];
-                s = __builtin_fmaf(a + b, prm.k11[5 + d], s);
-            }
-            int mean = (int)__builtin_rintf(s);
-            mean = clampi(mean, 0, 255);
-            int bv = BLUR(y, x);
-            if (bv - mean <= -2) {
-                lsum += (unsigned)bv;
-                lcnt += 1;
-            }
-        }
-        // wave reduce, then one atomic pair per wave
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-            lsum += __shfl_xor(lsum, off);
-            lcnt += __shfl_xor(lcnt, off);
-        }
-        if ((tid & 63) == 0 && lcnt) {
-            atomicAdd(shadow_sum + img, lsum);
-            atomicAdd(shadow_cnt + img, lcnt);
-        }
-    }
-#undef BLUR
+    uint8_t *c = cls ? cls + (size_t)img * H * W : nullptr;
+    uint8_t *bo = blurred_out ? blurred_out + (size_t)img * H * W : nullptr;
+    uint2 *tp = tile_part ? tile_part + (size_t)img * ntx * nty + t : nullptr;
+    if (aligned && tx0 >= 8 && ty0 >= HG && tx0 + TW + 8 <= W && ty0 + TH + HG <= H)
+        stencil_tile<false>(shm, src, H, W, tx0, ty0, c, bo, tp, prm);
+    else
+        stencil_tile<true>(shm, src, H, W, tx0, ty0, c, bo, tp, prm);
 }
 
 }  // namespace
 
 hipError_t launch_stencil(const uint8_t *bgr, int n, int h, int w, uint8_t *cls, uint8_t *blurred,
-                          unsigned long long *shadow_sum, unsigned long long *shadow_cnt, const StencilParams &p,
-                          hipStream_t s) {
+                          unsigned long long *shadow_sum, unsigned long long *shadow_cnt, uint2 *tile_part,
+                          const StencilParams &p, hipStream_t s) {
     int ntx = tiles_x(w), nty = tiles_y(h);
     dim3 grid(ntx * nty, n);
-    hipLaunchKernelGGL(k_stencil, grid, dim3(NT), 0, s, bgr, h, w, ntx, nty, cls, blurred, shadow_sum, shadow_cnt, p);
+    hipLaunchKernelGGL(k_stencil, grid, dim3(NT), 0, s, bgr, h, w, ntx, nty, cls, blurred,
+                       shadow_sum ? tile_part : nullptr, p);
+    if (shadow_sum)
+        hipLaunchKernelGGL(k_shadow_reduce, dim3(n), dim3(256), 0, s, tile_part, ntx * nty, shadow_sum, shadow_cnt);
     return hipGetLastError();
 }
 

@@ -174,18 +174,32 @@ __global__ __launch_bounds__(KB) void k_uq_scatter(const uint32_t *__restrict__ 
                 kv[4 * q + 3] = v.w;
             }
         } else {
+#pragma unroll
             for (int i = 0; i < PPT; i++) kv[i] = i < n ? in[p0 + i] : 0u;
         }
-        // rank within the block's bin: one LDS atomic per run of equal bins
+        // rank within the block's bin: one LDS atomic per run of equal bins.  Static
+        // register indexing only: the atomic sits on each run's last key and returns the
+        // run's base, which a backward pass hands to the run's other keys.
+        uint32_t bins[PPT], endm = 0;
+#pragma unroll
+        for (int i = 0; i < PPT; i++) bins[i] = kv[i] >> 18;
         {
-            int i = 0;
-            while (i < n) {
-                const uint32_t bin = kv[i] >> 18;
-                int j = i + 1;
-                while (j < n && (kv[j] >> 18) == bin) j++;
-                const uint32_t r0 = atomicAdd(&cnt[bin], (uint32_t)(j - i));
-                for (int q = i; q < j; q++) pos[q] = r0 + (uint32_t)(q - i);
-                i = j;
+            int run_start = 0;
+#pragma unroll
+            for (int i = 0; i < PPT; i++) {
+                if (i > 0 && bins[i] != bins[i - 1]) run_start = i;
+                const bool end = (i == PPT - 1) || (i + 1 >= n) || (bins[i + 1] != bins[i]);
+                pos[i] = 0;
+                if (i < n && end) {
+                    pos[i] = atomicAdd(&cnt[bins[i]], (uint32_t)(i - run_start + 1)) - (uint32_t)run_start;
+                    endm |= 1u << i;
+                }
+            }
+            uint32_t cur = 0;
+#pragma unroll
+            for (int i = PPT - 1; i >= 0; i--) {
+                if (endm & (1u << i)) cur = pos[i];
+                pos[i] = cur + (uint32_t)i;
             }
         }
         __syncthreads();
@@ -201,7 +215,9 @@ __global__ __launch_bounds__(KB) void k_uq_scatter(const uint32_t *__restrict__ 
             gbase[t] = c ? base[t] + atomicAdd(cursor + (size_t)img * NPART + t, c) : 0u;
         }
         __syncthreads();
-        for (int i = 0; i < n; i++) stage[lbase[kv[i] >> 18] + pos[i]] = kv[i];
+#pragma unroll
+        for (int i = 0; i < PPT; i++)
+            if (i < n) stage[lbase[bins[i]] + pos[i]] = kv[i];
         __syncthreads();
         const int tot = (int)min((long long)SK, P - st * SK);
         for (int i = t; i < tot; i += KB) {
@@ -358,52 +374,42 @@ __global__ __launch_bounds__(UT) void k_uq_part(const uint32_t *__restrict__ par
     }
 }
 
-// grid (n): contiguous sorted keys (from the partitions' segments) and cube table
-__global__ __launch_bounds__(UT) void k_uq_gather(const uint32_t *__restrict__ skeys, long long key_stride,
+// grid (64, n): one workgroup per (partition, image) copies the partition's sorted
+// unique keys and cube entries to their place in the contiguous per-image arrays
+constexpr int GT = 256;
+__global__ __launch_bounds__(GT) void k_uq_gather(const uint32_t *__restrict__ skeys, long long key_stride,
                                                   const uint32_t *__restrict__ hist, const uint32_t *__restrict__ uq,
                                                   const uint32_t *__restrict__ cc,
                                                   const CubeEnt *__restrict__ seg_cubes, uint32_t *__restrict__ keys,
                                                   CubeEnt *__restrict__ cubes, long long cube_stride,
                                                   long long *__restrict__ n_unique, int *__restrict__ n_cubes) {
-    __shared__ uint32_t pstart[NPART], ubase[NPART + 1], cbase[NPART + 1];
-    const int img = blockIdx.x, t = threadIdx.x;
+    __shared__ uint32_t sp, su, sc, nu, nc;
+    const int R = blockIdx.x, img = blockIdx.y, t = threadIdx.x;
     if (t < 64) {
-        uint32_t tot;
-        pstart[t] = part_base(hist + (size_t)img * NPART, t, &tot);
-        uint32_t ut, ct;
-        ubase[t] = part_base(uq + (size_t)img * NPART, t, &ut);
-        cbase[t] = part_base(cc + (size_t)img * NPART, t, &ct);
-        if (t == 0) {
-            ubase[NPART] = ut;
-            cbase[NPART] = ct;
+        uint32_t tot, ut, ct;
+        const uint32_t ps = part_base(hist + (size_t)img * NPART, t, &tot);
+        const uint32_t ub = part_base(uq + (size_t)img * NPART, t, &ut);
+        const uint32_t cb = part_base(cc + (size_t)img * NPART, t, &ct);
+        if (t == R) {
+            sp = ps;
+            su = ub;
+            sc = cb;
+            nu = uq[(size_t)img * NPART + R];
+            nc = cc[(size_t)img * NPART + R];
+        }
+        if (t == 0 && R == 0) {
             n_unique[img] = ut;
             n_cubes[img] = (int)ct;
         }
     }
     __syncthreads();
-    const uint32_t U = ubase[NPART], C = cbase[NPART];
-    const uint32_t *sk = skeys + (size_t)img * key_stride;
-    uint32_t *ok = keys + (size_t)img * key_stride;
-    for (uint32_t i = t; i < U; i += UT) {
-        int lo = 0, hi = NPART - 1;  // last partition with ubase <= i
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (ubase[mid] <= i) lo = mid;
-            else hi = mid - 1;
-        }
-        ok[i] = sk[pstart[lo] + (i - ubase[lo])];
-    }
-    const CubeEnt *sc = seg_cubes + (size_t)img * NPART * 4096;
-    CubeEnt *oc = cubes + (size_t)img * cube_stride;
-    for (uint32_t i = t; i < C; i += UT) {
-        int lo = 0, hi = NPART - 1;
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (cbase[mid] <= i) lo = mid;
-            else hi = mid - 1;
-        }
-        oc[i] = sc[(size_t)lo * 4096 + (i - cbase[lo])];
-    }
+    const uint32_t U = nu, C = nc;
+    const uint32_t *sk = skeys + (size_t)img * key_stride + sp;
+    uint32_t *ok = keys + (size_t)img * key_stride + su;
+    for (uint32_t i = t; i < U; i += GT) ok[i] = sk[i];
+    const CubeEnt *scp = seg_cubes + ((size_t)img * NPART + R) * 4096;
+    CubeEnt *oc = cubes + (size_t)img * cube_stride + sc;
+    for (uint32_t i = t; i < C; i += GT) oc[i] = scp[i];
 }
 
 }  // namespace
@@ -438,7 +444,7 @@ hipError_t launch_uq_part(const uint32_t *part, int n, int64_t key_stride, const
 hipError_t launch_uq_gather(const uint32_t *skeys, int n, int64_t key_stride, const uint32_t *hist, const uint32_t *uq,
                             const uint32_t *cc, const CubeEnt *seg_cubes, uint32_t *keys, CubeEnt *cubes,
                             int64_t cube_stride, int64_t *n_unique, int32_t *n_cubes, hipStream_t s) {
-    hipLaunchKernelGGL(k_uq_gather, dim3(n), dim3(UT), 0, s, skeys, (long long)key_stride, hist, uq, cc, seg_cubes,
+    hipLaunchKernelGGL(k_uq_gather, dim3(NPART, n), dim3(GT), 0, s, skeys, (long long)key_stride, hist, uq, cc, seg_cubes,
                        keys, cubes, (long long)cube_stride, (long long *)n_unique, (int *)n_cubes);
     return hipGetLastError();
 }
