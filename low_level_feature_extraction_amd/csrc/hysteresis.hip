@@ -12,8 +12,12 @@
 //                 in different tiles (tile right column / bottom row)
 //   k_ccl_flatten every local root -> its global root (one hop); strong flags OR-ed
 //                 into the global root
-//   k_ccl_dilate  edge = strong || (maybe && root strong); 3x3 dilate in LDS; one wave
-//                 per 64-pixel row segment packs the mask with __ballot
+//   k_ccl_strong  per tile: bit per local root whose global root is strong
+//   k_ccl_edge    edge = strong || (maybe && root strong), packed per 64-pixel row
+//                 segment with __ballot (no halo)
+//   k_bits_dilate 3x3 dilate on the packed words (shifts and ORs)
+#include <algorithm>
+
 #include "llfe_internal.h"
 
 namespace llfe {
@@ -182,112 +186,81 @@ __global__ __launch_bounds__(NT) void k_ccl_flatten(int ntiles, const uint16_t *
     }
 }
 
-constexpr int EH = TH + 2, EW = TW + 2, EWP = TW + 8;
-__device__ __forceinline__ uint8_t edge_global(const uint8_t *c, const uint16_t *lab, int img, int H, int W, int ntx,
-                                               int ntiles, int y, int x, const int *parent, const uint8_t *sroot) {
-    if ((unsigned)y >= (unsigned)H || (unsigned)x >= (unsigned)W) return 0;
-    const uint8_t v = c[(size_t)y * W + x];
-    if (v == 2) return 1;
-    if (v != 0) return 0;
-    return sroot[parent[gid_of(lab, img, H, W, ntx, ntiles, y, x)]];
-}
-
-// The tile's own pixels resolve "maybe" through an LDS bit per local root (one global
-// parent/sroot lookup per root instead of per pixel); only the 1-pixel ring of
-// neighbouring tiles' pixels goes through the global tables.
-__global__ __launch_bounds__(NT) void k_ccl_dilate(const uint8_t *__restrict__ cls, const uint16_t *__restrict__ lab,
-                                                    int H, int W, int ntx, int nty, const uint16_t *__restrict__ roots,
+// per tile: one bit per local root, set when its global root is strong
+__global__ __launch_bounds__(NT) void k_ccl_strong(int ntiles, const uint16_t *__restrict__ roots,
                                                     const int *__restrict__ nroots, const int *__restrict__ parent,
-                                                    const uint8_t *__restrict__ sroot, uint64_t *__restrict__ bits,
-                                                    uint8_t *__restrict__ mask_u8) {
-    __shared__ __attribute__((aligned(16))) uint8_t e[EH][EWP];  // local column lx at lx + 3
+                                                    const uint8_t *__restrict__ sroot, uint32_t *__restrict__ tstrong) {
     __shared__ uint32_t rs[TP / 32];
-    const int tid = threadIdx.x, img = blockIdx.y, t = blockIdx.x;
-    const int ntiles = ntx * nty;
-    const int tx0 = (t % ntx) * TW, ty0 = (t / ntx) * TH;
-    const uint8_t *c = cls + (size_t)img * H * W;
-    const size_t tile = (size_t)img * ntiles + t, gbase = tile * TP;
+    const size_t tile = (size_t)blockIdx.y * ntiles + blockIdx.x, gbase = tile * TP;
+    const int tid = threadIdx.x, n = nroots[tile];
     if (tid < TP / 32) rs[tid] = 0;
-    // the tile's classes and local labels first (independent of the root lookups below)
-    constexpr int NQ = TH * (TW / 4) / NT;
-    const bool full = tx0 + TW <= W && (W & 3) == 0;
-    uint32_t v4[NQ];
-    uint2 l4[NQ];
-#pragma unroll
-    for (int k = 0; k < NQ; k++) {
-        const int u = tid + k * NT, ly = u / (TW / 4), q = u - ly * (TW / 4), y = ty0 + ly, x = tx0 + 4 * q;
-        v4[k] = 0x01010101u;
-        l4[k] = make_uint2(0u, 0u);
-        if (y < H) {
-            if (full) {
-                v4[k] = *(const uint32_t *)(c + (size_t)y * W + x);
-                l4[k] = *(const uint2 *)(lab + ((size_t)img * H + y) * W + x);
-            } else {
-                uint32_t v = 0, l0 = 0, l1 = 0;
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const uint32_t cv = x + j < W ? c[(size_t)y * W + x + j] : 1u;
-                    const uint32_t lv = (x + j < W && cv == 0) ? lab[((size_t)img * H + y) * W + x + j] : 0u;
-                    v |= cv << (8 * j);
-                    if (j < 2) l0 |= lv << (16 * j);
-                    else l1 |= lv << (16 * (j - 2));
-                }
-                v4[k] = v;
-                l4[k] = make_uint2(l0, l1);
-            }
-        }
-    }
     __syncthreads();
-    const int nr = nroots[tile];
-    for (int k = tid; k < nr; k += NT) {
+    for (int k = tid; k < n; k += NT) {
         const int i = roots[gbase + k];
         if (sroot[parent[gbase + i]]) atomicOr(&rs[i >> 5], 1u << (i & 31));
     }
-    // ring: top / bottom rows (EW each), left / right columns (TH each)
-    if (tid < 2 * EW + 2 * TH) {
-        int ly, lx;
-        if (tid < EW) {
-            ly = 0;
-            lx = tid;
-        } else if (tid < 2 * EW) {
-            ly = EH - 1;
-            lx = tid - EW;
-        } else if (tid < 2 * EW + TH) {
-            ly = 1 + tid - 2 * EW;
-            lx = 0;
-        } else {
-            ly = 1 + tid - 2 * EW - TH;
-            lx = EW - 1;
-        }
-        e[ly][lx + 3] = edge_global(c, lab, img, H, W, ntx, ntiles, ty0 - 1 + ly, tx0 - 1 + lx, parent, sroot);
-    }
     __syncthreads();
+    if (tid < TP / 32) tstrong[tile * (TP / 32) + tid] = rs[tid];
+}
+
+// per tile, no halo: edge = strong || (maybe && strong local root); one wave per
+// 64-pixel row segment packs the row's edge word with __ballot
+__global__ __launch_bounds__(NT) void k_ccl_edge(const uint8_t *__restrict__ cls, const uint16_t *__restrict__ lab,
+                                                  int H, int W, int ntx, int nty, const uint32_t *__restrict__ tstrong,
+                                                  uint64_t *__restrict__ ebits) {
+    __shared__ uint32_t rs[TP / 32];
+    constexpr int RPW = TH / (NT / 64);  // rows per wave
+    const int tid = threadIdx.x, img = blockIdx.y, t = blockIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int ntiles = ntx * nty;
+    const int tx0 = (t % ntx) * TW, ty0 = (t / ntx) * TH, x = tx0 + lane;
+    const size_t tile = (size_t)img * ntiles + t;
+    const uint8_t *c = cls + (size_t)img * H * W;
+    const uint16_t *lb = lab + (size_t)img * H * W;
+    uint32_t v[RPW], l[RPW];
 #pragma unroll
-    for (int k = 0; k < NQ; k++) {
-        const int u = tid + k * NT, ly = u / (TW / 4), q = u - ly * (TW / 4);
-        const uint32_t lv[4] = {l4[k].x & 0xFFFFu, l4[k].x >> 16, l4[k].y & 0xFFFFu, l4[k].y >> 16};
-        uint32_t o = 0;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t v = (v4[k] >> (8 * j)) & 255u;
-            const uint32_t on = v == 2u ? 1u : (v == 0u ? (rs[(lv[j] >> 5) & (TP / 32 - 1)] >> (lv[j] & 31)) & 1u : 0u);
-            o |= on << (8 * j);
-        }
-        *(uint32_t *)&e[ly + 1][4 * q + 4] = o;
+    for (int r = 0; r < RPW; r++) {
+        const int y = ty0 + wid + r * (NT / 64);
+        const bool in = y < H && x < W;
+        v[r] = in ? c[(size_t)y * W + x] : 1u;
+        l[r] = in ? lb[(size_t)y * W + x] : 0u;  // meaningful only where v == 0
     }
+    if (tid < TP / 32) rs[tid] = tstrong[tile * (TP / 32) + tid];
     __syncthreads();
-    const int lane = tid & 63, wid = tid >> 6;
     const int wpr = (W + 63) / 64;
-    for (int ly = wid; ly < TH; ly += NT / 64) {
-        const int y = ty0 + ly, x = tx0 + lane;
-        if (y >= H) break;
-        bool on = false;
-        if (x < W)
-            on = e[ly][lane + 3] | e[ly][lane + 4] | e[ly][lane + 5] | e[ly + 1][lane + 3] | e[ly + 1][lane + 4] |
-                 e[ly + 1][lane + 5] | e[ly + 2][lane + 3] | e[ly + 2][lane + 4] | e[ly + 2][lane + 5];
+#pragma unroll
+    for (int r = 0; r < RPW; r++) {
+        const int y = ty0 + wid + r * (NT / 64);
+        const uint32_t li = l[r] & (TP - 1);
+        const bool on = v[r] == 2u || (v[r] == 0u && ((rs[li >> 5] >> (li & 31)) & 1u));
         const unsigned long long b = __ballot(on);
-        if (bits && lane == 0) bits[((size_t)img * H + y) * wpr + (tx0 >> 6)] = b;
-        if (mask_u8 && x < W) mask_u8[((size_t)img * H + y) * W + x] = on ? 255 : 0;
+        if (lane == 0 && y < H) ebits[((size_t)img * H + y) * wpr + (tx0 >> 6)] = b;
+    }
+}
+
+// 3x3 dilate on the packed edge words: one thread per 64-pixel word
+__global__ __launch_bounds__(NT) void k_bits_dilate(const uint64_t *__restrict__ eb, int n, int H, int W,
+                                                     uint64_t *__restrict__ bits, uint8_t *__restrict__ mask_u8) {
+    const int wpr = (W + 63) / 64;
+    const size_t total = (size_t)n * H * wpr;
+    for (size_t i = (size_t)blockIdx.x * NT + threadIdx.x; i < total; i += (size_t)gridDim.x * NT) {
+        const int k = (int)(i % wpr);
+        const size_t row = i / wpr;  // img * H + y
+        const int y = (int)(row % H);
+        uint64_t d = 0;
+#pragma unroll
+        for (int dy = -1; dy <= 1; dy++) {
+            if ((unsigned)(y + dy) >= (unsigned)H) continue;
+            const uint64_t *r = eb + (row + dy) * wpr;
+            const uint64_t w = r[k], wl = k > 0 ? r[k - 1] : 0ull, wr = k + 1 < wpr ? r[k + 1] : 0ull;
+            d |= w | (w << 1) | (w >> 1) | (wl >> 63) | (wr << 63);
+        }
+        if (k == wpr - 1 && (W & 63)) d &= (1ull << (W & 63)) - 1ull;
+        if (bits) bits[i] = d;
+        if (mask_u8) {
+            uint8_t *m = mask_u8 + row * W + (size_t)k * 64;
+            const int nx = min(64, W - k * 64);
+            for (int b = 0; b < nx; b++) m[b] = ((d >> b) & 1ull) ? 255 : 0;
+        }
     }
 }
 
@@ -303,8 +276,12 @@ hipError_t launch_hysteresis_dilate(const uint8_t *cls, int n, int h, int w, con
                        wk.nroots);
     hipLaunchKernelGGL(k_ccl_border, grid, dim3(128), 0, s, cls, wk.lab, h, w, ntx, nty, wk.parent);
     hipLaunchKernelGGL(k_ccl_flatten, grid, dim3(NT), 0, s, ntiles, wk.roots, wk.nroots, wk.parent, wk.sroot);
-    hipLaunchKernelGGL(k_ccl_dilate, grid, dim3(NT), 0, s, cls, wk.lab, h, w, ntx, nty, wk.roots, wk.nroots,
-                       wk.parent, wk.sroot, bits, mask_u8);
+    hipLaunchKernelGGL(k_ccl_strong, grid, dim3(NT), 0, s, ntiles, wk.roots, wk.nroots, wk.parent, wk.sroot,
+                       wk.tstrong);
+    hipLaunchKernelGGL(k_ccl_edge, grid, dim3(NT), 0, s, cls, wk.lab, h, w, ntx, nty, wk.tstrong, wk.ebits);
+    const size_t words = (size_t)n * h * words_per_row(w);
+    const int blocks = (int)std::min<size_t>((words + NT - 1) / NT, 65536);
+    hipLaunchKernelGGL(k_bits_dilate, dim3(blocks), dim3(NT), 0, s, wk.ebits, n, h, w, bits, mask_u8);
     return hipGetLastError();
 }
 

@@ -202,11 +202,11 @@ int pil_coeffs(int in_size, double in0, double in1, int out_size, std::vector<in
 struct Work {
     DevBuf<uint8_t> d_in, d_cls, d_sroot;
     DevBuf<int8_t> d_noise;
-    DevBuf<uint64_t> d_bits;
+    DevBuf<uint64_t> d_bits, d_ebits;
     DevBuf<unsigned long long> d_shadow;
     DevBuf<int> d_order, d_parent, d_nroots;
     DevBuf<uint16_t> d_lab, d_roots;
-    DevBuf<uint32_t> d_raw, d_keys, d_kscratch, d_pmeta;
+    DevBuf<uint32_t> d_raw, d_keys, d_kscratch, d_pmeta, d_tstrong;
     DevBuf<CubeEnt> d_segcubes, d_cubes;
     DevBuf<int32_t> d_ncubes;
     DevBuf<int64_t> d_nuniq;
@@ -395,8 +395,10 @@ int run_hysteresis_dilate(llfe_ctx *ctx, Work &W, int n, int h, int w, uint64_t 
     HIPCHK(ctx, W.d_sroot.ensure(ids));
     HIPCHK(ctx, W.d_roots.ensure(ids));
     HIPCHK(ctx, W.d_nroots.ensure(tiles));
-    HystWork wk{W.d_lab.p, W.d_parent.p, W.d_sroot.p, W.d_roots.p, W.d_nroots.p};
-    TIMED(ctx, s, "k_hysteresis_dilate", (double)n * h * w * (1 + 2 + 2 + 1 + 0.125),
+    HIPCHK(ctx, W.d_tstrong.ensure(tiles * (kTileW * kTileH / 32)));
+    HIPCHK(ctx, W.d_ebits.ensure((size_t)n * h * words_per_row(w)));
+    HystWork wk{W.d_lab.p, W.d_parent.p, W.d_sroot.p, W.d_roots.p, W.d_nroots.p, W.d_tstrong.p, W.d_ebits.p};
+    TIMED(ctx, s, "k_hysteresis_dilate", (double)n * h * w * (1 + 2 + 1 + 2 + 3 * 0.125),
           launch_hysteresis_dilate(W.d_cls.p, n, h, w, wk, bits, mask_u8, s));
     return LLFE_OK;
 }

@@ -35,6 +35,8 @@ struct HystWork {
     uint8_t *sroot;
     uint16_t *roots;
     int *nroots;
+    uint32_t *tstrong;  // per tile TP / 32 words
+    uint64_t *ebits;    // n x h x words_per_row, edges before the dilate
 };
 size_t hysteresis_ids(int n, int h, int w);
 hipError_t launch_hysteresis_dilate(const uint8_t *cls, int n, int h, int w, const HystWork &wk, uint64_t *bits,
