@@ -12,6 +12,8 @@ import threading
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_PKG, "libllfe.so")
+# experiments only: load a variant build (e.g. libllfe_<tag>.so built with LLFE_EXTRA_FLAGS)
+_VARIANT = os.environ.get("LLFE_LIB_VARIANT")
 
 LLFE_OK = 0
 LLFE_ERR_INVALID = -1
@@ -126,13 +128,16 @@ def lib():
         if _lib is None:
             from . import _build
 
-            if _build._stale():
+            if _VARIANT:
+                L = C.CDLL(os.path.join(_PKG, f"libllfe_{_VARIANT}.so"))
+            elif _build._stale():
                 try:
                     _build.build()
                 except Exception as e:  # pragma: no cover - surfaced to caller
                     if not os.path.exists(LIB_PATH):
                         raise RuntimeError(f"libllfe.so is missing and could not be built: {e}") from e
-            L = C.CDLL(LIB_PATH)
+            if not _VARIANT:
+                L = C.CDLL(LIB_PATH)
             for name, (res, args) in SIGNATURES.items():
                 f = getattr(L, name)
                 f.restype = res

@@ -2,7 +2,7 @@
 // KMEANS_PP_CENTERS) for a batch of images on gfx950
 // (app/services/analyze/color_extractor.py:189-197).
 //
-// One 1024-thread workgroup per (image, attempt); workgroups are issued largest-U
+// One 512-thread workgroup per (image, attempt), two per CU; workgroups are issued largest-U
 // first (LPT) so the many short "ui" attempts back-fill behind the long "photo" ones.
 // The point set is the compacted unique-colour key list (4 B / point, ascending =
 // np.unique row order); wave w owns a contiguous range of 256-point steps and reads
@@ -25,7 +25,10 @@
 namespace llfe {
 namespace {
 
-constexpr int KT = 1024;          // threads per (image, attempt)
+#ifndef LLFE_KM_THREADS
+#define LLFE_KM_THREADS 512
+#endif
+constexpr int KT = LLFE_KM_THREADS;  // threads per (image, attempt)
 constexpr int KW = KT / 64;       // waves
 constexpr int STEP = 256;         // points per wave step (64 lanes x 4)
 constexpr float kFar = 1e30f;     // coordinate of an unused centre: its distance is +inf
@@ -670,7 +673,10 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
     __syncthreads();
 }
 
-__global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys, long long key_stride,
+#ifndef LLFE_KM_MINW
+#define LLFE_KM_MINW 1
+#endif
+__global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__restrict__ keys, long long key_stride,
                                                const long long *__restrict__ n_unique, int n_colors,
                                                unsigned long long seed, long long index_base,
                                                const int *__restrict__ order,
@@ -1132,14 +1138,15 @@ __global__ __launch_bounds__(KT) void k_kmeans(const uint32_t *__restrict__ keys
                 bytes += 4ull * (unsigned long long)N;
             }
         }
-        // reduce 20 values (5 clusters x {x, y, z, count}) over 1024 lanes
-        if (tid < 640) {
-            const int v = tid >> 5, part = tid & 31;
+        // reduce 20 values (5 clusters x {x, y, z, count}) over the KT lanes
+        for (int q = tid; q < 640; q += KT) {
+            constexpr int LPP = KT / 32;  // lanes per part
+            const int v = q >> 5, part = q & 31;
             const int k = v >> 2, comp = v & 3;
             unsigned long long acc = 0;
             const unsigned long long *src = comp < 2 ? sm.accA[k] : sm.accB[k];
 #pragma unroll 4
-            for (int l = part * 32; l < part * 32 + 32; l++) {
+            for (int l = part * LPP; l < part * LPP + LPP; l++) {
                 unsigned long long wv = src[l];
                 acc += (comp & 1) ? (wv >> 32) : (wv & 0xFFFFFFFFull);
             }
