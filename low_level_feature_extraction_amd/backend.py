@@ -175,27 +175,26 @@ class Backend:
                     continue
                 self._chk(rc)
                 break
-        out = []
-        for i in range(n):
-            r = results[i]
-            k = r.n_colors
-            centers = np.array([[r.centers_rgb[j][c] for c in range(3)] for j in range(k)], np.uint8).reshape(-1, 3)
-            counts = np.array([r.counts[j] for j in range(k)], np.int64)
-            shp = []
-            if mask & L.FEATURE_SHAPES:
-                for j in range(r.shape_offset, r.shape_offset + r.n_shapes):
-                    s = shapes[j]
-                    shp.append({
-                        "type": L.SHAPE_TYPES[s.type],
-                        "x": int(s.x),
-                        "y": int(s.y),
-                        "width": int(s.width),
-                        "height": int(s.height),
-                        "border_radius": float(s.border_radius),
-                        "area": float(s.area),
-                    })
-            out.append(ImageFeatures(centers, counts, int(r.n_unique), float(r.compactness), int(r.shadow_sum),
-                                     int(r.shadow_count), shp, int(r.n_contours), w, h))
+        # bulk conversion through numpy views of the ctypes arrays (per-field ctypes
+        # access would cost ~20 us per image while the GPU waits for the next batch)
+        R = np.ctypeslib.as_array(results)[:n]
+        ncol = R["n_colors"].tolist()
+        cen = R["centers_rgb"].copy()
+        cnt = R["counts"].astype(np.int64)
+        nu, comp = R["n_unique"].tolist(), R["compactness"].tolist()
+        ssum, scnt = R["shadow_sum"].tolist(), R["shadow_count"].tolist()
+        off, nsh, ncont = R["shape_offset"].tolist(), R["n_shapes"].tolist(), R["n_contours"].tolist()
+        recs = []
+        if mask & L.FEATURE_SHAPES and n:
+            tot = max(o + c for o, c in zip(off, nsh))
+            S = np.ctypeslib.as_array(shapes)[:tot]
+            names = L.SHAPE_TYPES
+            recs = [{"type": names[t], "x": x, "y": y, "width": ww, "height": hh, "border_radius": br, "area": ar}
+                    for t, x, y, ww, hh, br, ar in zip(S["type"].tolist(), S["x"].tolist(), S["y"].tolist(),
+                                                       S["width"].tolist(), S["height"].tolist(),
+                                                       S["border_radius"].tolist(), S["area"].tolist())]
+        out = [ImageFeatures(cen[i, :ncol[i]], cnt[i, :ncol[i]], nu[i], comp[i], ssum[i], scnt[i],
+                             recs[off[i]:off[i] + nsh[i]] if recs else [], ncont[i], w, h) for i in range(n)]
         del keep, nkeep
         return out
 
