@@ -1,0 +1,119 @@
+"""Request micro-batching (batcher.py) and the host decode pool (decode.py): CPU tests
+with a stand-in batch runner; one GPU test through the real backend."""
+import asyncio
+import io
+import threading
+
+import numpy as np
+import pytest
+from PIL import Image
+
+from low_level_feature_extraction_amd import decode
+from low_level_feature_extraction_amd.batcher import MicroBatcher
+
+
+def _fake_run(calls):
+    def run(images, features):
+        calls.append(len(images))
+        return [{"sum": int(im.sum()), "shape": im.shape, "features": features} for im in images]
+
+    return run
+
+
+def test_batcher_groups_concurrent_requests_and_keeps_order():
+    calls = []
+    imgs = [np.full((4 + i % 3, 5, 3), i, np.uint8) for i in range(40)]
+    with MicroBatcher(features=("colors",), max_batch=16, max_wait_ms=50, run=_fake_run(calls)) as b:
+        futs = [b.submit(im) for im in imgs]
+        res = [f.result(timeout=10) for f in futs]
+    assert [r["sum"] for r in res] == [int(im.sum()) for im in imgs]
+    assert [r["shape"] for r in res] == [im.shape for im in imgs]
+    assert sum(calls) == 40 and max(calls) <= 16 and len(calls) < 40
+
+
+def test_batcher_from_threads_and_asyncio():
+    calls = []
+    b = MicroBatcher(max_batch=8, max_wait_ms=20, run=_fake_run(calls))
+    out = {}
+
+    def worker(i):
+        out[i] = b.submit(np.full((3, 3, 3), i, np.uint8)).result(timeout=10)["sum"]
+
+    th = [threading.Thread(target=worker, args=(i,)) for i in range(12)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    assert out == {i: 27 * i for i in range(12)}
+
+    async def main():
+        rs = await asyncio.gather(*[b.analyze(np.full((2, 2, 3), i, np.uint8)) for i in range(5)])
+        return [r["sum"] for r in rs]
+
+    assert asyncio.run(main()) == [12 * i for i in range(5)]
+    b.close()
+    with pytest.raises(RuntimeError):
+        b.submit(np.zeros((2, 2, 3), np.uint8))
+
+
+def test_batcher_propagates_errors_to_every_request():
+    def boom(images, features):
+        raise ValueError("backend failed")
+
+    with MicroBatcher(max_batch=4, max_wait_ms=20, run=boom) as b:
+        futs = [b.submit(np.zeros((2, 2, 3), np.uint8)) for _ in range(3)]
+        for f in futs:
+            with pytest.raises(ValueError, match="backend failed"):
+                f.result(timeout=10)
+
+
+def test_batcher_rejects_bad_inputs():
+    with MicroBatcher(run=_fake_run([])) as b:
+        with pytest.raises(ValueError):
+            b.submit(np.zeros((4, 4), np.uint8))
+    with pytest.raises(ValueError):
+        MicroBatcher(max_batch=0, run=_fake_run([]))
+
+
+def _png(a):
+    b = io.BytesIO()
+    Image.fromarray(a).save(b, "PNG")
+    return b.getvalue()
+
+
+def test_decode_batch_and_many():
+    rng = np.random.default_rng(3)
+    rgb = [rng.integers(0, 256, (17, 23, 3), dtype=np.uint8) for _ in range(6)]
+    blobs = [_png(a) for a in rgb]
+    out = decode.decode_batch(blobs, workers=3)
+    assert out.shape == (6, 17, 23, 3)
+    for i in range(6):
+        np.testing.assert_array_equal(out[i], rgb[i][:, :, ::-1])
+    buf = np.zeros((6, 17, 23, 3), np.uint8)
+    assert decode.decode_batch(blobs, out=buf, workers=2) is buf
+    many = decode.decode_many(blobs + [b"junk"], workers=4)
+    assert isinstance(many[-1], decode.DecodeError)
+    np.testing.assert_array_equal(many[2], rgb[2][:, :, ::-1])
+
+
+def test_decode_batch_errors():
+    a = np.zeros((8, 8, 3), np.uint8)
+    with pytest.raises(decode.DecodeError, match="image 1"):
+        decode.decode_batch([_png(a), b"not an image"], workers=2)
+    with pytest.raises(decode.DecodeError, match="differs"):
+        decode.decode_batch([_png(a), _png(np.zeros((9, 8, 3), np.uint8))], workers=2)
+    with pytest.raises(decode.DecodeError):
+        decode.decode_batch([])
+
+
+@pytest.mark.gpu
+def test_batcher_on_gpu_matches_run_batch():
+    from low_level_feature_extraction_amd import synth
+    from low_level_feature_extraction_amd.pipeline import run_batch
+
+    imgs = [synth.synth_numpy(i, 120 + 8 * (i % 2), 200, seed=5) for i in range(10)]
+    ref = run_batch(imgs, ("shapes", "shadows"))
+    with MicroBatcher(features=("colors", "shapes", "shadows"), max_batch=8, max_wait_ms=20) as b:
+        got = [f.result(timeout=60) for f in [b.submit(im) for im in imgs]]
+    for r, g in zip(ref, got):
+        assert g["shapes"] == r["shapes"] and g["shadows"] == r["shadows"]
+        assert g["colors"].primary is not None and g["colors"].metadata.get("success", True)
+    assert max(b.batch_sizes) > 1
