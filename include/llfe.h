@@ -199,6 +199,19 @@ int llfe_classify_contour(const int32_t *points, int32_t n, llfe_shape *out);
 int llfe_shapes_from_mask(const uint8_t *mask, int32_t h, int32_t w, llfe_shape *shapes, int32_t capacity,
                           int32_t *n_contours);
 
+/* ---- host PNG decode (cv2.imdecode(buf, IMREAD_COLOR), utils.py:108-109 and
+ * image_processor.py:208-211).  Host only, no ctx.  IMREAD_COLOR semantics: BGR u8,
+ * alpha dropped, grey expanded, palette looked up, 16-bit -> high byte; critical-chunk
+ * CRCs checked.  Interlaced and sub-byte-depth images return LLFE_ERR_UNSUPPORTED
+ * (the caller decodes those another way); corrupt data LLFE_ERR_INVALID. */
+/* size of a PNG from its IHDR */
+int llfe_png_info(const uint8_t *data, uint64_t size, int32_t *width, int32_t *height);
+/* n PNGs of one size into out_bgr (n x height x width x 3, host), `threads` host
+ * threads.  status[i] per image (LLFE_OK, LLFE_ERR_UNSUPPORTED, LLFE_ERR_INVALID, or
+ * LLFE_ERR_CAPACITY when its size differs); returns the first non-OK status. */
+int llfe_decode_png_batch(const uint8_t *const *data, const uint64_t *sizes, int32_t n, int32_t height,
+                          int32_t width, uint8_t *out_bgr, int32_t *status, int32_t threads);
+
 #ifdef __cplusplus
 }
 #endif

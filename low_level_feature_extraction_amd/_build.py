@@ -14,7 +14,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libllfe.so")
-SOURCES = ["llfe_api.cpp", "contours.cpp", "stencil.hip", "hysteresis.hip", "unique.hip", "kmeans.hip", "resize.hip",
+SOURCES = ["llfe_api.cpp", "contours.cpp", "png_decode.cpp", "stencil.hip", "hysteresis.hip", "unique.hip", "kmeans.hip", "resize.hip",
            "cvresize.hip"]
 HEADERS = ["llfe_internal.h", "contours.h"]
 ARCH = os.environ.get("LLFE_OFFLOAD_ARCH", "gfx950")
@@ -49,7 +49,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     for src in SOURCES:
         obj = os.path.join(tmpdir, src + ".o")
         objs.append(obj)
-        if src == "contours.cpp":  # pure host code
+        if src in ("contours.cpp", "png_decode.cpp"):  # pure host code
             lang = ["-x", "c++"]
         else:
             lang = ["-x", "hip", f"--offload-arch={ARCH}"]
@@ -68,7 +68,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         msg = "\n\n".join(" ".join(c) + "\n" + o for c, o in failed)
         raise RuntimeError("libllfe build failed:\n" + msg)
     tmp = LIB + ".tmp"
-    cmd = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp, "-lpthread"]
+    cmd = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp, "-lpthread", "-lz", "-ldl"]
     subprocess.run(cmd, check=True)
     os.replace(tmp, LIB)
     return LIB

@@ -1,0 +1,366 @@
+// Host PNG decoding for the decode step in front of the hot path: cv2.imdecode(buf,
+// IMREAD_COLOR) at app/services/analyze/utils.py:108-109 and
+// app/services/analyze/image_processor.py:208-211 (at ~10k 1080p
+// images/s per GPU the host decode, not the GPU, bounds the end-to-end rate).
+//
+// IMREAD_COLOR semantics (as decode.py's Pillow path): 8-bit BGR out, alpha dropped (not
+// composited), grey expanded, palette looked up, 16-bit samples reduced to their high
+// byte.  Critical-chunk CRCs are checked (corrupt input is an error, as in libpng).
+// Interlaced images and sub-byte depths return LLFE_ERR_UNSUPPORTED and are decoded by
+// the caller's fallback (Pillow).
+//
+// Inflate uses libdeflate when the image provides libdeflate.so.0 (whole-stream, ~2x
+// zlib's speed) and zlib otherwise; the filters are undone in place (SSE2 for the 3-
+// and 4-byte pixel cases), then each row is converted straight into the NHWC batch.
+// A batch fans out over std::threads, one image per task.
+#include <dlfcn.h>
+#include <emmintrin.h>
+#include <zlib.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdint>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "llfe.h"
+
+namespace {
+
+// ---------------------------------------------------------------- libdeflate (optional)
+struct Deflate {
+    void *(*alloc)() = nullptr;
+    void (*free_)(void *) = nullptr;
+    int (*zlib_dec)(void *, const void *, size_t, void *, size_t, size_t *) = nullptr;
+    uint32_t (*crc32)(uint32_t, const void *, size_t) = nullptr;
+    bool ok = false;
+    Deflate() {
+        if (const char *off = getenv("LLFE_NO_LIBDEFLATE"); off && *off == '1') return;
+        void *h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return;
+        alloc = (void *(*)())dlsym(h, "libdeflate_alloc_decompressor");
+        free_ = (void (*)(void *))dlsym(h, "libdeflate_free_decompressor");
+        zlib_dec = (int (*)(void *, const void *, size_t, void *, size_t, size_t *))dlsym(h, "libdeflate_zlib_decompress");
+        crc32 = (uint32_t(*)(uint32_t, const void *, size_t))dlsym(h, "libdeflate_crc32");
+        ok = alloc && free_ && zlib_dec && crc32;
+    }
+};
+const Deflate &deflate() {
+    static Deflate d;
+    return d;
+}
+
+uint32_t crc(const uint8_t *p, size_t n) {
+    const Deflate &d = deflate();
+    if (d.ok) return d.crc32(0, p, n);
+    uLong c = crc32(0L, Z_NULL, 0);
+    while (n) {  // zlib's length is a uInt
+        const uInt k = (uInt)std::min<size_t>(n, 1u << 30);
+        c = crc32(c, p, k);
+        p += k;
+        n -= k;
+    }
+    return (uint32_t)c;
+}
+
+inline uint32_t be32(const uint8_t *p) { return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3]; }
+
+struct Png {
+    uint32_t w = 0, h = 0;
+    int depth = 0, ctype = 0, interlace = 0;
+    const uint8_t *plte = nullptr;
+    uint32_t plte_n = 0;
+    std::vector<std::pair<const uint8_t *, size_t>> idat;
+    int channels() const { return ctype == 0 ? 1 : ctype == 2 ? 3 : ctype == 3 ? 1 : ctype == 4 ? 2 : 4; }
+};
+
+// chunk walk; info_only stops after IHDR
+int parse(const uint8_t *d, size_t n, Png &png, bool info_only) {
+    static const uint8_t sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
+    if (n < 8 || memcmp(d, sig, 8) != 0) return LLFE_ERR_INVALID;
+    size_t p = 8;
+    bool ihdr = false, iend = false;
+    while (p + 12 <= n) {
+        const uint32_t len = be32(d + p);
+        const uint8_t *type = d + p + 4, *body = d + p + 8;
+        if (len > n - p - 12) return LLFE_ERR_INVALID;
+        const bool critical = !(type[0] & 32);
+        if (critical && crc(type, (size_t)len + 4) != be32(body + len)) return LLFE_ERR_INVALID;
+        if (!memcmp(type, "IHDR", 4)) {
+            if (len != 13 || ihdr) return LLFE_ERR_INVALID;
+            png.w = be32(body);
+            png.h = be32(body + 4);
+            png.depth = body[8];
+            png.ctype = body[9];
+            png.interlace = body[12];
+            if (!png.w || !png.h || body[10] || body[11] || png.interlace > 1) return LLFE_ERR_INVALID;
+            const int c = png.ctype, b = png.depth;
+            const bool valid = (c == 0 && (b == 1 || b == 2 || b == 4 || b == 8 || b == 16)) ||
+                               (c == 3 && (b == 1 || b == 2 || b == 4 || b == 8)) ||
+                               ((c == 2 || c == 4 || c == 6) && (b == 8 || b == 16));
+            if (!valid) return LLFE_ERR_INVALID;
+            ihdr = true;
+            if (info_only) return LLFE_OK;
+        } else if (!ihdr) {
+            return LLFE_ERR_INVALID;
+        } else if (!memcmp(type, "PLTE", 4)) {
+            if (len % 3 || len > 768) return LLFE_ERR_INVALID;
+            png.plte = body;
+            png.plte_n = len / 3;
+        } else if (!memcmp(type, "IDAT", 4)) {
+            png.idat.emplace_back(body, (size_t)len);
+        } else if (!memcmp(type, "IEND", 4)) {
+            iend = true;
+            break;
+        } else if (critical) {
+            return LLFE_ERR_UNSUPPORTED;  // unknown critical chunk
+        }
+        p += (size_t)len + 12;
+    }
+    if (!ihdr || png.idat.empty()) return LLFE_ERR_INVALID;
+    (void)iend;  // a missing IEND after complete image data is tolerated (as libpng does)
+    if (png.ctype == 3 && !png.plte) return LLFE_ERR_INVALID;
+    if (png.interlace || png.depth < 8) return LLFE_ERR_UNSUPPORTED;
+    return LLFE_OK;
+}
+
+// zlib stream of the concatenated IDAT payloads -> exactly `out_n` bytes
+bool inflate_idat(const Png &png, uint8_t *out, size_t out_n, std::vector<uint8_t> &cat) {
+    const Deflate &d = deflate();
+    if (d.ok) {
+        const uint8_t *src = png.idat[0].first;
+        size_t src_n = png.idat[0].second;
+        if (png.idat.size() > 1) {
+            size_t tot = 0;
+            for (auto &c : png.idat) tot += c.second;
+            cat.resize(tot);
+            size_t o = 0;
+            for (auto &c : png.idat) {
+                memcpy(cat.data() + o, c.first, c.second);
+                o += c.second;
+            }
+            src = cat.data();
+            src_n = tot;
+        }
+        thread_local struct Dec {
+            void *p = nullptr;
+            ~Dec() {
+                if (p) deflate().free_(p);
+            }
+        } dec;
+        if (!dec.p) dec.p = d.alloc();
+        size_t got = 0;
+        if (dec.p) {
+            const int rc = d.zlib_dec(dec.p, src, src_n, out, out_n, &got);
+            if (rc == 0 && got == out_n) return true;
+            if (rc == 1) return false;  // LIBDEFLATE_BAD_DATA
+        }
+        // short / over-long streams: zlib below decides exactly as a streaming reader would
+    }
+    z_stream z{};
+    if (inflateInit(&z) != Z_OK) return false;
+    z.next_out = out;
+    z.avail_out = (uInt)out_n;
+    int rc = Z_OK;
+    for (size_t i = 0; i < png.idat.size() && z.avail_out; i++) {
+        z.next_in = const_cast<Bytef *>(png.idat[i].first);
+        z.avail_in = (uInt)png.idat[i].second;
+        while (z.avail_in && z.avail_out) {
+            rc = inflate(&z, Z_NO_FLUSH);
+            if (rc == Z_STREAM_END) break;
+            if (rc != Z_OK) {
+                inflateEnd(&z);
+                return false;
+            }
+        }
+        if (rc == Z_STREAM_END) break;
+    }
+    const bool full = z.avail_out == 0;
+    inflateEnd(&z);
+    return full;  // trailing data after a complete image is ignored (libpng warns only)
+}
+
+inline uint8_t paeth(int a, int b, int c) {
+    const int p = a + b - c, pa = abs(p - a), pb = abs(p - b), pc = abs(p - c);
+    return (uint8_t)((pa <= pb && pa <= pc) ? a : (pb <= pc ? b : c));
+}
+
+// undo one row's filter in place; prior = previous unfiltered row (nullptr for row 0)
+template <int BPP>
+void unfilter_simd(int f, uint8_t *cur, const uint8_t *prior, size_t n) {
+    // BPP 3 or 4: one pixel per step in 16-bit lanes (the left neighbour is a dependency)
+    const __m128i z = _mm_setzero_si128();
+    auto ld = [](const uint8_t *p) -> __m128i {
+        uint32_t v = 0;
+        memcpy(&v, p, BPP);
+        return _mm_cvtsi32_si128((int)v);
+    };
+    auto st = [](uint8_t *p, __m128i v) {
+        const uint32_t x = (uint32_t)_mm_cvtsi128_si32(v);
+        memcpy(p, &x, BPP);
+    };
+    __m128i a = z, c = z;
+    if (f == 1) {
+        for (size_t i = 0; i < n; i += BPP) {
+            a = _mm_add_epi8(ld(cur + i), a);
+            st(cur + i, a);
+        }
+    } else if (f == 3) {
+        for (size_t i = 0; i < n; i += BPP) {
+            const __m128i b = prior ? _mm_unpacklo_epi8(ld(prior + i), z) : z;
+            const __m128i avg = _mm_srli_epi16(_mm_add_epi16(_mm_unpacklo_epi8(a, z), b), 1);
+            a = _mm_add_epi8(ld(cur + i), _mm_packus_epi16(avg, avg));
+            st(cur + i, a);
+        }
+    } else {  // f == 4, Paeth
+        for (size_t i = 0; i < n; i += BPP) {
+            const __m128i b = prior ? _mm_unpacklo_epi8(ld(prior + i), z) : z;
+            const __m128i a16 = _mm_unpacklo_epi8(a, z);
+            // pa = |b - c|, pb = |a - c|, pc = |a + b - 2c|
+            const __m128i bc = _mm_sub_epi16(b, c), ac = _mm_sub_epi16(a16, c);
+            const __m128i pa = _mm_max_epi16(bc, _mm_sub_epi16(z, bc));
+            const __m128i pb = _mm_max_epi16(ac, _mm_sub_epi16(z, ac));
+            const __m128i s = _mm_add_epi16(bc, ac);
+            const __m128i pc = _mm_max_epi16(s, _mm_sub_epi16(z, s));
+            // a if pa <= pb && pa <= pc, else b if pb <= pc, else c
+            const __m128i use_a = _mm_andnot_si128(_mm_or_si128(_mm_cmpgt_epi16(pa, pb), _mm_cmpgt_epi16(pa, pc)),
+                                                   _mm_set1_epi16(-1));
+            const __m128i use_b = _mm_andnot_si128(_mm_cmpgt_epi16(pb, pc), _mm_set1_epi16(-1));
+            const __m128i bc_sel = _mm_or_si128(_mm_and_si128(use_b, b), _mm_andnot_si128(use_b, c));
+            const __m128i pred = _mm_or_si128(_mm_and_si128(use_a, a16), _mm_andnot_si128(use_a, bc_sel));
+            a = _mm_add_epi8(ld(cur + i), _mm_packus_epi16(pred, pred));
+            st(cur + i, a);
+            c = b;
+        }
+    }
+}
+
+bool unfilter(int f, uint8_t *cur, const uint8_t *prior, size_t n, int bpp) {
+    switch (f) {
+    case 0:
+        return true;
+    case 2:
+        if (prior)
+            for (size_t i = 0; i < n; i++) cur[i] = (uint8_t)(cur[i] + prior[i]);
+        return true;
+    case 1:
+    case 3:
+    case 4:
+        if (bpp == 3 && n % 3 == 0) {
+            unfilter_simd<3>(f, cur, prior, n);
+            return true;
+        }
+        if (bpp == 4 && n % 4 == 0) {
+            unfilter_simd<4>(f, cur, prior, n);
+            return true;
+        }
+        for (size_t i = 0; i < n; i++) {
+            const int a = i >= (size_t)bpp ? cur[i - bpp] : 0, b = prior ? prior[i] : 0,
+                      c = (prior && i >= (size_t)bpp) ? prior[i - bpp] : 0;
+            const int pr = f == 1 ? a : (f == 3 ? (a + b) >> 1 : paeth(a, b, c));
+            cur[i] = (uint8_t)(cur[i] + pr);
+        }
+        return true;
+    default:
+        return false;
+    }
+}
+
+// one unfiltered row -> BGR
+void row_to_bgr(const Png &png, const uint8_t *s, uint8_t *o) {
+    const uint32_t w = png.w;
+    const int hb = png.depth == 16 ? 2 : 1;  // high byte first (big-endian samples)
+    switch (png.ctype) {
+    case 2:
+        for (uint32_t x = 0; x < w; x++, s += 3 * hb, o += 3) {
+            o[0] = s[2 * hb];
+            o[1] = s[hb];
+            o[2] = s[0];
+        }
+        break;
+    case 6:
+        for (uint32_t x = 0; x < w; x++, s += 4 * hb, o += 3) {
+            o[0] = s[2 * hb];
+            o[1] = s[hb];
+            o[2] = s[0];
+        }
+        break;
+    case 0:
+        for (uint32_t x = 0; x < w; x++, s += hb, o += 3) o[0] = o[1] = o[2] = s[0];
+        break;
+    case 4:
+        for (uint32_t x = 0; x < w; x++, s += 2 * hb, o += 3) o[0] = o[1] = o[2] = s[0];
+        break;
+    case 3:
+        for (uint32_t x = 0; x < w; x++, s++, o += 3) {
+            const uint32_t i = s[0];
+            if (i < png.plte_n) {
+                o[0] = png.plte[3 * i + 2];
+                o[1] = png.plte[3 * i + 1];
+                o[2] = png.plte[3 * i];
+            } else {
+                o[0] = o[1] = o[2] = 0;
+            }
+        }
+        break;
+    }
+}
+
+int decode_one(const uint8_t *data, size_t size, int32_t h, int32_t w, uint8_t *out) {
+    Png png;
+    int rc = parse(data, size, png, false);
+    if (rc) return rc;
+    if ((int64_t)png.h != h || (int64_t)png.w != w) return LLFE_ERR_CAPACITY;
+    const int bpp = png.channels() * png.depth / 8;
+    const size_t rowb = (size_t)png.w * bpp, stride = rowb + 1, raw_n = stride * png.h;
+    thread_local std::vector<uint8_t> raw, cat;
+    raw.resize(raw_n);
+    if (!inflate_idat(png, raw.data(), raw_n, cat)) return LLFE_ERR_INVALID;
+    for (uint32_t y = 0; y < png.h; y++) {
+        uint8_t *r = raw.data() + y * stride;
+        if (!unfilter(r[0], r + 1, y ? r + 1 - stride : nullptr, rowb, bpp)) return LLFE_ERR_INVALID;
+        row_to_bgr(png, r + 1, out + (size_t)y * png.w * 3);
+    }
+    return LLFE_OK;
+}
+
+}  // namespace
+
+extern "C" int llfe_png_info(const uint8_t *data, uint64_t size, int32_t *width, int32_t *height) {
+    if (!data || !width || !height) return LLFE_ERR_INVALID;
+    Png png;
+    const int rc = parse(data, (size_t)size, png, true);
+    if (rc) return rc;
+    if (png.w > 0x7FFFFFFFu || png.h > 0x7FFFFFFFu) return LLFE_ERR_UNSUPPORTED;
+    *width = (int32_t)png.w;
+    *height = (int32_t)png.h;
+    return LLFE_OK;
+}
+
+extern "C" int llfe_decode_png_batch(const uint8_t *const *data, const uint64_t *sizes, int32_t n, int32_t height,
+                                     int32_t width, uint8_t *out_bgr, int32_t *status, int32_t threads) {
+    if (n < 0 || (n && (!data || !sizes || !out_bgr || !status)) || height <= 0 || width <= 0) return LLFE_ERR_INVALID;
+    const size_t img_bytes = (size_t)height * width * 3;
+    const int nt = std::max(1, std::min<int>(threads > 0 ? threads : 1, n));
+    std::atomic<int> next{0};
+    auto work = [&]() {
+        for (int i; (i = next.fetch_add(1)) < n;) {
+            int rc;
+            try {
+                rc = data[i] ? decode_one(data[i], (size_t)sizes[i], height, width, out_bgr + (size_t)i * img_bytes)
+                             : LLFE_ERR_INVALID;
+            } catch (const std::bad_alloc &) {
+                rc = LLFE_ERR_OOM;
+            }
+            status[i] = rc;
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; t++) th.emplace_back(work);
+    work();
+    for (auto &t : th) t.join();
+    for (int i = 0; i < n; i++)
+        if (status[i]) return status[i];
+    return LLFE_OK;
+}

@@ -17,12 +17,51 @@ class DecodeError(ValueError):
     pass
 
 
+_PNG_SIG = b"\x89PNG\r\n\x1a\n"
+
+
+def _png_native(blobs, h, w, out, threads) -> list:
+    """libllfe's host PNG decoder (csrc/png_decode.cpp) over all blobs into out[i];
+    non-PNG blobs get LLFE_ERR_INVALID.  Returns the per-image status list."""
+    import ctypes as C
+
+    from . import _lib
+
+    L = _lib.lib()
+    n = len(blobs)
+    keep = [C.c_char_p(b) if b[:8] == _PNG_SIG else None for b in blobs]
+    ptrs = (C.c_void_p * n)(*[C.cast(k, C.c_void_p) if k is not None else None for k in keep])
+    sizes = (C.c_uint64 * n)(*[len(b) for b in blobs])
+    status = (C.c_int32 * n)()
+    L.llfe_decode_png_batch(ptrs, sizes, n, h, w, out.ctypes.data, status, int(threads))
+    del keep
+    return list(status)
+
+
+def _png_size(b):
+    import ctypes as C
+
+    from . import _lib
+
+    if b[:8] != _PNG_SIG:
+        return None
+    w, h = C.c_int32(), C.c_int32()
+    if _lib.lib().llfe_png_info(b, len(b), C.byref(w), C.byref(h)) != 0:
+        return None
+    return h.value, w.value
+
+
 def decode_bgr(image_bytes: bytes) -> np.ndarray:
     """-> H x W x 3 uint8 BGR, or raises DecodeError (cv2.imdecode returned None)."""
     from PIL import Image, ImageOps, UnidentifiedImageError
 
     if not image_bytes:
         raise DecodeError("Failed to decode image")
+    hw = _png_size(image_bytes)
+    if hw is not None:  # native PNG path; anything it does not take goes through Pillow
+        out = np.empty((1, hw[0], hw[1], 3), np.uint8)
+        if _png_native([image_bytes], hw[0], hw[1], out, 1)[0] == 0:
+            return out[0]
     try:
         im = Image.open(io.BytesIO(image_bytes))
         im.load()
@@ -105,16 +144,23 @@ def decode_batch(blobs, out=None, workers=None) -> np.ndarray:
     """Decode equally sized images into one N x H x W x 3 BGR uint8 batch (``out`` if
     given, e.g. a pinned host tensor's numpy view).  Raises DecodeError naming the first
     image that fails or whose size differs from the first image's."""
-    blobs = list(blobs)
+    blobs = [bytes(b) for b in blobs]
     if not blobs:
         raise DecodeError("empty batch")
-    first = decode_bgr(blobs[0])
-    h, w = first.shape[:2]
+    hw = _png_size(blobs[0])
+    first = None if hw is not None else decode_bgr(blobs[0])
+    h, w = hw if hw is not None else first.shape[:2]
     if out is None:
         out = np.empty((len(blobs), h, w, 3), np.uint8)
-    if out.shape != (len(blobs), h, w, 3) or out.dtype != np.uint8:
-        raise ValueError(f"out must be {(len(blobs), h, w, 3)} uint8, got {out.shape} {out.dtype}")
-    out[0] = first
+    if out.shape != (len(blobs), h, w, 3) or out.dtype != np.uint8 or not out.flags.c_contiguous:
+        raise ValueError(f"out must be a C-contiguous {(len(blobs), h, w, 3)} uint8 array, got {out.shape} {out.dtype}")
+    todo = list(range(len(blobs)))
+    if hw is not None:  # PNG batch: native decoder, Pillow for whatever it leaves
+        st = _png_native(blobs, h, w, out, workers or default_decode_threads())
+        todo = [i for i, s_ in enumerate(st) if s_ != 0]
+    else:
+        out[0] = first
+        todo = todo[1:]
 
     def one(i):
         try:
@@ -126,7 +172,7 @@ def decode_batch(blobs, out=None, workers=None) -> np.ndarray:
         out[i] = im
         return None
 
-    errs = [e for e in _pool(workers).map(one, range(1, len(blobs))) if e]
+    errs = [e for e in _pool(workers).map(one, todo) if e] if todo else []
     if errs:
         raise DecodeError(errs[0])
     return out

@@ -1,0 +1,167 @@
+"""Host PNG decoder (csrc/png_decode.cpp via decode.py) against Pillow on the same bytes.
+
+PNG is lossless, so any two correct decoders agree bit for bit; the reference decodes
+with cv2.imdecode(IMREAD_COLOR) and decode.py restates those semantics over Pillow
+(alpha dropped, grey expanded, palette looked up, 16-bit -> high byte).  Filters 0-4
+are exercised with hand-built scanlines (Pillow's encoder only emits some of them).
+Runs on the CPU (host code in libllfe.so; no GPU call)."""
+import io
+import struct
+import zlib
+
+import numpy as np
+import pytest
+from PIL import Image
+
+from low_level_feature_extraction_amd import decode
+
+
+def _chunk(t, body):
+    return struct.pack(">I", len(body)) + t + body + struct.pack(">I", zlib.crc32(t + body) & 0xFFFFFFFF)
+
+
+def _png_bytes(raw_rows, w, h, depth, ctype, filters, plte=None, idat_split=1, level=6):
+    """Hand-built PNG: raw_rows (h x rowbytes uint8, unfiltered), filter per row."""
+    bpp = max(1, {0: 1, 2: 3, 3: 1, 4: 2, 6: 4}[ctype] * depth // 8)
+    prev = np.zeros(raw_rows.shape[1], np.int32)
+    out = bytearray()
+    for y in range(h):
+        cur = raw_rows[y].astype(np.int32)
+        f = filters[y % len(filters)]
+        left = np.concatenate([np.zeros(bpp, np.int32), cur[:-bpp]])
+        upleft = np.concatenate([np.zeros(bpp, np.int32), prev[:-bpp]])
+        if f == 0:
+            pred = np.zeros_like(cur)
+        elif f == 1:
+            pred = left
+        elif f == 2:
+            pred = prev
+        elif f == 3:
+            pred = (left + prev) >> 1
+        else:
+            p = left + prev - upleft
+            pa, pb, pc = abs(p - left), abs(p - prev), abs(p - upleft)
+            pred = np.where((pa <= pb) & (pa <= pc), left, np.where(pb <= pc, prev, upleft))
+        out.append(f)
+        out += ((cur - pred) & 255).astype(np.uint8).tobytes()
+        prev = cur
+    z = zlib.compress(bytes(out), level)
+    parts = [z[i * len(z) // idat_split:(i + 1) * len(z) // idat_split] for i in range(idat_split)]
+    png = b"\x89PNG\r\n\x1a\n" + _chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, depth, ctype, 0, 0, 0))
+    if plte is not None:
+        png += _chunk(b"PLTE", plte)
+    for p in parts:
+        png += _chunk(b"IDAT", p)
+    return png + _chunk(b"IEND", b"")
+
+
+def _pillow_ref(b):
+    """decode.py's Pillow restatement, bypassing the native path."""
+    from PIL import Image as I
+
+    im = I.open(io.BytesIO(b))
+    im.load()
+    mode = im.mode
+    if mode in ("I;16", "I;16B", "I;16L", "I"):
+        a = np.asarray(im)
+        g = (np.clip(a, 0, 65535).astype(np.uint16) >> 8).astype(np.uint8)
+        rgb = np.repeat(g[:, :, None], 3, axis=2)
+    elif mode == "RGB":
+        rgb = np.asarray(im)
+    elif mode in ("RGBA", "RGBX"):
+        rgb = np.asarray(im)[:, :, :3]
+    elif mode == "LA":
+        rgb = np.asarray(im.getchannel("L").convert("RGB"))
+    elif mode == "PA":
+        rgb = np.asarray(im.convert("RGBA"))[:, :, :3]
+    else:
+        rgb = np.asarray(im.convert("RGB"))[:, :, :3]
+    return np.ascontiguousarray(rgb[:, :, ::-1])
+
+
+def _native(b):
+    hw = decode._png_size(b)
+    assert hw is not None
+    out = np.zeros((1, hw[0], hw[1], 3), np.uint8)
+    st = decode._png_native([b], hw[0], hw[1], out, 1)
+    return st[0], out[0]
+
+
+@pytest.mark.parametrize("ctype,depth", [(2, 8), (6, 8), (0, 8), (4, 8), (3, 8), (2, 16), (6, 16), (0, 16), (4, 16)])
+@pytest.mark.parametrize("filters", [[0], [1], [2], [3], [4], [0, 1, 2, 3, 4]])
+def test_native_png_matches_pillow(ctype, depth, filters):
+    rng = np.random.default_rng(ctype * 100 + depth + len(filters) + filters[0])
+    w, h = 37, 11
+    ch = {0: 1, 2: 3, 3: 1, 4: 2, 6: 4}[ctype]
+    plte = None
+    if ctype == 3:
+        plte = rng.integers(0, 256, 3 * 200, dtype=np.uint8).tobytes()
+        raw = rng.integers(0, 200, (h, w), dtype=np.uint8)
+    else:
+        # smooth + noisy content so every predictor path sees varied neighbours
+        base = (np.arange(w * ch)[None, :] * 3 + np.arange(h)[:, None] * 7) % 256
+        raw = ((base + rng.integers(0, 40, (h, w * ch))) % 256).astype(np.uint8)
+        if depth == 16:
+            lo = rng.integers(0, 256, raw.shape, dtype=np.uint8)
+            raw = np.stack([raw, lo], -1).reshape(h, -1)
+    b = _png_bytes(raw, w, h, depth, ctype, filters, plte=plte, idat_split=3)
+    st, got = _native(b)
+    assert st == 0
+    np.testing.assert_array_equal(got, _pillow_ref(b))
+
+
+@pytest.mark.parametrize("w,h", [(1, 1), (2, 3), (64, 1), (1, 50), (1920, 4)])
+def test_native_png_sizes_and_pillow_encoded(w, h):
+    rng = np.random.default_rng(w * 7 + h)
+    a = rng.integers(0, 256, (h, w, 3), dtype=np.uint8)
+    for mode, arr in (("RGB", a), ("RGBA", np.concatenate([a, a[:, :, :1]], 2)), ("L", a[:, :, 0])):
+        buf = io.BytesIO()
+        Image.fromarray(arr, mode).save(buf, "PNG", compress_level=1)
+        st, got = _native(buf.getvalue())
+        assert st == 0
+        np.testing.assert_array_equal(got, _pillow_ref(buf.getvalue()))
+
+
+def test_unsupported_and_corrupt_inputs_fall_back_or_fail():
+    a = np.random.default_rng(0).integers(0, 256, (20, 30, 3), dtype=np.uint8)
+    buf = io.BytesIO()
+    Image.fromarray(a).save(buf, "PNG")
+    good = buf.getvalue()
+    # interlaced (Adam7): native says unsupported, decode_bgr still decodes via Pillow
+    raw = a.reshape(20, -1)
+    inter = bytearray(_png_bytes(raw, 30, 20, 8, 2, [0]))
+    inter[8 + 8 + 12] = 1  # IHDR interlace byte
+    inter[8 + 8 + 13:8 + 8 + 17] = struct.pack(">I", zlib.crc32(bytes(inter[8 + 4:8 + 8 + 13])) & 0xFFFFFFFF)
+    st, _ = _native(bytes(inter))
+    assert st == -5
+    # 1-bit grey: unsupported natively, Pillow path decodes it
+    bw = Image.fromarray((a[:, :, 0] > 128)).convert("1")
+    buf = io.BytesIO()
+    bw.save(buf, "PNG")
+    np.testing.assert_array_equal(decode.decode_bgr(buf.getvalue()), _pillow_ref(buf.getvalue()))
+    # CRC error in IDAT -> error
+    bad = bytearray(good)
+    i = bad.index(b"IDAT")
+    bad[i + 10] ^= 0xFF
+    st, _ = _native(bytes(bad))
+    assert st == -1
+    with pytest.raises(decode.DecodeError):
+        decode.decode_bgr(bytes(bad))
+    # truncated stream
+    with pytest.raises(decode.DecodeError):
+        decode.decode_bgr(good[: len(good) // 2])
+
+
+def test_decode_batch_mixed_png_and_jpeg():
+    rng = np.random.default_rng(5)
+    a = rng.integers(0, 256, (16, 24, 3), dtype=np.uint8)
+    p = io.BytesIO()
+    Image.fromarray(a).save(p, "PNG")
+    j = io.BytesIO()
+    Image.fromarray(a).save(j, "JPEG", quality=95)
+    out = decode.decode_batch([p.getvalue(), j.getvalue(), p.getvalue()], workers=2)
+    np.testing.assert_array_equal(out[0], a[:, :, ::-1])
+    np.testing.assert_array_equal(out[2], a[:, :, ::-1])
+    np.testing.assert_array_equal(out[1], _pillow_ref(j.getvalue()))
+    out2 = decode.decode_batch([j.getvalue(), p.getvalue()], workers=2)
+    np.testing.assert_array_equal(out2[1], a[:, :, ::-1])
