@@ -125,7 +125,7 @@ def e2e_png(be, B, H, W, feats, steps, distinct, seed):
     return {"value": round(B * steps / dt, 2), "unit": "images/s", "decode_threads": threads,
             "decode_ms_per_image_per_thread": round(dec_ms, 2),
             "sample": f"{steps} x {B} PNG-encoded {W}x{H} synthetic images ({distinct} distinct, {mb:.1f} MiB each), "
-                      f"decoded on the host (Pillow, cv2.imdecode IMREAD_COLOR semantics) into host batches, "
+                      f"decoded on the host (libllfe PNG decoder, cv2.imdecode IMREAD_COLOR semantics) into host batches, "
                       f"then the full GPU path incl. H2D"}
 
 

@@ -141,6 +141,11 @@ int llfe_shape_mask(llfe_ctx *ctx, const uint8_t *bgr, uint8_t *mask, int32_t n,
 /* Canny NMS classes before hysteresis: 0 weak, 1 suppressed, 2 strong */
 int llfe_edge_classes(llfe_ctx *ctx, const uint8_t *bgr, uint8_t *classes, int32_t n, int32_t h, int32_t w,
                       llfe_stream stream);
+/* FontDetector.preprocess_image (app/services/analyze/font_detector.py:17-37):
+ * adaptiveThreshold(cvtColor(BGR2GRAY), 255, GAUSSIAN_C, THRESH_BINARY_INV, 11, 2) as
+ * 0/255 u8; bgr and mask are device pointers (n x h x w x 3 / n x h x w). */
+int llfe_font_binary(llfe_ctx *ctx, const uint8_t *bgr, uint8_t *mask, int32_t n, int32_t h, int32_t w,
+                     llfe_stream stream);
 /* sums[n], counts[n] host: adaptive-threshold shadow statistics (shadow pyc @L15-21) */
 int llfe_shadow_stats(llfe_ctx *ctx, const uint8_t *bgr, uint64_t *sums, uint64_t *counts, int32_t n, int32_t h,
                       int32_t w, llfe_stream stream);

@@ -7,13 +7,15 @@ Drop-in replacements for the reference's hot-path services:
     ColorExtractor.extract_colors       (app/services/analyze/color_extractor.py)
     ShapeAnalyzer.analyze_shapes        (app/services/shape_analyzer)
     ShadowAnalyzer.analyze_shadow_level (app/services/shadow_analyzer)
+    FontDetector.detect_font            (app/services/analyze/font_detector.py)
 
 plus batched entry points (``run_batch``, ``*_batch``).  All per-pixel work runs in
 libllfe.so (HIP kernels for gfx950, C ABI in include/llfe.h); there is no CPU fallback.
 """
 from .color_extractor import ColorExtractor
+from .font_detector import FontDetector
 from .image_processor import ImageProcessor
-from .models import ColorFeatures, FeatureType
+from .models import ColorFeatures, FeatureType, FontFeatures
 from .shadow_analyzer import ShadowAnalyzer
 from .shape_analyzer import ShapeAnalyzer
 from .utils import PreprocessingMode, validate_and_preprocess_image
@@ -29,6 +31,8 @@ __all__ = [
     "ColorExtractor",
     "ColorFeatures",
     "FeatureType",
+    "FontDetector",
+    "FontFeatures",
     "ImageProcessor",
     "PreprocessingMode",
     "ShadowAnalyzer",

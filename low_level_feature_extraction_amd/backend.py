@@ -223,6 +223,15 @@ class Backend:
         self._chk(self._lib.llfe_edge_classes(self.ctx, x.data_ptr(), out.data_ptr(), n, h, w, self._stream(x)))
         return out
 
+    def font_binary(self, images):
+        """FontDetector.preprocess_image on the GPU: n x h x w u8 0/255 device tensor."""
+        torch = _torch()
+        x = self._dev_batch(images)
+        n, h, w, _ = x.shape
+        out = torch.empty((n, h, w), dtype=torch.uint8, device=x.device)
+        self._chk(self._lib.llfe_font_binary(self.ctx, x.data_ptr(), out.data_ptr(), n, h, w, self._stream(x)))
+        return out
+
     def shape_mask(self, images):
         torch = _torch()
         x = self._dev_batch(images)

@@ -743,6 +743,15 @@ int llfe_edge_classes(llfe_ctx *ctx, const uint8_t *bgr, uint8_t *classes, int32
     return LLFE_OK;
 }
 
+int llfe_font_binary(llfe_ctx *ctx, const uint8_t *bgr, uint8_t *mask, int32_t n, int32_t h, int32_t w,
+                     llfe_stream stream) {
+    if (!ctx || !valid_dims(n, h, w) || !bgr || !mask) return LLFE_ERR_INVALID;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    HIPCHK(ctx, launch_font_binary(bgr, n, h, w, mask, ctx->sp, (hipStream_t)stream));
+    HIPCHK(ctx, hipStreamSynchronize((hipStream_t)stream));
+    return LLFE_OK;
+}
+
 int llfe_shape_mask(llfe_ctx *ctx, const uint8_t *bgr, uint8_t *mask, int32_t n, int32_t h, int32_t w,
                     llfe_stream stream) {
     if (!ctx || !valid_dims(n, h, w) || !bgr || !mask) return LLFE_ERR_INVALID;

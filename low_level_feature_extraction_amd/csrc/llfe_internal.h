@@ -26,6 +26,12 @@ hipError_t launch_stencil(const uint8_t *bgr, int n, int h, int w, uint8_t *cls,
                           unsigned long long *shadow_sum, unsigned long long *shadow_cnt, uint2 *tile_part,
                           const StencilParams &p, hipStream_t s);
 
+// FontDetector.preprocess_image (font_detector.py:17-37): gray -> adaptiveThreshold(
+// GAUSSIAN_C, THRESH_BINARY_INV, 11, 2) -> n x h x w u8 255 / 0 (the stencil kernel
+// with the Gaussian mean taken over the gray image instead of the blurred one)
+hipError_t launch_font_binary(const uint8_t *bgr, int n, int h, int w, uint8_t *mask, const StencilParams &p,
+                              hipStream_t s);
+
 // Canny hysteresis as connected components + dilate(3x3) + bit-pack (hysteresis.hip).
 // Workspace: lab n*h*w u16; parent/sroot/roots over hysteresis_ids() entries; nroots
 // per tile.  bits: n x h x words_per_row u64 (bit x&63 of word x>>6), mask_u8 optional.

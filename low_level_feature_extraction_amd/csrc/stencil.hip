@@ -62,7 +62,7 @@ __device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(
 template <bool BORDER>
 __device__ void stencil_tile(FastSmem &sm, const uint8_t *__restrict__ src, int H, int W, int tx0, int ty0,
                                  uint8_t *__restrict__ cls, uint8_t *__restrict__ blurred_out,
-                                 uint2 *tile_part,
+                                 uint2 *tile_part, uint8_t *__restrict__ font_mask,
                                  const StencilParams &prm) {
     const int tid = threadIdx.x;
     // 1) gray: 4 BGR pixels (12 bytes, 3 dwords) -> one dword of gray.  Per pixel the
@@ -96,6 +96,16 @@ __device__ void stencil_tile(FastSmem &sm, const uint8_t *__restrict__ src, int 
         sm.g[row][q] = y0 | (y1 << 8) | (y2 << 16) | (y3 << 24);
     }
     __syncthreads();
+    if (font_mask) {
+        // FontDetector.preprocess_image thresholds the gray image itself (no blur5): the
+        // "blurred" rows are the gray rows y = ty0 - 5 + ly, x = tx0 - 6 + 4q .. (two
+        // bytes into gray dword q)
+        for (int u = tid; u < BHT * (FBW / 4); u += NT) {
+            const int ly = u / (FBW / 4), q = u - ly * (FBW / 4);
+            sm.blur[ly][q] = __builtin_amdgcn_perm(sm.g[ly + 2][q + 1], sm.g[ly + 2][q], 0x05040302u);
+        }
+        __syncthreads();
+    } else {
     // 2) horizontal blur5 in packed u16 with the unscaled taps [1, 4, 6, 4, 1] (sum of a
     //    row <= 16 * 255): hb col c <-> x = tx0 - 6 + c; taps are gray cols c .. c + 4.
     //    (the 8U blur is (sum_ij w_i w_j g + 128) >> 8, so both passes fit in 16 bits)
@@ -133,6 +143,7 @@ __device__ void stencil_tile(FastSmem &sm, const uint8_t *__restrict__ src, int 
         sm.blur[ly][q] = __builtin_amdgcn_perm(as_u32(s23), as_u32(s01), 0x06040200u);
     }
     __syncthreads();
+    }
     if (BORDER) {
         // blurred values outside the image: REPLICATE (Sobel's and the CV_32F Gauss11's
         // border on the blurred image)
@@ -233,7 +244,7 @@ __device__ void stencil_tile(FastSmem &sm, const uint8_t *__restrict__ src, int 
         }
     }
 
-    if (tile_part) {
+    if (tile_part || font_mask) {
         // 6) CV_32F row pass (fma chain left -> right) for 4 consecutive x = tx0 + 4q + j
         //    on two rows at once (packed FP32: lane 0 = row ly, lane 1 = row ly + 1; each
         //    lane is the same fma chain as the scalar form): taps are blur cols
@@ -281,6 +292,7 @@ __device__ void stencil_tile(FastSmem &sm, const uint8_t *__restrict__ src, int 
             const uint32_t bw = sm.blur[ly][q + 1], bw2 = sm.blur[ly][q + 2];
             // blur cols for x = tx0 + 4q + j are 4q + 6 + j: bytes 2, 3 of dword q + 1, 0, 1 of q + 2
             const int bv[4] = {(int)byte_of(bw, 2), (int)byte_of(bw, 3), (int)byte_of(bw2, 0), (int)byte_of(bw2, 1)};
+            uint32_t mo = 0;
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 int mean = (int)__builtin_rintf(sj[j]);
@@ -289,6 +301,16 @@ __device__ void stencil_tile(FastSmem &sm, const uint8_t *__restrict__ src, int 
                 if (in && bv[j] - mean <= -2) {
                     lsum += (unsigned)bv[j];
                     lcnt += 1;
+                    mo |= 255u << (8 * j);
+                }
+            }
+            if (font_mask) {  // adaptiveThreshold(..., THRESH_BINARY_INV, 11, 2) -> 255 / 0
+                if (BORDER) {
+                    const int Y = ty0 + ty, X = tx0 + 4 * q;
+                    if (Y < H)
+                        for (int j = 0; j < 4 && X + j < W; j++) font_mask[(size_t)Y * W + X + j] = (uint8_t)(mo >> (8 * j));
+                } else {
+                    *(uint32_t *)(font_mask + (size_t)(ty0 + ty) * W + tx0 + 4 * q) = mo;
                 }
             }
         }
@@ -300,7 +322,7 @@ __device__ void stencil_tile(FastSmem &sm, const uint8_t *__restrict__ src, int 
         // one (sum, count) per tile, no atomics: k_shadow_reduce adds the tiles up
         if ((tid & 63) == 0) sm.red[tid >> 6] = make_uint2(lsum, lcnt);
         __syncthreads();
-        if (tid == 0) {
+        if (tid == 0 && tile_part) {
             uint2 r = sm.red[0];
 #pragma unroll
             for (int w = 1; w < NT / 64; w++) {
@@ -342,21 +364,24 @@ __global__ __launch_bounds__(256) void k_shadow_reduce(const uint2 *__restrict__
 
 __global__ __launch_bounds__(NT) void k_stencil(const uint8_t *__restrict__ bgr, int H, int W, int ntx, int nty,
                                                 uint8_t *__restrict__ cls, uint8_t *__restrict__ blurred_out,
-                                                uint2 *__restrict__ tile_part, StencilParams prm) {
+                                                uint2 *__restrict__ tile_part, uint8_t *__restrict__ font_mask,
+                                                StencilParams prm) {
     __shared__ FastSmem shm;
     const int tid = threadIdx.x;
     const int img = blockIdx.y;
     const int t = blockIdx.x;
     const int tx0 = (t % ntx) * TW, ty0 = (t / ntx) * TH;
     const uint8_t *src = bgr + (size_t)img * H * W * 3;
-    const bool aligned = (((uintptr_t)bgr | (uintptr_t)cls | (uintptr_t)blurred_out) & 3) == 0 && (W & 3) == 0;
+    const bool aligned =
+        (((uintptr_t)bgr | (uintptr_t)cls | (uintptr_t)blurred_out | (uintptr_t)font_mask) & 3) == 0 && (W & 3) == 0;
+    uint8_t *fm = font_mask ? font_mask + (size_t)img * H * W : nullptr;
     uint8_t *c = cls ? cls + (size_t)img * H * W : nullptr;
     uint8_t *bo = blurred_out ? blurred_out + (size_t)img * H * W : nullptr;
     uint2 *tp = tile_part ? tile_part + (size_t)img * ntx * nty + t : nullptr;
     if (aligned && tx0 >= 8 && ty0 >= HG && tx0 + TW + 8 <= W && ty0 + TH + HG <= H)
-        stencil_tile<false>(shm, src, H, W, tx0, ty0, c, bo, tp, prm);
+        stencil_tile<false>(shm, src, H, W, tx0, ty0, c, bo, tp, fm, prm);
     else
-        stencil_tile<true>(shm, src, H, W, tx0, ty0, c, bo, tp, prm);
+        stencil_tile<true>(shm, src, H, W, tx0, ty0, c, bo, tp, fm, prm);
 }
 
 }  // namespace
@@ -367,9 +392,18 @@ hipError_t launch_stencil(const uint8_t *bgr, int n, int h, int w, uint8_t *cls,
     int ntx = tiles_x(w), nty = tiles_y(h);
     dim3 grid(ntx * nty, n);
     hipLaunchKernelGGL(k_stencil, grid, dim3(NT), 0, s, bgr, h, w, ntx, nty, cls, blurred,
-                       shadow_sum ? tile_part : nullptr, p);
+                       shadow_sum ? tile_part : nullptr, (uint8_t *)nullptr, p);
     if (shadow_sum)
         hipLaunchKernelGGL(k_shadow_reduce, dim3(n), dim3(256), 0, s, tile_part, ntx * nty, shadow_sum, shadow_cnt);
+    return hipGetLastError();
+}
+
+hipError_t launch_font_binary(const uint8_t *bgr, int n, int h, int w, uint8_t *mask, const StencilParams &p,
+                              hipStream_t s) {
+    int ntx = tiles_x(w), nty = tiles_y(h);
+    dim3 grid(ntx * nty, n);
+    hipLaunchKernelGGL(k_stencil, grid, dim3(NT), 0, s, bgr, h, w, ntx, nty, (uint8_t *)nullptr, (uint8_t *)nullptr,
+                       (uint2 *)nullptr, mask, p);
     return hipGetLastError();
 }
 

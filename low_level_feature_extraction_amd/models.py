@@ -46,6 +46,25 @@ except Exception:  # standalone
                                  "processing_time": md.get("processing_time", 0.0)})
 
 
+try:  # inside the reference app: use its contract directly
+    from app.api.v1.models.analyze import FontFeatures  # type: ignore  # noqa: F401
+except Exception:  # standalone
+
+    class FontFeatures(BaseModel):
+        """Font analysis result (same fields as the reference's FontFeatures,
+        app/api/v1/models/analyze.py:207-241)."""
+
+        font_family: Optional[str] = None
+        font_size: Optional[float] = None
+        font_style: Optional[str] = None
+        confidence: Optional[float] = None
+
+        @classmethod
+        def from_dict(cls, data: Dict[str, Any]) -> "FontFeatures":
+            return cls(font_family=data.get("font_family"), font_size=data.get("font_size"),
+                       font_style=data.get("font_style"), confidence=data.get("confidence"))
+
+
 class FeatureType(str, Enum):
     """FeatureType of app/api/v1/models/analyze.py:6-10 plus the two analyzers that
     exist in the reference only as bytecode (shape / shadow)."""
