@@ -36,12 +36,16 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 def _load_traffic():
     try:
         with open(os.path.join(ROOT, "profiles", "traffic_latest.json")) as f:
-            return {k: round(v["bytes"]) for k, v in json.load(f)["kernels"].items()}
+            k = json.load(f)["kernels"]
+        return ({n: round(v["bytes"]) for n, v in k.items()},
+                {n: v["valu_insts"] for n, v in k.items() if "valu_insts" in v})
     except (OSError, KeyError, ValueError):
-        return {}
+        return {}, {}
 
 
-TRAFFIC: dict = _load_traffic()
+# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 4 cycles each
+VALU_SLOTS_PER_S = 256 * 4 / 4 * 2.4e9
+TRAFFIC, VALU_INSTS = _load_traffic()
 
 
 def _cpu_worker(args):
@@ -200,9 +204,14 @@ def main():
         avg_ms = st["total_ms"] / max(st["launches"], 1)
         bpl = st["bytes"] / max(st["launches"], 1)
         achieved = bpl / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-        return {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": TRAFFIC.get(name),
-                "bytes_per_launch": bpl, "avg_launch_ms": round(avg_ms, 4)}
+        r = {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": TRAFFIC.get(name),
+             "bytes_per_launch": bpl, "avg_launch_ms": round(avg_ms, 4)}
+        if name in VALU_INSTS and avg_ms > 0:
+            # PMC SQ_INSTS_VALU per launch (profiles/traffic_latest.json) over the launch's
+            # VALU issue capacity at 2.4 GHz: how close the kernel is to its compute bound
+            r["valu_busy"] = round(VALU_INSTS[name] / (VALU_SLOTS_PER_S * avg_ms * 1e-3), 3)
+        return r
 
     kernels = {}
     for name, st in stats.items():

@@ -3,7 +3,7 @@
 preprocess_image -- cvtColor(BGR2GRAY) + adaptiveThreshold(GAUSSIAN_C, THRESH_BINARY_INV,
 11, 2) (:17-37) -- runs on the GPU (llfe_font_binary: the stencil kernel with the CV_32F
 11x11 Gaussian mean over the gray image, bit-exact vs the oracle).  Region detection
-(findContours RETR_EXTERNAL + boundingRect + the aspect / height filter, :39-67) runs on
+(findContours RETR_EXTERNAL + boundingRect + the aspect / height filter, :40-67) runs on
 the host contour code of the shapes path; the remaining heuristics (:69-171) are the
 reference's, restated: font size = int(0.75 h), weight from the region's mean gray,
 family "Arial", confidence 0.8, and ``detect_font`` returns None when no region is found

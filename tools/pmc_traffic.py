@@ -2,7 +2,7 @@
 """Per-launch HBM traffic from rocprofv3 PMC passes (FETCH_SIZE and WRITE_SIZE run
 separately, MI355X_MICROARCH.md §HBM / §PMC slots).
 
-    python tools/pmc_traffic.py FETCH_DIR WRITE_DIR > traffic.json
+    python tools/pmc_traffic.py FETCH_DIR WRITE_DIR [VALU_DIR] > traffic.json
 
 Each DIR holds run_counter_collection.csv from
 ``rocprofv3 --pmc <C> --kernel-trace -d DIR -o run --output-format csv -- python3 bench.py ...``.
@@ -30,7 +30,9 @@ FETCH_X2 = {"k_kmeans", "k_uq_keys", "k_uq_scatter"}  # 16 B/lane streaming read
 
 LOGICAL = [  # (substring of the device kernel name, logical launch)
     ("k_stencil", "k_stencil"),
+    ("k_shadow_reduce", "k_stencil"),
     ("k_ccl_", "k_hysteresis_dilate"),
+    ("k_bits_dilate", "k_hysteresis_dilate"),
     ("k_uq_keys", "k_uq_keys"),
     ("k_uq_scatter", "k_uq_scatter"),
     ("k_uq_part", "k_uq_part"),
@@ -86,6 +88,12 @@ def main():
         lg = logical(k)
         if lg:
             agg[lg]["write_kib_raw"] += v / chunks(wd)
+    if len(sys.argv) > 3:  # SQ_INSTS_VALU pass: VALU wave-instructions per logical launch
+        vt, vd = load(sys.argv[3], "SQ_INSTS_VALU")
+        for k, v in vt.items():
+            lg = logical(k)
+            if lg:
+                agg[lg]["valu_insts"] = agg[lg].get("valu_insts", 0.0) + v / chunks(vd)
     for lg, a in agg.items():
         a["bytes"] = a["fetch_kib_raw"] * 1024 * (2 if lg in FETCH_X2 else 1) + a["write_kib_raw"] * 1024
         out["kernels"][lg] = a
