@@ -217,9 +217,11 @@ __device__ __forceinline__ int moved_label(const KmSmem &sm, int i, int l) {
 // are contiguous ranges of the sorted keys and unions of whole cubes (cube id = R << 12
 // | ...), so the partition holding p comes from per-partition cube totals and only that
 // partition's sorted keys are scanned.
+// |a|, |b|, |c| <= 255: 24-bit multiplies (v_mul_i32_i24 / v_mad_i32_i24, full rate) instead
+// of the quarter-rate v_mul_lo_u32 a plain int product compiles to
 __device__ __forceinline__ int d2i(int x, int y, int z, int cx, int cy, int cz) {
     const int a = x - cx, b = y - cy, c = z - cz;
-    return a * a + b * b + c * c;
+    return __mul24(a, a) + __mul24(b, b) + __mul24(c, c);
 }
 
 struct ICent {
@@ -259,8 +261,11 @@ __device__ __forceinline__ CubeGeo cube_geo(const CubeEnt &e) {
     return g;
 }
 __device__ __forceinline__ uint32_t cube_sum(const CubeGeo &g, int cx, int cy, int cz) {
+    // n <= 64, |a| <= 255, S_u <= 192: every factor fits 24 bits (n |o - c|^2 < 2^24 unsigned)
     const int ax = g.ox - cx, ay = g.oy - cy, az = g.oz - cz;
-    return (uint32_t)(g.n * (ax * ax + ay * ay + az * az) + 2 * (ax * g.sx + ay * g.sy + az * g.sz) + g.s2);
+    const uint32_t q = (uint32_t)(__mul24(ax, ax) + __mul24(ay, ay) + __mul24(az, az));
+    return __umul24((uint32_t)g.n, q) + 2u * (uint32_t)(__mul24(ax, g.sx) + __mul24(ay, g.sy) + __mul24(az, g.sz)) +
+           (uint32_t)g.s2;
 }
 
 // per lane: bit `lane` of the wave-uniform 64-bit mask m ? a : b -- one v_cndmask_b32
