@@ -74,15 +74,27 @@ void trace_outer(int8_t *im, int pitch, int64_t i0, int x, int y, std::vector<in
 }
 
 // Raster scan of the padded {0,1} image in OpenCV's order (RETR_EXTERNAL: holes and
-// borders enclosed by an already traced border are skipped).
-void scan_external(int8_t *im, int h, int w, const uint8_t *row_nonzero, Contours &out) {
+// borders enclosed by an already traced border are skipped).  `bits` (optional) is the
+// mask bit-packed (bit x & 63 of word x >> 6 of row y - 1): runs of zeros seen with
+// prev == 0 change no scan state, so they are skipped a word at a time.
+void scan_external(int8_t *im, int h, int w, const uint8_t *row_nonzero, Contours &out,
+                   const uint64_t *bits = nullptr, int wpr = 0) {
     const int pitch = w + 2;
     for (int y = 1; y <= h; y++) {
         if (row_nonzero && !row_nonzero[y - 1]) continue;  // nothing can start or mark here
         int8_t *row = im + (int64_t)y * pitch;
+        const uint64_t *rb = bits ? bits + (size_t)(y - 1) * wpr : nullptr;
         int lnbd = 0;
         int prev = 0;
         for (int x = 1; x <= w; x++) {
+            if (rb && prev == 0) {  // jump to the next nonzero pixel (bit x - 1 onwards)
+                int q = (x - 1) >> 6;
+                uint64_t word = rb[q] & (~0ull << ((x - 1) & 63));
+                while (!word && ++q < wpr) word = rb[q];
+                if (!word) break;
+                x = q * 64 + __builtin_ctzll(word) + 1;
+                if (x > w) break;
+            }
             int v = row[x];
             if (v == prev) continue;
             bool start = false;
@@ -102,6 +114,19 @@ void scan_external(int8_t *im, int h, int w, const uint8_t *row_nonzero, Contour
         }
     }
 }
+
+// byte i of kExpand[b] = bit i of b (0 / 1)
+struct ExpandTable {
+    uint64_t t[256];
+    ExpandTable() {
+        for (int b = 0; b < 256; b++) {
+            uint64_t v = 0;
+            for (int i = 0; i < 8; i++) v |= (uint64_t)((b >> i) & 1) << (8 * i);
+            t[b] = v;
+        }
+    }
+};
+const ExpandTable kExpand;
 
 }  // namespace
 
@@ -153,6 +178,11 @@ void external_contours_bits(const uint64_t *bits, int h, int w, int wpr, std::ve
             int8_t *dst = r + 1 + x0;
             if (!v) {
                 std::memset(dst, 0, (size_t)n);
+            } else if (n == 64) {
+                for (int k = 0; k < 8; k++) {
+                    const uint64_t e = kExpand.t[(v >> (8 * k)) & 255];
+                    std::memcpy(dst + 8 * k, &e, 8);
+                }
             } else {
                 for (int b = 0; b < n; b++) dst[b] = (int8_t)((v >> b) & 1);
             }
@@ -160,7 +190,7 @@ void external_contours_bits(const uint64_t *bits, int h, int w, int wpr, std::ve
     }
     out.xy.clear();
     out.start.clear();
-    scan_external(work.data(), h, w, nz.data(), out);
+    scan_external(work.data(), h, w, nz.data(), out, bits, wpr);
     out.start.push_back((int64_t)(out.xy.size() / 2));
 }
 

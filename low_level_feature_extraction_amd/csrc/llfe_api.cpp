@@ -333,6 +333,8 @@ struct llfe_ctx {
     HostBuf<unsigned long long> h_shadow_s[2];
     HostBuf<KmeansImageOut> h_kout_s[2];
     hipEvent_t chunk_done[2] = {nullptr, nullptr};
+    hipEvent_t input_ready = nullptr, colour_done = nullptr, front_done = nullptr;  // intra-chunk stream split
+    bool shapes_after_front = false;  // LLFE_SHAPES_AFTER_FRONT=1: shapes wait for the colour front
     hipEvent_t mask_done[2] = {nullptr, nullptr};  // shapes/shadows results are on the host
     // the mask / shadow D2H runs on its own stream so the colour stage starts right after
     // the hysteresis kernels; mask_ready[slot] orders it after them, and a workspace is
@@ -509,6 +511,27 @@ int enqueue_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_
     const int8_t *noise;
     int rc = stage_input(ctx, W, b, i0, n, &img, &noise, s);
     if (rc) return rc;
+    // single-slot mode: the colour path (unique colours + k-means) runs on the second
+    // stream, concurrently with shapes / shadows (both only read the input).  Measured
+    // (512 x 1080p): shapes alongside the colour front 13.1k images/s; shapes held back
+    // to share the GPU with k-means (LLFE_SHAPES_AFTER_FRONT=1) 12.8k -- the stencil
+    // waves slow the k-means attempts more than they fill its tail.
+    hipStream_t col_s = s;
+    if (want_col && ctx->nstreams == 1 && (want_shp || want_shd)) {
+        col_s = ctx->streams[1];
+        HIPCHK(ctx, hipEventRecord(ctx->input_ready, s));
+        HIPCHK(ctx, hipStreamWaitEvent(col_s, ctx->input_ready, 0));
+    }
+    // colour front (unique colours), then shapes / shadows (on the other stream unless
+    // held back), then k-means
+    if (want_col) {
+        rc = color_stage(ctx, W, img, noise, n, h, w, seed, b->index_base + i0, col_s);
+        if (rc) return rc;
+        if (col_s != s && ctx->shapes_after_front) {
+            HIPCHK(ctx, hipEventRecord(ctx->front_done, col_s));
+            HIPCHK(ctx, hipStreamWaitEvent(s, ctx->front_done, 0));
+        }
+    }
     // d_shadow / d_bits of this workspace may still be in the previous chunk's D2H
     if (ctx->w_mask_slot[q] >= 0) HIPCHK(ctx, hipStreamWaitEvent(s, ctx->mask_done[ctx->w_mask_slot[q]], 0));
     if (want_shp || want_shd) {
@@ -519,8 +542,8 @@ int enqueue_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_
                              want_shd ? W.d_shadow.p : nullptr, want_shd ? W.d_shadow.p + n : nullptr,
                              (uint2 *)(W.d_shadow.p + 2 * n), ctx->sp, s));
     }
-    // shapes + shadows first: their results go to the host (event mask_done) while the
-    // GPU is still in this chunk's colour stage, so contour tracing overlaps k-means
+    // shapes + shadows go to the host (event mask_done) while the GPU is still in this
+    // chunk's colour stage, so contour tracing overlaps k-means
     if (want_shp) {
         HIPCHK(ctx, W.d_bits.ensure((size_t)n * h * wpr));
         HIPCHK(ctx, ctx->h_bits_s[slot].ensure((size_t)n * h * wpr));
@@ -544,16 +567,18 @@ int enqueue_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_
         HIPCHK(ctx, hipEventRecord(ctx->mask_done[slot], s));
     }
     if (want_col) {
-        rc = color_stage(ctx, W, img, noise, n, h, w, seed, b->index_base + i0, s);
-        if (rc) return rc;
         const KmeansCubes cubes{W.d_cubes.p, std::min<int64_t>(key_stride, kMaxCubes), W.d_ncubes.p,
                                 W.d_pmeta.p + (size_t)2 * n * kParts};
         rc = kmeans_stage(ctx, W, W.d_keys.p, key_stride, W.d_nuniq.p, n, b->n_colors ? b->n_colors : kMaxK, seed,
-                          b->index_base + i0, cubes, s);
+                          b->index_base + i0, cubes, col_s);
         if (rc) return rc;
         HIPCHK(ctx, ctx->h_kout_s[slot].ensure(n));
         HIPCHK(ctx, hipMemcpyAsync(ctx->h_kout_s[slot].p, W.d_kout.p, sizeof(KmeansImageOut) * n,
-                                   hipMemcpyDeviceToHost, s));
+                                   hipMemcpyDeviceToHost, col_s));
+        if (col_s != s) {  // the chunk (and the next chunk's use of this workspace) ends after both
+            HIPCHK(ctx, hipEventRecord(ctx->colour_done, col_s));
+            HIPCHK(ctx, hipStreamWaitEvent(s, ctx->colour_done, 0));
+        }
     }
     HIPCHK(ctx, hipEventRecord(ctx->chunk_done[slot], s));
     return LLFE_OK;
@@ -631,7 +656,8 @@ int llfe_init(int device, llfe_ctx **out) {
     llfe_ctx *c = new llfe_ctx();
     c->device = device;
     for (hipEvent_t *e : {&c->chunk_done[0], &c->chunk_done[1], &c->mask_done[0], &c->mask_done[1], &c->start_ev,
-                          &c->stream_done[0], &c->stream_done[1], &c->mask_ready[0], &c->mask_ready[1]})
+                          &c->stream_done[0], &c->stream_done[1], &c->mask_ready[0], &c->mask_ready[1],
+                          &c->input_ready, &c->colour_done, &c->front_done})
         if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) {
             llfe_destroy(c);
             return LLFE_ERR_HIP;
@@ -643,6 +669,7 @@ int llfe_init(int device, llfe_ctx **out) {
         }
     if (const char *ch = getenv("LLFE_CHUNK"); ch && atoi(ch) > 0) c->chunk = std::min(atoi(ch), kMaxKmeansBatch);
     if (const char *ns = getenv("LLFE_STREAMS"); ns && atoi(ns) == 2) c->nstreams = 2;
+    if (const char *sa = getenv("LLFE_SHAPES_AFTER_FRONT"); sa && atoi(sa) == 1) c->shapes_after_front = true;
     gauss_kernel_f32(11, c->sp.k11);
     c->pool = new Pool(default_threads() - 1);
     int nt = c->pool->size() + 1;
@@ -659,7 +686,8 @@ int llfe_destroy(llfe_ctx *ctx) {
     for (hipStream_t st : {ctx->streams[0], ctx->streams[1], ctx->copy_stream})
         if (st) (void)hipStreamSynchronize(st);
     for (hipEvent_t e : {ctx->chunk_done[0], ctx->chunk_done[1], ctx->mask_done[0], ctx->mask_done[1], ctx->start_ev,
-                         ctx->stream_done[0], ctx->stream_done[1], ctx->mask_ready[0], ctx->mask_ready[1]})
+                         ctx->stream_done[0], ctx->stream_done[1], ctx->mask_ready[0], ctx->mask_ready[1],
+                         ctx->input_ready, ctx->colour_done, ctx->front_done})
         if (e) (void)hipEventDestroy(e);
     for (hipStream_t st : {ctx->streams[0], ctx->streams[1], ctx->copy_stream})
         if (st) (void)hipStreamDestroy(st);
