@@ -189,6 +189,15 @@ def main():
     barrier()
     dt = shard.max_over_ranks(t1 - t0, device=f"cuda:{local}")
     stats = be.kernel_stats()
+    # one extra, untimed step with every kernel in order on one stream: isolated kernel
+    # durations for the secondary rooflines (in the timed steps the shapes kernels share
+    # the GPU with the colour front, which stretches their event-timed spans)
+    be.set_concurrency(False)
+    be.set_profiling(True)
+    be.process(imgs, feats, seed=args.seed, index_base=base)
+    torch.cuda.synchronize()
+    iso = be.kernel_stats()
+    be.set_concurrency(True)
     be.set_profiling(False)
 
     if rank != 0:
@@ -197,10 +206,10 @@ def main():
         return
 
     total_images = B * world * args.steps
-    def roof(name):
+    def roof(name, src=None):
         """HBM roofline of one kernel: algorithmic bytes per launch
         / its average hipEvent-timed launch duration."""
-        st = stats[name]
+        st = (src or stats)[name]
         avg_ms = st["total_ms"] / max(st["launches"], 1)
         bpl = st["bytes"] / max(st["launches"], 1)
         achieved = bpl / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
@@ -220,10 +229,17 @@ def main():
                          "share_of_step": round(st["total_ms"] / (dt * 1e3), 4),
                          "gbs": r["achieved"] if st["bytes"] else None, "frac": r["frac"] if st["bytes"] else None}
     # `roofline` is the dominant kernel's (largest total time); k_kmeans' algorithmic
-    # bytes are 4 U per full sweep over the unique-colour keys x the sweeps it made.
+    # bytes are 16 B per cube-table entry per pass (K k-means++ passes + one per Lloyd
+    # iteration, counted on the device) + 4 B per colour of the selection scans.
     dominant = max(stats, key=lambda k: stats[k]["total_ms"]) if stats else None
     roofline = roof(dominant) if dominant else None
-    roofline_stencil = roof("k_stencil") if "k_stencil" in stats else None
+    roofline_stencil = None
+    if "k_stencil" in iso:
+        roofline_stencil = roof("k_stencil", iso)
+        roofline_stencil["measured"] = "isolated step (all kernels on one stream), after the timed region"
+    for name, st in iso.items():
+        if name in kernels:
+            kernels[name]["isolated_ms"] = round(st["total_ms"] / max(st["launches"], 1), 4)
 
     cpu = None
     if args.cpu_baseline == "auto" and world == 1:

@@ -116,6 +116,9 @@ const char *llfe_last_error(llfe_ctx *ctx);
 int llfe_abi_version(void);
 /* enable (1) / disable (0) event timing; enabling resets the statistics */
 int llfe_set_profiling(llfe_ctx *ctx, int enable);
+/* llfe_process_batch runs the colour path on a second stream beside shapes / shadows
+ * (1, the default) or everything in order on one stream (0: isolated kernel timings) */
+int llfe_set_concurrency(llfe_ctx *ctx, int enable);
 /* copies up to cap entries, returns the number of kernels with statistics */
 int llfe_kernel_stats(llfe_ctx *ctx, llfe_kernel_stat *out, int32_t cap);
 

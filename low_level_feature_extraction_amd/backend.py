@@ -104,6 +104,11 @@ class Backend:
     def set_profiling(self, enable: bool):
         self._chk(self._lib.llfe_set_profiling(self.ctx, int(bool(enable))))
 
+    def set_concurrency(self, enable: bool):
+        """Colour path on a second stream beside shapes / shadows (default) or all kernels
+        in order on one stream (isolated kernel timings)."""
+        self._chk(self._lib.llfe_set_concurrency(self.ctx, int(bool(enable))))
+
     def kernel_stats(self) -> dict:
         """{kernel: {"launches", "total_ms", "bytes"}} accumulated while profiling."""
         arr = (L.LlfeKernelStat * 64)()

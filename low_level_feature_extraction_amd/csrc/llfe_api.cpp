@@ -335,6 +335,7 @@ struct llfe_ctx {
     hipEvent_t chunk_done[2] = {nullptr, nullptr};
     hipEvent_t input_ready = nullptr, colour_done = nullptr, front_done = nullptr;  // intra-chunk stream split
     bool shapes_after_front = false;  // LLFE_SHAPES_AFTER_FRONT=1: shapes wait for the colour front
+    bool concurrent = true;           // llfe_set_concurrency
     hipEvent_t mask_done[2] = {nullptr, nullptr};  // shapes/shadows results are on the host
     // the mask / shadow D2H runs on its own stream so the colour stage starts right after
     // the hysteresis kernels; mask_ready[slot] orders it after them, and a workspace is
@@ -517,7 +518,7 @@ int enqueue_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_
     // to share the GPU with k-means (LLFE_SHAPES_AFTER_FRONT=1) 12.8k -- the stencil
     // waves slow the k-means attempts more than they fill its tail.
     hipStream_t col_s = s;
-    if (want_col && ctx->nstreams == 1 && (want_shp || want_shd)) {
+    if (want_col && ctx->concurrent && ctx->nstreams == 1 && (want_shp || want_shd)) {
         col_s = ctx->streams[1];
         HIPCHK(ctx, hipEventRecord(ctx->input_ready, s));
         HIPCHK(ctx, hipStreamWaitEvent(col_s, ctx->input_ready, 0));
@@ -702,6 +703,12 @@ int llfe_set_profiling(llfe_ctx *ctx, int enable) {
     if (!ctx) return LLFE_ERR_INVALID;
     if (enable) ctx->prof.reset();
     ctx->prof.on = enable != 0;
+    return LLFE_OK;
+}
+
+int llfe_set_concurrency(llfe_ctx *ctx, int enable) {
+    if (!ctx) return LLFE_ERR_INVALID;
+    ctx->concurrent = enable != 0;
     return LLFE_OK;
 }
 
