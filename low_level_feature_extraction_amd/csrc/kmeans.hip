@@ -285,17 +285,16 @@ __device__ __forceinline__ uint32_t cube_origin_key(uint32_t id) {
 }
 
 // Boundary colours are packed densely into the wave's lanes before they are labelled:
-// the colours of cube (m, id) go to lanes [fill, fill + popc(m)) of pk (ds_permute
+// the colours of cube (m, origin key) go to lanes [fill, fill + popc(m)) of pk (ds_permute
 // push; lane b's rank among the set bits comes from mbcnt).  fill + popc(m) <= 64;
 // m and id are wave-uniform (SGPRs).
 __device__ __forceinline__ uint32_t lane_off_rel(int fill) { return (uint32_t)(__lane_id() - fill); }
-__device__ __forceinline__ void pack_cube(uint32_t &pk, int fill, unsigned long long m, uint32_t id,
-                                          uint32_t lane_off) {
+__device__ __forceinline__ void pack_key(uint32_t &pk, int fill, unsigned long long m, uint32_t okey,
+                                         uint32_t lane_off) {
     const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
     const int n = __popcll(m);
-    // lanes without a colour push into a lane outside [fill, fill + n) (ignored)
     const uint32_t dst = lane_sel(m, (uint32_t)fill + rank, fill > 0 ? 0u : 63u);
-    const uint32_t v = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst * 4u), (int)(cube_origin_key(id) | lane_off));
+    const uint32_t v = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst * 4u), (int)(okey | lane_off));
     const uint32_t rel = lane_off_rel(fill);
     pk = rel < (uint32_t)n ? v : pk;
 }
@@ -518,6 +517,7 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
         const uint32_t loff = lane_offset(lane);
         int fill = 0;
         auto flush_pk = [&]() {
+            fails += (unsigned long long)fill;
             if (lane < fill) {
                 const int x = unpack_r(pk), y = unpack_g(pk), z = unpack_b(pk);
                 const int D = dmin_chosen(x, y, z, ch, kk);
@@ -608,16 +608,20 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
                 // undecided cubes: their colours (enumerated from the occupancy mask)
                 // packed densely into the lanes, summed 64 at a time
                 unsigned long long fm = __ballot(mine && fail);
-                while (fm) {
-                    const int src = __builtin_ctzll(fm);
-                    fm &= fm - 1;
-                    const unsigned long long m = lane_mask(e, src);
-                    const uint32_t id = __builtin_amdgcn_readlane(e.id, src);
-                    const int n = __popcll(m);
-                    if (fill + n > 64) flush_pk();
-                    pack_cube(pk, fill, m, id, loff);
-                    fill += n;
-                    fails += (unsigned long long)n;
+                if (fm) {
+                    const uint32_t okey = cube_origin_key(e.id);  // read back per cube below
+                    const uint32_t mlo = (uint32_t)e.mask, mhi = (uint32_t)(e.mask >> 32);
+                    while (fm) {
+                        const int src = __builtin_ctzll(fm);
+                        fm &= fm - 1;
+                        const unsigned long long m =
+                            ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(mhi, src) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane(mlo, src);
+                        const int n = __popcll(m);
+                        if (fill + n > 64) flush_pk();
+                        pack_key(pk, fill, m, (uint32_t)__builtin_amdgcn_readlane(okey, src), loff);
+                        fill += n;
+                    }
                 }
                 const unsigned long long rest = __ballot(P > Pseg && P < kParts);
                 if (!rest) break;

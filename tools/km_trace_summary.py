@@ -3,7 +3,7 @@
 per-phase times for the "photo" (U > 300k) and "ui" classes, Lloyd time per iteration,
 Lloyd bytes per iteration relative to a plain sweep, and the kernel span / CU balance.
 
-    python tools/km_trace_summary.py gpurun_out/km_trace.txt [launch_index]
+    python tools/km_trace_summary.py gpurun_out/km_trace.txt [launch_index] [attempts_per_launch]
 """
 import sys
 
@@ -14,7 +14,8 @@ def main():
     path = sys.argv[1]
     launch = int(sys.argv[2]) if len(sys.argv) > 2 else -1
     a = np.loadtxt(path, dtype=np.int64)
-    n_att = 2560 if len(a) >= 2560 else len(a)
+    n_att = int(sys.argv[3]) if len(sys.argv) > 3 else 5120  # attempts per launch (10 x images per pass)
+    n_att = n_att if len(a) >= n_att else len(a)
     nl = len(a) // n_att
     a = a[(launch % nl) * n_att:(launch % nl + 1) * n_att]
     img, att, U, it, t0, t1, hw, xcc, tpp, tll, by = a.T[:11]
