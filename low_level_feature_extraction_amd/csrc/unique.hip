@@ -289,9 +289,21 @@ __global__ __launch_bounds__(UT) void k_uq_part(const uint32_t *__restrict__ par
         return;
     }
     const uint32_t *in = part + (size_t)img * key_stride + start;
-    for (uint32_t i = t; i < count; i += UT) {
-        const uint32_t k = in[i];
-        atomicOr(&W[((k >> 16) & 3u) * 2048 + ((k >> 5) & 2047u)], 1u << (k & 31u));
+    // 8 independent (coalesced) key loads in flight per thread before their LDS atomics:
+    // one load per atomic in sequence left the workgroup waiting on HBM latency
+    constexpr int KB8 = 8;
+    for (uint32_t base = 0; base < count; base += UT * KB8) {
+        uint32_t kk[KB8];
+#pragma unroll
+        for (int j = 0; j < KB8; j++) {
+            const uint32_t i = base + (uint32_t)j * UT + t;
+            kk[j] = i < count ? in[i] : 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (int j = 0; j < KB8; j++) {
+            const uint32_t k = kk[j];
+            if (k != 0xFFFFFFFFu) atomicOr(&W[((k >> 16) & 3u) * 2048 + ((k >> 5) & 2047u)], 1u << (k & 31u));
+        }
     }
     __syncthreads();
     // (a) unique keys in ascending order: thread t owns words 8t .. 8t + 7
