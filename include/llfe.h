@@ -133,6 +133,18 @@ int llfe_process_batch(llfe_ctx *ctx, const llfe_batch *batch, uint32_t features
                        llfe_image_result *results, llfe_shape *shapes, int64_t shape_capacity,
                        int64_t *shapes_needed, llfe_stream stream);
 
+/* Asynchronous form (serving loops): llfe_submit_batch enqueues the device work of one
+ * batch (n <= one device pass) and returns a ticket; llfe_collect_batch (tickets in
+ * submission order) waits for it, traces contours and fills results / shapes exactly as
+ * llfe_process_batch would.  At most two batches are in flight; batch k + 1 runs on the
+ * second workspace, so its kernels start in the tail of batch k's k-means.  The input
+ * (and parity noise) must stay valid until the ticket is collected.  On
+ * LLFE_ERR_CAPACITY the ticket stays collectable with a larger shapes buffer. */
+int llfe_submit_batch(llfe_ctx *ctx, const llfe_batch *batch, uint32_t features, uint64_t seed, llfe_stream stream,
+                      int64_t *ticket);
+int llfe_collect_batch(llfe_ctx *ctx, int64_t ticket, llfe_image_result *results, llfe_shape *shapes,
+                       int64_t shape_capacity, int64_t *shapes_needed);
+
 /* ---- stage entry points (parity tests; device in/out unless noted) ------ */
 /* gray = cvtColor(BGR2GRAY); out = GaussianBlur(gray, (5,5), 0)
  * (shape pyc @L18-21, shadow pyc @L8-9) */

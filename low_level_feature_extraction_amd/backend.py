@@ -180,6 +180,12 @@ class Backend:
                     continue
                 self._chk(rc)
                 break
+        out = self._convert(results, shapes, n, mask, w, h)
+        del keep, nkeep
+        return out
+
+    @staticmethod
+    def _convert(results, shapes, n, mask, w, h) -> list:
         # bulk conversion through numpy views of the ctypes arrays (per-field ctypes
         # access would cost ~20 us per image while the GPU waits for the next batch)
         R = np.ctypeslib.as_array(results)[:n]
@@ -200,8 +206,43 @@ class Backend:
                                                        S["border_radius"].tolist(), S["area"].tolist())]
         out = [ImageFeatures(cen[i, :ncol[i]], cnt[i, :ncol[i]], nu[i], comp[i], ssum[i], scnt[i],
                              recs[off[i]:off[i] + nsh[i]] if recs else [], ncont[i], w, h) for i in range(n)]
-        del keep, nkeep
         return out
+
+    # ------------------------------------------------------------------ async batches
+    def submit(self, images, features=("colors", "shapes", "shadows"), seed: int = 0, noise=None,
+               index_base: int = 0, n_colors: int = 5) -> int:
+        """Enqueue one batch (llfe_submit_batch) and return its ticket; at most two in
+        flight.  Results: ``collect(ticket)``, in submission order."""
+        ptr, n, h, w, on_dev, keep = self._batch_view(images)
+        nptr, n_on_dev, nkeep = self._noise_view(noise, n, h, w)
+        mask = feature_mask(features)
+        b = L.LlfeBatch(C.c_void_p(ptr), n, h, w, on_dev, C.c_void_p(nptr) if nptr else None, n_on_dev,
+                        int(n_colors), index_base)
+        ticket = C.c_int64(0)
+        with self._lock:
+            self._chk(self._lib.llfe_submit_batch(self.ctx, C.byref(b), mask, C.c_uint64(seed & (2**64 - 1)),
+                                                  self._stream(keep), C.byref(ticket)))
+        if not hasattr(self, "_inflight"):
+            self._inflight = {}
+        self._inflight[ticket.value] = (n, h, w, mask, keep, nkeep, b)  # inputs stay alive
+        return ticket.value
+
+    def collect(self, ticket: int) -> list:
+        n, h, w, mask, keep, nkeep, b = self._inflight[ticket]
+        results = (L.LlfeImageResult * max(n, 1))()
+        cap = max(64 * n, 64)
+        needed = C.c_int64(0)
+        with self._lock:
+            while True:
+                shapes = (L.LlfeShape * cap)()
+                rc = self._lib.llfe_collect_batch(self.ctx, C.c_int64(ticket), results, shapes, cap, C.byref(needed))
+                if rc == L.LLFE_ERR_CAPACITY and needed.value > cap:
+                    cap = int(needed.value)
+                    continue
+                self._chk(rc)
+                break
+        del self._inflight[ticket]
+        return self._convert(results, shapes, n, mask, w, h)
 
     # ------------------------------------------------------------------ stages (device tensors)
     def _dev_batch(self, images):

@@ -217,7 +217,7 @@ struct Work {
 // hipEvent pairs around launches (enabled by llfe_set_profiling)
 struct Profiler {
     struct Rec {
-        int kid;
+        int kid, slot;
         hipEvent_t a, b;
         double bytes;
     };
@@ -227,17 +227,20 @@ struct Profiler {
         double ms = 0, bytes = 0;
     };
     bool on = false;
-    std::vector<hipEvent_t> pool;
-    size_t used = 0;
+    int cur_slot = 0;  // slot of the work being enqueued (records are collected per slot)
+    std::vector<hipEvent_t> all, free_;
     std::vector<Rec> pending;
     std::vector<Stat> stats;
     hipEvent_t ev() {
-        if (used == pool.size()) {
+        if (free_.empty()) {
             hipEvent_t e;
             if (hipEventCreate(&e) != hipSuccess) return nullptr;
-            pool.push_back(e);
+            all.push_back(e);
+            return e;
         }
-        return pool[used++];
+        hipEvent_t e = free_.back();
+        free_.pop_back();
+        return e;
     }
     int kid(const char *name) {
         for (size_t i = 0; i < stats.size(); i++)
@@ -254,34 +257,47 @@ struct Profiler {
     void end(hipEvent_t a, hipStream_t s, const char *name, double bytes) {
         if (!on || !a) return;
         hipEvent_t b = ev();
-        if (!b) return;
+        if (!b) {
+            free_.push_back(a);
+            return;
+        }
         (void)hipEventRecord(b, s);
-        pending.push_back(Rec{kid(name), a, b, bytes});
+        pending.push_back(Rec{kid(name), cur_slot, a, b, bytes});
     }
-    // call after the stream has been synchronised
-    void collect() {
-        for (auto &r : pending) {
+    // call after the slot's (slot < 0: every) stream work has completed
+    void collect(int slot = -1) {
+        size_t keep = 0;
+        for (size_t i = 0; i < pending.size(); i++) {
+            Rec &r = pending[i];
+            if (slot >= 0 && r.slot != slot) {
+                pending[keep++] = r;
+                continue;
+            }
             float ms = 0.f;
             if (hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
                 stats[r.kid].launches++;
                 stats[r.kid].ms += ms;
                 stats[r.kid].bytes += r.bytes;
             }
+            free_.push_back(r.a);
+            free_.push_back(r.b);
         }
-        pending.clear();
-        used = 0;
+        pending.resize(keep);
     }
     // bytes known only after the launch completed (k-means sweeps)
     void add_bytes(const char *name, double bytes) {
         if (on) stats[kid(name)].bytes += bytes;
     }
     void reset() {
+        for (auto &r : pending) {
+            free_.push_back(r.a);
+            free_.push_back(r.b);
+        }
         pending.clear();
-        used = 0;
         stats.clear();
     }
     ~Profiler() {
-        for (auto e : pool) (void)hipEventDestroy(e);
+        for (auto e : all) (void)hipEventDestroy(e);
     }
 };
 
@@ -324,7 +340,18 @@ struct llfe_ctx {
     Work ws[2];
     int nstreams = 1;
     hipStream_t streams[2] = {nullptr, nullptr};
+    hipStream_t col_streams[2] = {nullptr, nullptr};  // colour path of workspace q
     hipEvent_t start_ev = nullptr, stream_done[2] = {nullptr, nullptr};
+    // asynchronous submissions (llfe_submit_batch / llfe_collect_batch): slot = ticket & 1
+    struct Pending {
+        bool busy = false, done = false;
+        llfe_batch b{};
+        uint32_t features = 0;
+        std::vector<llfe_image_result> res;
+        std::vector<llfe_shape> shp;
+    };
+    Pending inflight[2];
+    int64_t next_ticket = 0, next_collect = 0;
     DevBuf<uint8_t> d_rsz_tmp, d_rsz_src;
     DevBuf<int32_t> d_coef;
     // pinned host staging; the per-chunk results are double-buffered so the host can
@@ -499,8 +526,9 @@ bool valid_dims(int n, int h, int w) { return n >= 0 && h > 0 && w > 0 && (int64
 // Device half of one chunk, on slot `slot`'s stream and workspace: every kernel, then
 // the D2H of the per-image results into host slot `slot`, with events the host half
 // waits on.
-int enqueue_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_t seed, int i0, int n, int slot) {
-    const int q = ctx->nstreams > 1 ? slot : 0;
+int enqueue_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_t seed, int i0, int n, int slot,
+                  int q) {
+    ctx->prof.cur_slot = slot;
     Work &W = ctx->ws[q];
     hipStream_t s = ctx->streams[q];
     const int h = b->height, w = b->width, wpr = words_per_row(w);
@@ -519,7 +547,7 @@ int enqueue_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_
     // waves slow the k-means attempts more than they fill its tail.
     hipStream_t col_s = s;
     if (want_col && ctx->concurrent && ctx->nstreams == 1 && (want_shp || want_shd)) {
-        col_s = ctx->streams[1];
+        col_s = ctx->col_streams[q];
         HIPCHK(ctx, hipEventRecord(ctx->input_ready, s));
         HIPCHK(ctx, hipStreamWaitEvent(col_s, ctx->input_ready, 0));
     }
@@ -663,7 +691,7 @@ int llfe_init(int device, llfe_ctx **out) {
             llfe_destroy(c);
             return LLFE_ERR_HIP;
         }
-    for (hipStream_t *st : {&c->streams[0], &c->streams[1], &c->copy_stream})
+    for (hipStream_t *st : {&c->streams[0], &c->streams[1], &c->col_streams[0], &c->col_streams[1], &c->copy_stream})
         if (hipStreamCreateWithFlags(st, hipStreamNonBlocking) != hipSuccess) {
             llfe_destroy(c);
             return LLFE_ERR_HIP;
@@ -684,13 +712,13 @@ int llfe_init(int device, llfe_ctx **out) {
 int llfe_destroy(llfe_ctx *ctx) {
     if (!ctx) return LLFE_OK;
     (void)hipSetDevice(ctx->device);
-    for (hipStream_t st : {ctx->streams[0], ctx->streams[1], ctx->copy_stream})
+    for (hipStream_t st : {ctx->streams[0], ctx->streams[1], ctx->col_streams[0], ctx->col_streams[1], ctx->copy_stream})
         if (st) (void)hipStreamSynchronize(st);
     for (hipEvent_t e : {ctx->chunk_done[0], ctx->chunk_done[1], ctx->mask_done[0], ctx->mask_done[1], ctx->start_ev,
                          ctx->stream_done[0], ctx->stream_done[1], ctx->mask_ready[0], ctx->mask_ready[1],
                          ctx->input_ready, ctx->colour_done, ctx->front_done})
         if (e) (void)hipEventDestroy(e);
-    for (hipStream_t st : {ctx->streams[0], ctx->streams[1], ctx->copy_stream})
+    for (hipStream_t st : {ctx->streams[0], ctx->streams[1], ctx->col_streams[0], ctx->col_streams[1], ctx->copy_stream})
         if (st) (void)hipStreamDestroy(st);
     delete ctx->pool;
     delete ctx;  // DevBuf / HostBuf members free themselves
@@ -734,6 +762,8 @@ int llfe_process_batch(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, ui
         return ctx->fail(LLFE_ERR_INVALID, "invalid batch n=%d h=%d w=%d", b->n, b->height, b->width);
     if (b->n_colors < 0 || b->n_colors > kMaxK)
         return ctx->fail(LLFE_ERR_UNSUPPORTED, "n_colors=%d outside [1, %d]", b->n_colors, kMaxK);
+    if (ctx->inflight[0].busy || ctx->inflight[1].busy)
+        return ctx->fail(LLFE_ERR_INVALID, "llfe_process_batch with submitted batches not yet collected");
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t s = (hipStream_t)stream;
     const bool want_shp = features & LLFE_FEATURE_SHAPES;
@@ -748,7 +778,7 @@ int llfe_process_batch(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, ui
     const int chunk = chunk_for(ctx->chunk, b->height, b->width);
     for (int i0 = 0; i0 < b->n; i0 += chunk) {
         const int n = std::min(chunk, b->n - i0);
-        int rc = enqueue_chunk(ctx, b, features, seed, i0, n, slot);
+        int rc = enqueue_chunk(ctx, b, features, seed, i0, n, slot, ctx->nstreams > 1 ? slot : 0);
         if (rc) return rc;
         if (prev_i0 >= 0) {
             rc = finish_chunk(ctx, b, features, prev_i0, prev_n, slot ^ 1, results, shapes, shape_capacity, total_shapes);
@@ -772,6 +802,75 @@ int llfe_process_batch(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, ui
     if (want_shp && total_shapes > shape_capacity)
         return ctx->fail(LLFE_ERR_CAPACITY, "shape capacity %lld < %lld", (long long)shape_capacity,
                          (long long)total_shapes);
+    return LLFE_OK;
+}
+
+// Asynchronous form of llfe_process_batch: up to two batches in flight, each on its own
+// workspace and stream pair, so batch k + 1's unique-colour and stencil kernels start in
+// the tail of batch k's k-means launch (where most CUs are idle) instead of after it.
+int llfe_submit_batch(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_t seed, llfe_stream stream,
+                      int64_t *ticket) {
+    if (!ctx || !b || !ticket) return LLFE_ERR_INVALID;
+    if (!valid_dims(b->n, b->height, b->width) || (b->n > 0 && !b->data))
+        return ctx->fail(LLFE_ERR_INVALID, "invalid batch n=%d h=%d w=%d", b->n, b->height, b->width);
+    if (b->n_colors < 0 || b->n_colors > kMaxK)
+        return ctx->fail(LLFE_ERR_UNSUPPORTED, "n_colors=%d outside [1, %d]", b->n_colors, kMaxK);
+    if (b->n > chunk_for(ctx->chunk, b->height, b->width))
+        return ctx->fail(LLFE_ERR_UNSUPPORTED, "llfe_submit_batch: n=%d exceeds one device pass (%d)", b->n,
+                         chunk_for(ctx->chunk, b->height, b->width));
+    const int slot = (int)(ctx->next_ticket & 1);
+    auto &pd = ctx->inflight[slot];
+    if (pd.busy) return ctx->fail(LLFE_ERR_CAPACITY, "two batches already in flight: collect one first");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(ctx, hipEventRecord(ctx->start_ev, s));
+    HIPCHK(ctx, hipStreamWaitEvent(ctx->streams[slot], ctx->start_ev, 0));
+    if (b->n > 0) {
+        int rc = enqueue_chunk(ctx, b, features, seed, 0, b->n, slot, slot);
+        if (rc) return rc;
+    }
+    pd.busy = true;
+    pd.done = false;
+    pd.b = *b;
+    pd.features = features;
+    *ticket = ctx->next_ticket++;
+    return LLFE_OK;
+}
+
+int llfe_collect_batch(llfe_ctx *ctx, int64_t ticket, llfe_image_result *results, llfe_shape *shapes,
+                       int64_t shape_capacity, int64_t *shapes_needed) {
+    if (!ctx || !results) return LLFE_ERR_INVALID;
+    if (ticket != ctx->next_collect) return ctx->fail(LLFE_ERR_INVALID, "collect tickets in submission order");
+    const int slot = (int)(ticket & 1);
+    auto &pd = ctx->inflight[slot];
+    if (!pd.busy) return ctx->fail(LLFE_ERR_INVALID, "ticket %lld was not submitted", (long long)ticket);
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    const int n = pd.b.n;
+    if (!pd.done) {  // host half once; a retry after LLFE_ERR_CAPACITY only copies
+        pd.res.assign((size_t)n, llfe_image_result{});
+        int64_t total = 0;
+        if (n > 0) {
+            int rc = finish_chunk(ctx, &pd.b, pd.features, 0, n, slot, pd.res.data(), nullptr, 0, total);
+            if (rc) return rc;
+        }
+        pd.shp.clear();
+        if (pd.features & LLFE_FEATURE_SHAPES) {
+            pd.shp.reserve((size_t)total);
+            // finish_chunk left the per-image shapes in ctx->img_shapes
+            for (int i = 0; i < n; i++)
+                pd.shp.insert(pd.shp.end(), ctx->img_shapes[i].begin(), ctx->img_shapes[i].end());
+        }
+        ctx->prof.collect(slot);
+        pd.done = true;
+    }
+    const int64_t total = (int64_t)pd.shp.size();
+    if (shapes_needed) *shapes_needed = total;
+    std::memcpy(results, pd.res.data(), sizeof(llfe_image_result) * (size_t)n);
+    if (shapes) std::memcpy(shapes, pd.shp.data(), sizeof(llfe_shape) * (size_t)std::min(total, shape_capacity));
+    if (total > shape_capacity)
+        return ctx->fail(LLFE_ERR_CAPACITY, "shape capacity %lld < %lld", (long long)shape_capacity, (long long)total);
+    pd.busy = false;
+    ctx->next_collect++;
     return LLFE_OK;
 }
 

@@ -82,6 +82,43 @@ def test_results_independent_of_batching(backend):
     assert all(np.array_equal(p.centers_rgb, q.centers_rgb) for p, q in zip(a, again))
 
 
+def _same(a, b):
+    for ra, rb in zip(a, b):
+        assert np.array_equal(ra.centers_rgb, rb.centers_rgb) and np.array_equal(ra.counts, rb.counts)
+        assert ra.n_unique == rb.n_unique and ra.compactness == rb.compactness
+        assert ra.shapes == rb.shapes and (ra.shadow_sum, ra.shadow_count) == (rb.shadow_sum, rb.shadow_count)
+    assert len(a) == len(b)
+
+
+def test_submit_collect_matches_process(backend):
+    """llfe_submit_batch / llfe_collect_batch (two batches in flight) == llfe_process_batch."""
+    import torch
+
+    feats = ("colors", "shapes", "shadows")
+    x = _batch(5, 150, 260, seed=31)
+    y = _batch(3, 97, 131, seed=32)
+    xd = torch.from_numpy(x).cuda()
+    ref_x = backend.process(x, feats, seed=7, index_base=100)
+    ref_y = backend.process(y, feats, seed=8, index_base=200)
+    t1 = backend.submit(xd, feats, seed=7, index_base=100)   # device input
+    t2 = backend.submit(y, feats, seed=8, index_base=200)    # host input, different size
+    _same(backend.collect(t1), ref_x)
+    t3 = backend.submit(x, ("shapes",), seed=7, index_base=100)
+    _same(backend.collect(t2), ref_y)
+    got3 = backend.collect(t3)
+    assert [r.shapes for r in got3] == [r.shapes for r in ref_x]
+    # a third submission before collecting is refused, and order is enforced
+    ta = backend.submit(x, feats, seed=7, index_base=100)
+    tb = backend.submit(x, feats, seed=7, index_base=100)
+    with pytest.raises(Exception):
+        backend.submit(x, feats, seed=7, index_base=100)
+    with pytest.raises(Exception):
+        backend.collect(tb)
+    _same(backend.collect(ta), ref_x)
+    _same(backend.collect(tb), ref_x)
+    _same(backend.process(x, feats, seed=7, index_base=100), ref_x)  # sync path still fine
+
+
 def test_many_shapes_capacity_retry(backend, orc):
     x = np.zeros((1, 540, 960, 3), np.uint8)
     for y in range(6, 530, 24):  # a grid of separated 12 x 12 squares -> ~880 shapes
