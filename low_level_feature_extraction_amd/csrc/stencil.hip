@@ -192,20 +192,31 @@ __device__ void stencil_tile(FastSmem &sm, const uint8_t *__restrict__ src, int 
                 bv[r][4] = (int)byte_of(b2, 0);
                 bv[r][5] = (int)byte_of(b2, 1);
             }
+            int gx[4], gy[4], m[4];
+            bool need = false;  // the direction class matters only where m > LOW (stage 5)
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                gx[j] = (bv[0][j + 2] + 2 * bv[1][j + 2] + bv[2][j + 2]) - (bv[0][j] + 2 * bv[1][j] + bv[2][j]);
+                gy[j] = (bv[2][j] + 2 * bv[2][j + 1] + bv[2][j + 2]) - (bv[0][j] + 2 * bv[0][j + 1] + bv[0][j + 2]);
+                m[j] = abs(gx[j]) + abs(gy[j]);
+                need = need || m[j] > 50;
+            }
+            int dir[4] = {0, 0, 0, 0};
+            if (need) {  // whole waves of flat / noise-only pixels skip the direction math
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int ax = abs(gx[j]), ay = abs(gy[j]) << 15, tg22x = ax * TG22;
+                    if (ay < tg22x) dir[j] = 0;
+                    else if (ay > tg22x + (ax << 16)) dir[j] = 1;
+                    else dir[j] = (gx[j] ^ gy[j]) < 0 ? 2 : 3;
+                }
+            }
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const int mc = 4 * q + j;
                 if (mc >= FMW) break;
-                const int gx = (bv[0][j + 2] + 2 * bv[1][j + 2] + bv[2][j + 2]) - (bv[0][j] + 2 * bv[1][j] + bv[2][j]);
-                const int gy = (bv[2][j] + 2 * bv[2][j + 1] + bv[2][j + 2]) - (bv[0][j] + 2 * bv[0][j + 1] + bv[0][j + 2]);
-                const int m = abs(gx) + abs(gy);
-                const int ax = abs(gx), ay = abs(gy) << 15, tg22x = ax * TG22;
-                int dir;
-                if (ay < tg22x) dir = 0;
-                else if (ay > tg22x + (ax << 16)) dir = 1;
-                else dir = (gx ^ gy) < 0 ? 2 : 3;
                 const bool out = BORDER && ((unsigned)(ty0 - 1 + my) >= (unsigned)H || (unsigned)(tx0 - 1 + mc) >= (unsigned)W);
-                sm.md[my][mc] = out ? (uint16_t)0 : (uint16_t)(m | (dir << 12));  // Canny: no magnitude outside
+                sm.md[my][mc] = out ? (uint16_t)0 : (uint16_t)(m[j] | (dir[j] << 12));  // Canny: no magnitude outside
             }
         }
         __syncthreads();
@@ -213,11 +224,19 @@ __device__ void stencil_tile(FastSmem &sm, const uint8_t *__restrict__ src, int 
         constexpr int LOW = 50, HIGH = 150;
         for (int u = tid; u < TH * (TW / 4); u += NT) {
             const int ty = u / (TW / 4), q = u - ty * (TW / 4);
-            uint32_t o = 0;
+            uint32_t o = 0x01010101u;  // class 1 (not an edge) unless m > LOW
+            int mv[4];
+            bool any = false;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                mv[j] = sm.md[ty + 1][4 * q + j + 1];
+                any = any || (mv[j] & 4095) > LOW;
+            }
+            if (any)
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const int tx = 4 * q + j;
-                const int v = sm.md[ty + 1][tx + 1];
+                const int v = mv[j];
                 const int m = v & 4095, dir = v >> 12;
                 uint32_t c = 1;
                 if (m > LOW) {
@@ -232,7 +251,7 @@ __device__ void stencil_tile(FastSmem &sm, const uint8_t *__restrict__ src, int 
                     }
                     if (keep) c = m > HIGH ? 2u : 0u;
                 }
-                o |= c << (8 * j);
+                o = (o & ~(255u << (8 * j))) | (c << (8 * j));
             }
             if (BORDER) {
                 const int Y = ty0 + ty, X = tx0 + 4 * q;
