@@ -131,7 +131,11 @@ __device__ __forceinline__ int label5p(uint32_t key, const CentP &c) {
 }
 
 constexpr int PF = 4;  // steps of 16-B key loads kept in flight per wave
-constexpr int kStage = 256;  // per-wave LDS ring of boundary colours awaiting labelling
+#ifndef LLFE_KM_UNROLL
+#define LLFE_KM_UNROLL 4
+#endif
+// per-wave LDS ring of boundary colours awaiting labelling (>= 64 + 64 x unroll)
+constexpr int kStage = LLFE_KM_UNROLL <= 2 ? 256 : 512;
 
 // the 4 keys of lane `lane` in 256-point step `s` (zeros past the full steps)
 __device__ __forceinline__ uint4 load_step(const uint32_t *pts, int s, int se_full, int lane) {
@@ -1083,30 +1087,25 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
                 // readlane instead of rebuilding it in scalar code)
                 const uint32_t okey = cube_origin_key(e.id);
                 const uint32_t mlo = (uint32_t)e.mask, mhi = (uint32_t)(e.mask >> 32);
-                // two failing cubes per trip: independent readlane / mbcnt chains interleave,
-                // and the ring (kStage = 256) holds <= 63 pending + 2 x 64 new colours
+                // LLFE_KM_UNROLL failing cubes per trip: independent readlane / mbcnt chains
+                // interleave; the ring (kStage) holds <= 63 pending + UNROLL x 64 new colours
+                auto push = [&](int src) {
+                    const unsigned long long m =
+                        ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(mhi, src) << 32) |
+                        (uint32_t)__builtin_amdgcn_readlane(mlo, src);
+                    const uint32_t k = __builtin_amdgcn_readlane(okey, src);
+                    const uint32_t r =
+                        __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    stg[lane_sel(m, ((uint32_t)head + r) & (kStage - 1), kStage + lane)] = k | loff;
+                    head += __popcll(m);
+                };
                 while (fm) {
-                    const int s1 = __builtin_ctzll(fm);
-                    fm &= fm - 1;
-                    const unsigned long long m1 =
-                        ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(mhi, s1) << 32) |
-                        (uint32_t)__builtin_amdgcn_readlane(mlo, s1);
-                    const uint32_t k1 = __builtin_amdgcn_readlane(okey, s1);
-                    const uint32_t r1 =
-                        __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
-                    stg[lane_sel(m1, ((uint32_t)head + r1) & (kStage - 1), kStage + lane)] = k1 | loff;
-                    head += __popcll(m1);
-                    if (fm) {
-                        const int s2 = __builtin_ctzll(fm);
+#pragma unroll
+                    for (int u = 0; u < LLFE_KM_UNROLL; u++) {
+                        if (u > 0 && !fm) break;
+                        const int src = __builtin_ctzll(fm);
                         fm &= fm - 1;
-                        const unsigned long long m2 =
-                            ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(mhi, s2) << 32) |
-                            (uint32_t)__builtin_amdgcn_readlane(mlo, s2);
-                        const uint32_t k2 = __builtin_amdgcn_readlane(okey, s2);
-                        const uint32_t r2 = __builtin_amdgcn_mbcnt_hi((uint32_t)(m2 >> 32),
-                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)m2, 0u));
-                        stg[lane_sel(m2, ((uint32_t)head + r2) & (kStage - 1), kStage + lane)] = k2 | loff;
-                        head += __popcll(m2);
+                        push(src);
                     }
                     while (head - tail >= 64) label_stage(64);
                 }
