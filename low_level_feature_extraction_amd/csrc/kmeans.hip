@@ -184,6 +184,7 @@ struct KmSmem {
     unsigned long long wchunk[3][KW];    // per trial: sum of D over each wave's chunk
     uint32_t stage[KW][kStage + 64];     // per-wave ring of boundary colours (+ a dummy row)
     unsigned long long qtot;             // sum of |p|^2 over all colours (exact)
+    int marg[kMaxK * kMaxK + 6 * kMaxK]; // k-means++ corner margins: centre pairs, trial vs centre (+/-)
 };
 
 __device__ __forceinline__ Cent load_centres(const float (*c)[3]) {
@@ -507,9 +508,9 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
 #pragma unroll
             for (int j = 0; j < 3; j++) {
                 const uint32_t k = pts[sm.pj[j]];
-                tx[j] = unpack_r(k);
-                ty[j] = unpack_g(k);
-                tz[j] = unpack_b(k);
+                tx[j] = __builtin_amdgcn_readfirstlane(unpack_r(k));
+                ty[j] = __builtin_amdgcn_readfirstlane(unpack_g(k));
+                tz[j] = __builtin_amdgcn_readfirstlane(unpack_b(k));
             }
         }
         // ---- trial sums T_j = sum min(D, d(., t_j)) per partition (kk == 0: sum d(., c0))
@@ -531,6 +532,37 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
             }
             fill = 0;
         };
+        // Round constants (wave-uniform).  Every test below is linear in the cube origin o:
+        // with D_c(o) = |c|^2 - 2 o.c, d(o, c) = |o|^2 + D_c(o), so
+        //   d(o, a) - d(o, b) = D_a(o) - D_b(o)          (never / always closer tests)
+        //   sum over the cube |p - c|^2 = n (|o|^2 + D_c(o)) + 2 (o - c).S_u + S_u2
+        // and the corner margins 6 sum max(+-(a - b), 0) depend on the centres only.
+        // The pairwise corner margins live in LDS (per-lane reads indexed by the lane's
+        // owner k); the per-centre constants stay in scalar registers.
+        int C2[kMaxK], S3[kMaxK], T2[3];
+#pragma unroll
+        for (int m = 0; m < kMaxK; m++) {
+            C2[m] = ch.x[m] * ch.x[m] + ch.y[m] * ch.y[m] + ch.z[m] * ch.z[m];
+            S3[m] = 3 * (ch.x[m] + ch.y[m] + ch.z[m]);
+        }
+#pragma unroll
+        for (int j = 0; j < 3; j++) T2[j] = tx[j] * tx[j] + ty[j] * ty[j] + tz[j] * tz[j];
+        if (tid < kMaxK * kMaxK) {  // Mkk[m][k] = 6 sum max(c_m - c_k, 0)
+            const int m = tid / kMaxK, k2 = tid % kMaxK;
+            sm.marg[tid] = 6 * (max(sm.icc[m][0] - sm.icc[k2][0], 0) + max(sm.icc[m][1] - sm.icc[k2][1], 0) +
+                                max(sm.icc[m][2] - sm.icc[k2][2], 0));
+        } else if (tid < kMaxK * kMaxK + 6 * kMaxK) {  // NA[j][k], NB[j][k]
+            const int q = tid - kMaxK * kMaxK, j = (q / kMaxK) % 3, k2 = q % kMaxK;
+            const int t[3] = {j == 0 ? tx[0] : (j == 1 ? tx[1] : tx[2]), j == 0 ? ty[0] : (j == 1 ? ty[1] : ty[2]),
+                              j == 0 ? tz[0] : (j == 1 ? tz[1] : tz[2])};
+            const int sg = q < 3 * kMaxK ? 1 : -1;  // NA: t - c_k ; NB: c_k - t
+            int acc = 0;
+#pragma unroll
+            for (int d = 0; d < 3; d++) acc += max(sg * (t[d] - sm.icc[k2][d]), 0);
+            sm.marg[tid] = 6 * acc;
+        }
+        __syncthreads();
+        const int *Mkk = sm.marg, *NA = sm.marg + kMaxK * kMaxK, *NB = sm.marg + kMaxK * kMaxK + 3 * kMaxK;
         CubeRing ring;
         ring.init(ctab, cb, cend, lane);
         for (int base = cb; base < cend; base += 64) {
@@ -546,40 +578,57 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
                     v0 = cube_sum(g, tx[0], ty[0], tz[0]);
                     qacc += cube_sum(g, 0, 0, 0);
                 } else {
-                    // owner candidate: nearest chosen centre to the cube centre o + 1.5
-                    const int qx = 2 * g.ox + 3, qy = 2 * g.oy + 3, qz = 2 * g.oz + 3;
-                    int k = 0, bd = d2i(qx, qy, qz, 2 * ch.x[0], 2 * ch.y[0], 2 * ch.z[0]);
+                    // owner candidate: nearest chosen centre to the cube centre q = o + 1.5:
+                    // argmin_m |q - c_m|^2 = argmin_m (D_m(o) - 3 sum(c_m)), first minimum
+                    int Dc[kMaxK];
+#pragma unroll
+                    for (int m = 0; m < kMaxK; m++)
+                        Dc[m] = C2[m] - 2 * (__mul24(g.ox, ch.x[m]) + __mul24(g.oy, ch.y[m]) + __mul24(g.oz, ch.z[m]));
+                    int k = 0, bd = Dc[0] - S3[0];
 #pragma unroll
                     for (int m = 1; m < kMaxK; m++) {
                         if (m >= kk) break;
-                        const int d = d2i(qx, qy, qz, 2 * ch.x[m], 2 * ch.y[m], 2 * ch.z[m]);
+                        const int d = Dc[m] - S3[m];
                         if (d < bd) {
                             bd = d;
                             k = m;
                         }
                     }
-                    int kx = ch.x[0], ky = ch.y[0], kz = ch.z[0];
+                    // owner k's values (per-lane selects from the uniform tables)
+                    int Dk = Dc[0], kx = ch.x[0], ky = ch.y[0], kz = ch.z[0];
 #pragma unroll
                     for (int m = 1; m < kMaxK; m++) {
+                        if (m >= kk) break;
+                        Dk = k == m ? Dc[m] : Dk;
                         kx = k == m ? ch.x[m] : kx;
                         ky = k == m ? ch.y[m] : ky;
                         kz = k == m ? ch.z[m] : kz;
                     }
+                    auto selk = [&](const int *row) { return row[k]; };  // LDS read, per-lane k
+                    // owned: no other chosen centre is ever strictly closer on the cube
                     bool owned = true;
 #pragma unroll
                     for (int m = 0; m < kMaxK; m++) {
                         if (m >= kk) break;
-                        if (m != k) owned = owned && never_closer(g.ox, g.oy, g.oz, ch.x[m], ch.y[m], ch.z[m], kx, ky, kz);
+                        if (m != k) owned = owned && (Dc[m] - Dk - selk(Mkk + m * kMaxK) >= 0);
                     }
-                    const uint32_t ds = cube_sum(g, kx, ky, kz);
+                    // cube sums: P + n D_c(o) - 2 c.S_u, P = n |o|^2 + 2 o.S_u + S_u2
+                    const int Pc = __mul24(g.n, __mul24(g.ox, g.ox) + __mul24(g.oy, g.oy) + __mul24(g.oz, g.oz)) +
+                                   2 * (__mul24(g.ox, g.sx) + __mul24(g.oy, g.sy) + __mul24(g.oz, g.sz)) + g.s2;
+                    const uint32_t ds = (uint32_t)(Pc + __mul24(g.n, Dk) -
+                                                   2 * (__mul24(kx, g.sx) + __mul24(ky, g.sy) + __mul24(kz, g.sz)));
                     uint32_t vv[3];
                     bool dec = owned;
 #pragma unroll
                     for (int j = 0; j < 3; j++) {
-                        const bool A = never_closer(g.ox, g.oy, g.oz, tx[j], ty[j], tz[j], kx, ky, kz);
-                        const bool B = always_closer(g.ox, g.oy, g.oz, tx[j], ty[j], tz[j], kx, ky, kz);
+                        const int Dt = T2[j] - 2 * (__mul24(g.ox, tx[j]) + __mul24(g.oy, ty[j]) + __mul24(g.oz, tz[j]));
+                        const int f = Dt - Dk;
+                        const bool A = f - selk(NA + j * kMaxK) >= 0;  // t_j never strictly closer than c_k
+                        const bool B = f + selk(NB + j * kMaxK) <= 0;  // t_j always at least as close
                         dec = dec && (A || B);
-                        vv[j] = A ? ds : cube_sum(g, tx[j], ty[j], tz[j]);
+                        vv[j] = A ? ds
+                                  : (uint32_t)(Pc + __mul24(g.n, Dt) -
+                                               2 * (__mul24(tx[j], g.sx) + __mul24(ty[j], g.sy) + __mul24(tz[j], g.sz)));
                     }
                     v0 = vv[0];
                     v1 = vv[1];
