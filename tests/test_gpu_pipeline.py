@@ -276,3 +276,36 @@ def test_validate_and_preprocess_image_resizes_on_gpu(orc):
     for mode in ("auto", "performance", "high_quality", "none"):
         out = asyncio.run(validate_and_preprocess_image(buf.getvalue(), "r", mode))
         assert np.array_equal(out, orc.preprocess(np.ascontiguousarray(bgr), mode)), mode
+
+
+def _flat(h, w, colours, seed=0):
+    """Image made of vertical bands of the given BGR colours (few unique colours)."""
+    img = np.zeros((h, w, 3), np.uint8)
+    bands = np.array_split(np.arange(w), len(colours))
+    for c, xs in zip(colours, bands):
+        img[:, xs] = c
+    return img
+
+
+@pytest.mark.parametrize("ncol", [1, 2, 3, 5, 6, 9])
+def test_few_unique_colours_vs_oracle(backend, orc, ncol):
+    """U <= 5 (K = U: every colour its own centre, compactness 0), U = 1 (K = 1) and a few
+    more colours than K, with zero parity noise so U is exactly the band count."""
+    rng = np.random.default_rng(ncol)
+    cols = [tuple(int(v) for v in rng.integers(0, 256, 3)) for _ in range(ncol)]
+    x = np.stack([_flat(90, 160, cols), _flat(90, 160, cols[::-1])])
+    noise = np.zeros((2, 90 * 160 * 3), np.int8)
+    res = backend.process(x, ("colors", "shapes", "shadows"), seed=3, noise=noise, index_base=40)
+    for i, r in enumerate(res):
+        _check_against_oracle(orc, x[i], r, noise[i], 3, 40 + i)
+        assert r.n_unique == ncol
+        if ncol <= 5:
+            got = sorted(map(tuple, r.centers_rgb.tolist()))
+            want = sorted((c[2], c[1], c[0]) for c in cols)  # BGR bands -> RGB centres
+            assert got == want and r.compactness == 0.0
+
+
+def test_empty_batch(backend):
+    assert backend.process(np.zeros((0, 32, 48, 3), np.uint8)) == []
+    t = backend.submit(np.zeros((0, 32, 48, 3), np.uint8))
+    assert backend.collect(t) == []
