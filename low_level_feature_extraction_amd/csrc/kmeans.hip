@@ -294,15 +294,6 @@ __device__ __forceinline__ uint32_t cube_origin_key(uint32_t id) {
 // push; lane b's rank among the set bits comes from mbcnt).  fill + popc(m) <= 64;
 // m and id are wave-uniform (SGPRs).
 __device__ __forceinline__ uint32_t lane_off_rel(int fill) { return (uint32_t)(__lane_id() - fill); }
-__device__ __forceinline__ void pack_key(uint32_t &pk, int fill, unsigned long long m, uint32_t okey,
-                                         uint32_t lane_off) {
-    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    const int n = __popcll(m);
-    const uint32_t dst = lane_sel(m, (uint32_t)fill + rank, fill > 0 ? 0u : 63u);
-    const uint32_t v = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst * 4u), (int)(okey | lane_off));
-    const uint32_t rel = lane_off_rel(fill);
-    pk = rel < (uint32_t)n ? v : pk;
-}
 
 // The cube table is streamed 64 entries per wave step with the next CPF steps' 16-B
 // loads in flight (3 measured no faster: the sweeps are VALU-bound).
@@ -518,19 +509,27 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
         __syncthreads();
         unsigned long long acc0 = 0, acc1 = 0, acc2 = 0, fails = 0;
         int Pcur = -1;
-        uint32_t pk = 0;  // packed boundary colours in lanes [0, fill)
+        // undecided cubes' colours go through the wave's LDS ring (as in the Lloyd
+        // sweeps) and are summed 64 at a time
         const uint32_t loff = lane_offset(lane);
-        int fill = 0;
-        auto flush_pk = [&]() {
-            fails += (unsigned long long)fill;
-            if (lane < fill) {
-                const int x = unpack_r(pk), y = unpack_g(pk), z = unpack_b(pk);
+        uint32_t *stg = sm.stage[wid];
+        int head = 0, tail = 0;  // wave-uniform ring counters
+        auto sum_stage = [&](int count) {
+            __builtin_amdgcn_wave_barrier();
+            fails += (unsigned long long)count;
+            if (lane < count) {
+                const uint32_t kq = stg[(tail + lane) & (kStage - 1)];
+                const int x = unpack_r(kq), y = unpack_g(kq), z = unpack_b(kq);
                 const int D = dmin_chosen(x, y, z, ch, kk);
                 acc0 += (uint32_t)min(D, d2i(x, y, z, tx[0], ty[0], tz[0]));
                 acc1 += (uint32_t)min(D, d2i(x, y, z, tx[1], ty[1], tz[1]));
                 acc2 += (uint32_t)min(D, d2i(x, y, z, tx[2], ty[2], tz[2]));
             }
-            fill = 0;
+            tail += count;
+        };
+        auto flush_pk = [&]() {
+            while (head - tail >= 64) sum_stage(64);
+            if (head > tail) sum_stage(head - tail);
         };
         // Round constants (wave-uniform).  Every test below is linear in the cube origin o:
         // with D_c(o) = |c|^2 - 2 o.c, d(o, c) = |o|^2 + D_c(o), so
@@ -665,15 +664,21 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
                     const uint32_t okey = cube_origin_key(e.id);  // read back per cube below
                     const uint32_t mlo = (uint32_t)e.mask, mhi = (uint32_t)(e.mask >> 32);
                     while (fm) {
-                        const int src = __builtin_ctzll(fm);
-                        fm &= fm - 1;
-                        const unsigned long long m =
-                            ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(mhi, src) << 32) |
-                            (uint32_t)__builtin_amdgcn_readlane(mlo, src);
-                        const int n = __popcll(m);
-                        if (fill + n > 64) flush_pk();
-                        pack_key(pk, fill, m, (uint32_t)__builtin_amdgcn_readlane(okey, src), loff);
-                        fill += n;
+#pragma unroll
+                        for (int u = 0; u < LLFE_KM_UNROLL; u++) {
+                            if (u > 0 && !fm) break;
+                            const int src = __builtin_ctzll(fm);
+                            fm &= fm - 1;
+                            const unsigned long long m =
+                                ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(mhi, src) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane(mlo, src);
+                            const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                            stg[lane_sel(m, ((uint32_t)head + r) & (kStage - 1), kStage + lane)] =
+                                (uint32_t)__builtin_amdgcn_readlane(okey, src) | loff;
+                            head += __popcll(m);
+                        }
+                        while (head - tail >= 64) sum_stage(64);
                     }
                 }
                 const unsigned long long rest = __ballot(P > Pseg && P < kParts);
