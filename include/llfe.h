@@ -218,6 +218,17 @@ int llfe_classify_contour(const int32_t *points, int32_t n, llfe_shape *out);
 /* host-side shape records from a host u8 mask (the analyze_shapes loop). */
 int llfe_shapes_from_mask(const uint8_t *mask, int32_t h, int32_t w, llfe_shape *shapes, int32_t capacity,
                           int32_t *n_contours);
+/* The same two on the GPU path the batch uses (contours_gpu.hip: components, border
+ * following from first pixels, the raster-scan replay, geometry), from host u8 masks
+ * of width <= 4096.  llfe_find_contours_gpu: as llfe_find_contours (cv2 order).
+ * llfe_shapes_from_masks_gpu: n masks; per image n_shapes / n_contours, shape records
+ * concatenated (LLFE_ERR_CAPACITY with *needed when capacity is short). */
+int llfe_find_contours_gpu(llfe_ctx *ctx, const uint8_t *mask, int32_t h, int32_t w, int32_t *points,
+                           int64_t points_capacity, int32_t *offsets, int32_t offsets_capacity,
+                           int64_t *needed_points);
+int llfe_shapes_from_masks_gpu(llfe_ctx *ctx, const uint8_t *masks, int32_t n, int32_t h, int32_t w,
+                               llfe_shape *shapes, int64_t capacity, int32_t *n_shapes, int32_t *n_contours,
+                               int64_t *needed);
 
 /* ---- host PNG decode (cv2.imdecode(buf, IMREAD_COLOR), utils.py:108-109 and
  * image_processor.py:208-211).  Host only, no ctx.  IMREAD_COLOR semantics: BGR u8,

@@ -113,6 +113,9 @@ SIGNATURES = {
     "llfe_border_radius": (C.c_double, [_vp, _i32, C.c_double]),
     "llfe_classify_contour": (C.c_int, [_vp, _i32, C.POINTER(LlfeShape)]),
     "llfe_shapes_from_mask": (C.c_int, [_vp, _i32, _i32, _vp, _i32, C.POINTER(C.c_int32)]),
+    "llfe_find_contours_gpu": (C.c_int, [_vp, _vp, _i32, _i32, _vp, _i64, _vp, _i32, C.POINTER(C.c_int64)]),
+    "llfe_shapes_from_masks_gpu": (C.c_int, [_vp, _vp, _i32, _i32, _i32, _vp, _i64, _vp, _vp,
+                                             C.POINTER(C.c_int64)]),
     "llfe_png_info": (C.c_int, [_vp, C.c_uint64, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "llfe_decode_png_batch": (C.c_int, [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _i32]),
 }

@@ -286,6 +286,49 @@ class Backend:
         self._chk(self._lib.llfe_shape_mask(self.ctx, x.data_ptr(), out.data_ptr(), n, h, w, self._stream(x)))
         return out
 
+    def find_contours_gpu(self, mask: np.ndarray) -> list:
+        """findContours(RETR_EXTERNAL, CHAIN_APPROX_SIMPLE) of one host u8 mask on the GPU
+        contour path (the one llfe_process_batch uses) -> list of (n,2) int32, cv2 order."""
+        m = np.ascontiguousarray(mask, np.uint8)
+        h, w = m.shape
+        cap = 1 << 16
+        while True:
+            pts = np.empty((cap, 2), np.int32)
+            offs = np.empty(cap + 1, np.int32)
+            need = C.c_int64(0)
+            nc = self._lib.llfe_find_contours_gpu(self.ctx, m.ctypes.data, h, w, pts.ctypes.data, cap,
+                                                  offs.ctypes.data, cap + 1, C.byref(need))
+            if nc == L.LLFE_ERR_CAPACITY:
+                cap = max(int(need.value), cap * 2)
+                continue
+            self._chk(min(nc, 0))
+            return [pts[offs[i]:offs[i + 1]].copy() for i in range(nc)]
+
+    def shapes_from_masks_gpu(self, masks: np.ndarray):
+        """analyze_shapes' records for n host u8 masks (n x h x w) on the GPU contour path
+        -> (list of per-image shape dict lists, n_contours np.int32[n])."""
+        m = np.ascontiguousarray(masks, np.uint8)
+        n, h, w = m.shape
+        cap = max(64, 16 * n)
+        while True:
+            arr = (L.LlfeShape * cap)()
+            ns = np.zeros(n, np.int32)
+            nc = np.zeros(n, np.int32)
+            need = C.c_int64(0)
+            rc = self._lib.llfe_shapes_from_masks_gpu(self.ctx, m.ctypes.data, n, h, w, arr, cap, ns.ctypes.data,
+                                                      nc.ctypes.data, C.byref(need))
+            if rc == L.LLFE_ERR_CAPACITY:
+                cap = int(need.value)
+                continue
+            self._chk(rc)
+            out, k = [], 0
+            for i in range(n):
+                out.append([{"type": L.SHAPE_TYPES[s.type], "x": int(s.x), "y": int(s.y), "width": int(s.width),
+                             "height": int(s.height), "border_radius": float(s.border_radius),
+                             "area": float(s.area)} for s in arr[k:k + ns[i]]])
+                k += int(ns[i])
+            return out, nc
+
     def shadow_stats(self, images):
         x = self._dev_batch(images)
         n, h, w, _ = x.shape

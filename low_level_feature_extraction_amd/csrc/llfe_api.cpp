@@ -212,6 +212,15 @@ struct Work {
     DevBuf<int64_t> d_nuniq;
     DevBuf<KmeansAttemptOut> d_att;
     DevBuf<KmeansImageOut> d_kout;
+    // GPU contours (contours_gpu.hip); capacities grow when a pass overflows them
+    DevBuf<uint64_t> d_ct_planes;
+    DevBuf<CtComp> d_ct_comps;
+    DevBuf<uint8_t> d_ct_acc;
+    DevBuf<int2> d_ct_pts, d_ct_refs;
+    DevBuf<CtCounters> d_ct_ctr;
+    DevBuf<int> d_ct_info;
+    DevBuf<llfe_shape> d_ct_shapes;
+    CtCaps ct_min{0, 0, 0, 0};  // grown minimum capacities (0 = defaults)
 };
 
 // hipEvent pairs around launches (enabled by llfe_set_profiling)
@@ -357,6 +366,13 @@ struct llfe_ctx {
     // pinned host staging; the per-chunk results are double-buffered so the host can
     // trace chunk c's contours while the GPU runs chunk c + 1
     HostBuf<uint64_t> h_bits_s[2];
+    // GPU contours: per-image (components, ref base, contours, kept, shape base),
+    // counters and shape records of each slot
+    bool gpu_contours = true;  // LLFE_CONTOURS=host: contours on the host thread pool
+    HostBuf<int> h_ct_info_s[2];
+    HostBuf<CtCounters> h_ct_ctr_s[2];
+    HostBuf<llfe_shape> h_ct_shapes_s[2];
+    int64_t h_ct_shape_cap[2] = {0, 0};
     HostBuf<unsigned long long> h_shadow_s[2];
     HostBuf<KmeansImageOut> h_kout_s[2];
     hipEvent_t chunk_done[2] = {nullptr, nullptr};
@@ -445,6 +461,59 @@ int run_hysteresis_dilate(llfe_ctx *ctx, Work &W, int n, int h, int w, uint64_t 
     TIMED(ctx, s, "k_hysteresis_dilate", (double)n * h * w * (1 + 2 + 1 + 2 + 3 * 0.125),
           launch_hysteresis_dilate(W.d_cls.p, n, h, w, wk, bits, mask_u8, s));
     return LLFE_OK;
+}
+
+// External contours + shape records of W.d_bits on the GPU (hysteresis workspace reused)
+int run_contours(llfe_ctx *ctx, Work &W, int n, int h, int w, const uint64_t *bits, hipStream_t s) {
+    CtCaps c = contours_default_caps(n, h, w);
+    c.comps = std::max(c.comps, W.ct_min.comps);
+    c.pts = std::max(c.pts, W.ct_min.pts);
+    c.refs = std::max(c.refs, W.ct_min.refs);
+    c.shapes = std::max(c.shapes, W.ct_min.shapes);
+    const size_t ids = hysteresis_ids(n, h, w);
+    HIPCHK(ctx, W.d_lab.ensure((size_t)n * h * w));
+    HIPCHK(ctx, W.d_parent.ensure(ids));
+    HIPCHK(ctx, W.d_roots.ensure(ids));
+    HIPCHK(ctx, W.d_nroots.ensure((size_t)tiles_x(w) * tiles_y(h) * n));
+    HIPCHK(ctx, W.d_ct_planes.ensure(5 * contours_plane_words(n, h, w)));
+    HIPCHK(ctx, W.d_ct_comps.ensure(c.comps));
+    HIPCHK(ctx, W.d_ct_acc.ensure(c.comps));
+    HIPCHK(ctx, W.d_ct_pts.ensure(c.pts));
+    HIPCHK(ctx, W.d_ct_refs.ensure(c.refs));
+    HIPCHK(ctx, W.d_ct_ctr.ensure(1));
+    HIPCHK(ctx, W.d_ct_info.ensure((size_t)n * kCtInfo));
+    HIPCHK(ctx, W.d_ct_shapes.ensure(c.shapes));
+    CtWork wk{W.d_lab.p, W.d_parent.p, W.d_roots.p, W.d_nroots.p, W.d_ct_planes.p, W.d_ct_comps.p, W.d_ct_acc.p,
+              W.d_ct_pts.p, W.d_ct_refs.p, W.d_ct_ctr.p, W.d_ct_info.p, W.d_ct_shapes.p, c};
+    // algorithmic bytes: mask bits read by components + scan, labels written and read
+    TIMED(ctx, s, "k_contours", (double)n * h * w * (0.25 + 4.0), launch_contours(bits, n, h, w, wk, s));
+    return LLFE_OK;
+}
+
+// enqueue the D2H of a contour pass's results into host slot `slot` on stream cs
+int copy_contours(llfe_ctx *ctx, Work &W, int n, int slot, hipStream_t cs) {
+    HIPCHK(ctx, ctx->h_ct_info_s[slot].ensure((size_t)n * kCtInfo));
+    HIPCHK(ctx, ctx->h_ct_ctr_s[slot].ensure(1));
+    HIPCHK(ctx, ctx->h_ct_shapes_s[slot].ensure(W.d_ct_shapes.n));
+    ctx->h_ct_shape_cap[slot] = (int64_t)W.d_ct_shapes.n;
+    HIPCHK(ctx, hipMemcpyAsync(ctx->h_ct_info_s[slot].p, W.d_ct_info.p, sizeof(int) * n * kCtInfo,
+                               hipMemcpyDeviceToHost, cs));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->h_ct_ctr_s[slot].p, W.d_ct_ctr.p, sizeof(CtCounters), hipMemcpyDeviceToHost, cs));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->h_ct_shapes_s[slot].p, W.d_ct_shapes.p, sizeof(llfe_shape) * W.d_ct_shapes.n,
+                               hipMemcpyDeviceToHost, cs));
+    return LLFE_OK;
+}
+
+// grow the contour capacities after an overflowing pass (counters hold what was asked)
+void grow_contour_caps(Work &W, int n, int h, int w, const CtCounters &ct) {
+    const CtCaps d = contours_default_caps(n, h, w);
+    CtCaps &m = W.ct_min;
+    auto up = [](int64_t cur, int64_t dflt, int64_t need) { return std::max({2 * std::max(cur, dflt), need + need / 4}); };
+    if (ct.flags & kCtOverflowComps) m.comps = up(m.comps, d.comps, (int64_t)ct.comps + (int64_t)n * kCtQuirkCap);
+    if (ct.flags & kCtOverflowPts) m.pts = up(m.pts, d.pts, (int64_t)ct.pts);
+    if (ct.flags & (kCtOverflowRefs | kCtOverflowComps))
+        m.refs = up(m.refs, d.refs, std::max<int64_t>(m.comps, d.comps) + (int64_t)n * kCtQuirkCap);
+    if (ct.flags & kCtOverflowShapes) m.shapes = up(m.shapes, d.shapes, (int64_t)ct.shapes);
 }
 
 int color_stage(llfe_ctx *ctx, Work &W, const uint8_t *img, const int8_t *noise, int n, int h, int w, uint64_t seed,
@@ -573,20 +642,29 @@ int enqueue_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_
     }
     // shapes + shadows go to the host (event mask_done) while the GPU is still in this
     // chunk's colour stage, so contour tracing overlaps k-means
+    const bool gpu_ct = ctx->gpu_contours && w <= kCtMaxWidth;
     if (want_shp) {
         HIPCHK(ctx, W.d_bits.ensure((size_t)n * h * wpr));
-        HIPCHK(ctx, ctx->h_bits_s[slot].ensure((size_t)n * h * wpr));
+        if (!gpu_ct) HIPCHK(ctx, ctx->h_bits_s[slot].ensure((size_t)n * h * wpr));
         rc = run_hysteresis_dilate(ctx, W, n, h, w, W.d_bits.p, nullptr, s);
         if (rc) return rc;
+        if (gpu_ct) {
+            rc = run_contours(ctx, W, n, h, w, W.d_bits.p, s);
+            if (rc) return rc;
+        }
     }
     if (want_shd) HIPCHK(ctx, ctx->h_shadow_s[slot].ensure(2 * (size_t)n));
     if (want_shp || want_shd) {
         hipStream_t cs = ctx->copy_stream;
         HIPCHK(ctx, hipEventRecord(ctx->mask_ready[slot], s));
         HIPCHK(ctx, hipStreamWaitEvent(cs, ctx->mask_ready[slot], 0));
-        if (want_shp)
+        if (want_shp && gpu_ct) {
+            rc = copy_contours(ctx, W, n, slot, cs);
+            if (rc) return rc;
+        } else if (want_shp) {
             HIPCHK(ctx, hipMemcpyAsync(ctx->h_bits_s[slot].p, W.d_bits.p, sizeof(uint64_t) * n * h * wpr,
                                        hipMemcpyDeviceToHost, cs));
+        }
         if (want_shd)
             HIPCHK(ctx, hipMemcpyAsync(ctx->h_shadow_s[slot].p, W.d_shadow.p, sizeof(unsigned long long) * 2 * n,
                                        hipMemcpyDeviceToHost, cs));
@@ -613,6 +691,61 @@ int enqueue_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_
     return LLFE_OK;
 }
 
+// Shape records of a chunk whose contours ran on the GPU (slot's host copies).  A pass
+// that overflowed a capacity is redone for this chunk alone, synchronously, with the
+// capacities grown from what its counters asked for.
+int gpu_shapes_of_chunk(llfe_ctx *ctx, const llfe_batch *b, int i0, int n, int slot, llfe_image_result *results,
+                        llfe_shape *shapes, int64_t shape_capacity, int64_t &total_shapes) {
+    const int h = b->height, w = b->width;
+    for (int attempt = 0;; attempt++) {
+        const CtCounters ct = *ctx->h_ct_ctr_s[slot].p;
+        if (ct.flags & (kCtBadTrace | kCtTooWide | kCtDpOverflow))
+            return ctx->fail(LLFE_ERR_UNSUPPORTED, "GPU contours: unsupported mask (flags 0x%x)", ct.flags);
+        if (!(ct.flags & kCtOverflowMask)) break;
+        if (attempt >= 8) return ctx->fail(LLFE_ERR_CAPACITY, "GPU contours: capacities still overflow (0x%x)", ct.flags);
+        // redo the shapes path of this chunk on workspace 0 once the device is idle
+        HIPCHK(ctx, hipDeviceSynchronize());
+        Work &W = ctx->ws[0];
+        grow_contour_caps(W, n, h, w, ct);
+        hipStream_t s = ctx->streams[0];
+        const uint8_t *img;
+        const int8_t *noise;
+        llfe_batch nb = *b;
+        nb.noise = nullptr;
+        int rc = stage_input(ctx, W, &nb, i0, n, &img, &noise, s);
+        if (rc) return rc;
+        HIPCHK(ctx, W.d_cls.ensure((size_t)n * h * w));
+        HIPCHK(ctx, W.d_bits.ensure((size_t)n * h * words_per_row(w)));
+        HIPCHK(ctx, launch_stencil(img, n, h, w, W.d_cls.p, nullptr, nullptr, nullptr, nullptr, ctx->sp, s));
+        rc = run_hysteresis_dilate(ctx, W, n, h, w, W.d_bits.p, nullptr, s);
+        if (rc) return rc;
+        rc = run_contours(ctx, W, n, h, w, W.d_bits.p, s);
+        if (rc) return rc;
+        rc = copy_contours(ctx, W, n, slot, s);
+        if (rc) return rc;
+        HIPCHK(ctx, hipStreamSynchronize(s));
+    }
+    const int *info = ctx->h_ct_info_s[slot].p;
+    const llfe_shape *src = ctx->h_ct_shapes_s[slot].p;
+    ctx->img_shapes.resize(n);
+    ctx->img_ncont.assign(n, 0);
+    for (int i = 0; i < n; i++) {
+        llfe_image_result &r = results[i0 + i];
+        const int nk = info[i * kCtInfo + 3], sb = info[i * kCtInfo + 4];
+        r.shape_offset = total_shapes;
+        r.n_shapes = nk;
+        r.n_contours = info[i * kCtInfo + 2];
+        ctx->img_ncont[i] = r.n_contours;
+        ctx->img_shapes[i].assign(src + sb, src + sb + nk);
+        if (shapes) {
+            const int64_t room = std::max<int64_t>(0, std::min<int64_t>(nk, shape_capacity - total_shapes));
+            if (room > 0) std::memcpy(shapes + total_shapes, src + sb, sizeof(llfe_shape) * (size_t)room);
+        }
+        total_shapes += nk;
+    }
+    return LLFE_OK;
+}
+
 // Host half of one chunk: wait for its slot, fill the result records, trace contours.
 int finish_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, int i0, int n, int slot,
                  llfe_image_result *results, llfe_shape *shapes, int64_t shape_capacity, int64_t &total_shapes) {
@@ -630,7 +763,10 @@ int finish_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, int i0, 
             r.shadow_count = sh[n + i];
         }
     }
-    if (want_shp) {
+    if (want_shp && ctx->gpu_contours && w <= kCtMaxWidth) {
+        int rc = gpu_shapes_of_chunk(ctx, b, i0, n, slot, results, shapes, shape_capacity, total_shapes);
+        if (rc) return rc;
+    } else if (want_shp) {
         ctx->img_shapes.resize(n);
         ctx->img_ncont.assign(n, 0);
         const uint64_t *hb = ctx->h_bits_s[slot].p;
@@ -699,6 +835,7 @@ int llfe_init(int device, llfe_ctx **out) {
     if (const char *ch = getenv("LLFE_CHUNK"); ch && atoi(ch) > 0) c->chunk = std::min(atoi(ch), kMaxKmeansBatch);
     if (const char *ns = getenv("LLFE_STREAMS"); ns && atoi(ns) == 2) c->nstreams = 2;
     if (const char *sa = getenv("LLFE_SHAPES_AFTER_FRONT"); sa && atoi(sa) == 1) c->shapes_after_front = true;
+    if (const char *cm = getenv("LLFE_CONTOURS"); cm && !strcmp(cm, "host")) c->gpu_contours = false;
     gauss_kernel_f32(11, c->sp.k11);
     c->pool = new Pool(default_threads() - 1);
     int nt = c->pool->size() + 1;
@@ -1158,6 +1295,94 @@ int llfe_find_contours(const uint8_t *mask, int32_t h, int32_t w, int32_t *point
         offsets[k + 1] = (int32_t)wpos;
     }
     return nc;
+}
+
+namespace {
+// host u8 masks -> bit-packed on the device -> GPU contour pass on workspace 0 (synchronous;
+// capacities grown until nothing overflows).  Leaves the results in W.d_ct_* and
+// slot 0's host copies.
+int gpu_contours_of_masks(llfe_ctx *ctx, const uint8_t *masks, int n, int h, int w) {
+    if (w > kCtMaxWidth) return ctx->fail(LLFE_ERR_UNSUPPORTED, "GPU contours need width <= %d", kCtMaxWidth);
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    HIPCHK(ctx, hipDeviceSynchronize());
+    Work &W = ctx->ws[0];
+    hipStream_t s = ctx->streams[0];
+    const int wpr = words_per_row(w);
+    std::vector<uint64_t> bits((size_t)n * h * wpr, 0ull);
+    for (size_t r = 0; r < (size_t)n * h; r++)
+        for (int x = 0; x < w; x++)
+            if (masks[r * w + x]) bits[r * wpr + (x >> 6)] |= 1ull << (x & 63);
+    HIPCHK(ctx, W.d_bits.ensure(bits.size()));
+    HIPCHK(ctx, hipMemcpyAsync(W.d_bits.p, bits.data(), sizeof(uint64_t) * bits.size(), hipMemcpyHostToDevice, s));
+    for (int attempt = 0;; attempt++) {
+        int rc = run_contours(ctx, W, n, h, w, W.d_bits.p, s);
+        if (rc) return rc;
+        rc = copy_contours(ctx, W, n, 0, s);
+        if (rc) return rc;
+        HIPCHK(ctx, hipStreamSynchronize(s));
+        const CtCounters ct = *ctx->h_ct_ctr_s[0].p;
+        if (ct.flags & (kCtBadTrace | kCtTooWide | kCtDpOverflow))
+            return ctx->fail(LLFE_ERR_UNSUPPORTED, "GPU contours: unsupported mask (flags 0x%x)", ct.flags);
+        if (!(ct.flags & kCtOverflowMask)) return LLFE_OK;
+        if (attempt >= 8) return ctx->fail(LLFE_ERR_CAPACITY, "GPU contours: capacities still overflow");
+        grow_contour_caps(W, n, h, w, ct);
+    }
+}
+}  // namespace
+
+int llfe_find_contours_gpu(llfe_ctx *ctx, const uint8_t *mask, int32_t h, int32_t w, int32_t *points,
+                           int64_t points_capacity, int32_t *offsets, int32_t offsets_capacity,
+                           int64_t *needed_points) {
+    if (!ctx || !mask || h <= 0 || w <= 0 || !valid_dims(1, h, w)) return LLFE_ERR_INVALID;
+    int rc = gpu_contours_of_masks(ctx, mask, 1, h, w);
+    if (rc) return rc;
+    Work &W = ctx->ws[0];
+    const CtCounters ct = *ctx->h_ct_ctr_s[0].p;
+    const int *info = ctx->h_ct_info_s[0].p;
+    const int base = info[1], nc = info[2];
+    std::vector<int2> refs(nc);
+    std::vector<CtComp> comps(ct.comps);
+    std::vector<int2> pts(ct.pts);
+    if (nc) HIPCHK(ctx, hipMemcpy(refs.data(), W.d_ct_refs.p + base, sizeof(int2) * nc, hipMemcpyDeviceToHost));
+    if (ct.comps) HIPCHK(ctx, hipMemcpy(comps.data(), W.d_ct_comps.p, sizeof(CtComp) * ct.comps, hipMemcpyDeviceToHost));
+    if (ct.pts) HIPCHK(ctx, hipMemcpy(pts.data(), W.d_ct_pts.p, sizeof(int2) * ct.pts, hipMemcpyDeviceToHost));
+    int64_t npts = 0;
+    for (int k = 0; k < nc; k++) npts += comps[refs[k].x].nv;
+    if (needed_points) *needed_points = npts;
+    if (npts > points_capacity || nc + 1 > offsets_capacity) return LLFE_ERR_CAPACITY;
+    int64_t wpos = 0;  // cv2 order: newest first
+    offsets[0] = 0;
+    for (int k = 0; k < nc; k++) {
+        const CtComp &c = comps[refs[nc - 1 - k].x];
+        for (uint32_t v = 0; v < c.nv; v++) {
+            points[2 * (wpos + v)] = pts[c.off + v].x;
+            points[2 * (wpos + v) + 1] = pts[c.off + v].y;
+        }
+        wpos += c.nv;
+        offsets[k + 1] = (int32_t)wpos;
+    }
+    return nc;
+}
+
+int llfe_shapes_from_masks_gpu(llfe_ctx *ctx, const uint8_t *masks, int32_t n, int32_t h, int32_t w,
+                               llfe_shape *shapes, int64_t capacity, int32_t *n_shapes, int32_t *n_contours,
+                               int64_t *needed) {
+    if (!ctx || !masks || !valid_dims(n, h, w) || n <= 0) return LLFE_ERR_INVALID;
+    int rc = gpu_contours_of_masks(ctx, masks, n, h, w);
+    if (rc) return rc;
+    const int *info = ctx->h_ct_info_s[0].p;
+    const llfe_shape *src = ctx->h_ct_shapes_s[0].p;
+    int64_t total = 0;
+    for (int i = 0; i < n; i++) {
+        const int nk = info[i * kCtInfo + 3], sb = info[i * kCtInfo + 4];
+        if (n_shapes) n_shapes[i] = nk;
+        if (n_contours) n_contours[i] = info[i * kCtInfo + 2];
+        for (int k = 0; k < nk; k++)
+            if (shapes && total + k < capacity) shapes[total + k] = src[sb + k];
+        total += nk;
+    }
+    if (needed) *needed = total;
+    return total > capacity ? LLFE_ERR_CAPACITY : LLFE_OK;
 }
 
 double llfe_border_radius(const int32_t *points, int32_t n, double epsilon_factor) {

@@ -5,6 +5,8 @@
 
 #include <vector>
 
+#include "../../include/llfe.h"
+
 namespace llfe {
 
 // ---------------------------------------------------------------- stencils
@@ -47,6 +49,50 @@ struct HystWork {
 size_t hysteresis_ids(int n, int h, int w);
 hipError_t launch_hysteresis_dilate(const uint8_t *cls, int n, int h, int w, const HystWork &wk, uint64_t *bits,
                                     uint8_t *mask_u8, hipStream_t s);
+
+// External contours + shape records on the GPU (contours_gpu.hip).  Reuses the
+// hysteresis workspace (lab, parent, roots, nroots) once the dilated mask exists.
+struct CtComp {  // one outer border: a component's (or a border started elsewhere)
+    uint32_t key;    // raster key y * W + x of the start pixel
+    int32_t img;
+    uint32_t nv;     // CHAIN_APPROX_SIMPLE vertices at pts[off, off + nv)
+    uint32_t off;
+    int64_t area2;   // signed twice contourArea (shoelace, exact)
+    uint16_t x0, y0, x1, y1;  // bounding box (inclusive)
+};
+static_assert(sizeof(CtComp) == 32, "CtComp is 32 bytes");
+struct CtCounters {
+    unsigned int comps, refs;
+    unsigned long long pts;
+    unsigned int flags, quirks, shapes, pad;
+};
+constexpr unsigned kCtOverflowComps = 1, kCtOverflowPts = 2, kCtOverflowRefs = 4, kCtOverflowShapes = 8;
+constexpr unsigned kCtBadTrace = 16, kCtTooWide = 32, kCtDpOverflow = 64;
+constexpr unsigned kCtOverflowMask = 15;  // capacity flags: the host grows and reruns
+constexpr int kCtInfo = 5;       // per image: components, ref base, contours, kept, shape base
+constexpr int kCtQuirkCap = 64;  // borders per image started away from a first pixel
+constexpr int kCtMaxWidth = 4096;  // GPU contours: widest image (hull columns in LDS)
+struct CtCaps {
+    int64_t comps, pts, refs, shapes;
+};
+struct CtWork {
+    uint16_t *lab;
+    int *parent;
+    uint16_t *roots;
+    int *nroots;
+    uint64_t *planes;  // 5 bit planes of contours_plane_words(): visited, right-bound, Q visited, Q right, first
+    CtComp *comps;     // caps.comps
+    uint8_t *acc;      // caps.comps
+    int2 *pts;         // caps.pts
+    int2 *refs;        // caps.refs: (component slot, shape index or -1) in start order
+    CtCounters *ctr;
+    int *img_info;     // n * kCtInfo
+    llfe_shape *shapes;  // caps.shapes
+    CtCaps caps;
+};
+CtCaps contours_default_caps(int n, int h, int w);
+size_t contours_plane_words(int n, int h, int w);
+hipError_t launch_contours(const uint64_t *bits, int n, int h, int w, const CtWork &wk, hipStream_t s);
 
 inline int words_per_row(int w) { return (w + 63) / 64; }
 inline int tiles_x(int w) { return (w + kTileW - 1) / kTileW; }
