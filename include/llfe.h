@@ -119,6 +119,15 @@ int llfe_set_profiling(llfe_ctx *ctx, int enable);
 /* llfe_process_batch runs the colour path on a second stream beside shapes / shadows
  * (1, the default) or everything in order on one stream (0: isolated kernel timings) */
 int llfe_set_concurrency(llfe_ctx *ctx, int enable);
+/* where llfe_process_batch / llfe_collect_batch run findContours + the shape loop of
+ * ShapeAnalyzer.analyze_shapes (shape pyc @L140-181): LLFE_CONTOURS_HOST (default) on the
+ * context's host thread pool from the bit-packed mask copied back, overlapping the
+ * GPU's k-means; LLFE_CONTOURS_GPU on the GPU (contours_gpu.hip; images up to 4096 wide
+ * and 65535 tall, wider ones stay on the host).  Identical results either way.  The
+ * environment variable LLFE_CONTOURS=gpu sets the initial mode. */
+#define LLFE_CONTOURS_HOST 0
+#define LLFE_CONTOURS_GPU 1
+int llfe_set_contour_mode(llfe_ctx *ctx, int mode);
 /* copies up to cap entries, returns the number of kernels with statistics */
 int llfe_kernel_stats(llfe_ctx *ctx, llfe_kernel_stat *out, int32_t cap);
 

@@ -109,6 +109,11 @@ class Backend:
         in order on one stream (isolated kernel timings)."""
         self._chk(self._lib.llfe_set_concurrency(self.ctx, int(bool(enable))))
 
+    def set_contour_mode(self, mode: str):
+        """"host" (default): findContours + shape geometry on the host pool while the GPU
+        runs k-means; "gpu": on the GPU (contours_gpu.hip).  Identical results."""
+        self._chk(self._lib.llfe_set_contour_mode(self.ctx, {"host": 0, "gpu": 1}[mode]))
+
     def kernel_stats(self) -> dict:
         """{kernel: {"launches", "total_ms", "bytes"}} accumulated while profiling."""
         arr = (L.LlfeKernelStat * 64)()

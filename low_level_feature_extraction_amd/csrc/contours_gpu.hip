@@ -43,14 +43,15 @@ constexpr int TW = kTileW, TH = kTileH, TP = TW * TH;
 constexpr int NT = 256;
 constexpr uint8_t kUndecided = 0, kAccepted = 1, kRejected = 2;
 constexpr int kRejBoxes = 64;     // rejected-component boxes kept in LDS by k_ct_scan
-constexpr int kDpStack = 2048;    // Douglas-Peucker slice stack (pairs)
+constexpr int kDpStack = 512;     // Douglas-Peucker slice stack (pairs)
+constexpr int kPtsLds = 1024;     // contours up to this many vertices are staged in LDS
 constexpr int kHullCols = kCtMaxWidth;  // widest contour bbox the hull pass handles
 
 __constant__ int kDX[8] = {1, 1, 0, -1, -1, -1, 0, 1};
 __constant__ int kDY[8] = {0, -1, -1, -1, 0, 1, 1, 1};
 
 struct Geo {
-    int H, W, wpr, ntx, ntiles;
+    int H, W, wpr, ntx, ntiles, n;
 };
 
 // raster key (y * W + x) <-> tile-major id of the same pixel
@@ -116,12 +117,23 @@ __global__ __launch_bounds__(NT) void k_ct_local(const uint64_t *__restrict__ bi
                                                  int *__restrict__ nroots) {
     __shared__ int L[TP];
     __shared__ uint64_t rows[TH];
-    __shared__ int cnt;
-    const int tid = threadIdx.x, img = blockIdx.y, t = blockIdx.x;
+    __shared__ int cnt, s_any;
+    const int tid = threadIdx.x;
+    for (int64_t tt = blockIdx.x; tt < (int64_t)g.ntiles * g.n; tt += gridDim.x) {
+    const int img = (int)(tt / g.ntiles), t = (int)(tt % g.ntiles);
     const int tx = t % g.ntx, ty0 = (t / g.ntx) * TH, tx0 = tx * TW;
     if (tid < TH) rows[tid] = ty0 + tid < g.H ? bits[((size_t)img * g.H + ty0 + tid) * g.wpr + tx] : 0ull;
     if (tid == 0) cnt = 0;
     __syncthreads();
+    if (tid < 64) {  // empty tile (most of an edge mask): no roots
+        const bool any = __any(tid < TH && rows[tid] != 0ull);
+        if (tid == 0) s_any = any;
+    }
+    __syncthreads();
+    if (!s_any) {
+        if (tid == 0) nroots[(size_t)img * g.ntiles + t] = 0;
+        continue;
+    }
     bool on[TP / NT];
 #pragma unroll
     for (int k = 0; k < TP / NT; k++) {
@@ -156,6 +168,8 @@ __global__ __launch_bounds__(NT) void k_ct_local(const uint64_t *__restrict__ bi
     }
     __syncthreads();
     if (tid == 0) nroots[(size_t)img * g.ntiles + t] = cnt;
+    __syncthreads();
+    }
 }
 
 __device__ __forceinline__ int root_key_of_pixel(const Geo &g, const uint16_t *lab, int img, int y, int x) {
@@ -172,8 +186,12 @@ __device__ __forceinline__ bool bit_at(const uint64_t *b, const Geo &g, int img,
 // grid (ntiles, n): threads 0..31 the tile's right column (look east), 32..95 its
 // bottom row (look south)
 __global__ __launch_bounds__(128) void k_ct_border(const uint64_t *__restrict__ bits, Geo g,
-                                                   const uint16_t *__restrict__ lab, int *__restrict__ P) {
-    const int tid = threadIdx.x, img = blockIdx.y, t = blockIdx.x;
+                                                   const uint16_t *__restrict__ lab, const int *__restrict__ nroots,
+                                                   int *__restrict__ P) {
+    const int tid = threadIdx.x;
+    for (int64_t tt = blockIdx.x; tt < (int64_t)g.ntiles * g.n; tt += gridDim.x) {
+    const int img = (int)(tt / g.ntiles), t = (int)(tt % g.ntiles);
+    if (!nroots[tt]) continue;  // no foreground in the tile
     const int tx0 = (t % g.ntx) * TW, ty0 = (t / g.ntx) * TH;
     int x, y;
     if (tid < TH) {
@@ -183,9 +201,9 @@ __global__ __launch_bounds__(128) void k_ct_border(const uint64_t *__restrict__ 
         x = tx0 + tid - TH;
         y = ty0 + TH - 1;
     } else {
-        return;
+        continue;
     }
-    if (!bit_at(bits, g, img, y, x)) return;
+    if (!bit_at(bits, g, img, y, x)) continue;
     const int a = root_key_of_pixel(g, lab, img, y, x);
     for (int dy = -1; dy <= 1; dy++)
         for (int dx = -1; dx <= 1; dx++) {
@@ -196,19 +214,39 @@ __global__ __launch_bounds__(128) void k_ct_border(const uint64_t *__restrict__ 
             if (!bit_at(bits, g, img, yy, xx)) continue;
             k_union(g, img, P, a, root_key_of_pixel(g, lab, img, yy, xx));
         }
+    }
 }
 
 __global__ __launch_bounds__(NT) void k_ct_flatten(Geo g, const uint16_t *__restrict__ roots,
                                                     const int *__restrict__ nroots, int *__restrict__ P) {
-    const int img = blockIdx.y, t = blockIdx.x;
-    const size_t tile = (size_t)img * g.ntiles + t, gbase = tile * TP;
-    const int n = nroots[tile];
-    const int tx0 = (t % g.ntx) * TW, ty0 = (t / g.ntx) * TH;
-    for (int k = threadIdx.x; k < n; k += NT) {
-        const int l = roots[gbase + k];
-        const int key = (ty0 + (l >> 6)) * g.W + tx0 + (l & 63);
-        const int r = k_find(g, img, P, key);
-        if (r != key) P[gbase + l] = r;
+    for (int64_t tt = blockIdx.x; tt < (int64_t)g.ntiles * g.n; tt += gridDim.x) {
+        const int n = nroots[tt];
+        if (!n) continue;
+        const int img = (int)(tt / g.ntiles), t = (int)(tt % g.ntiles);
+        const size_t gbase = (size_t)tt * TP;
+        const int tx0 = (t % g.ntx) * TW, ty0 = (t / g.ntx) * TH;
+        for (int k = threadIdx.x; k < n; k += NT) {
+            const int l = roots[gbase + k];
+            const int key = (ty0 + (l >> 6)) * g.W + tx0 + (l & 63);
+            const int r = k_find(g, img, P, key);
+            if (r != key) P[gbase + l] = r;
+        }
+    }
+}
+
+// every tile root -> -(slot + 1) of its component: a pixel's slot is two loads
+__global__ __launch_bounds__(NT) void k_ct_finalize(Geo g, const uint16_t *__restrict__ roots,
+                                                     const int *__restrict__ nroots, int *__restrict__ P) {
+    for (int64_t tt = blockIdx.x; tt < (int64_t)g.ntiles * g.n; tt += gridDim.x) {
+        const int n = nroots[tt];
+        if (!n) continue;
+        const int img = (int)(tt / g.ntiles);
+        const size_t gbase = (size_t)tt * TP;
+        for (int k = threadIdx.x; k < n; k += NT) {
+            const int l = roots[gbase + k];
+            const int v = P[gbase + l];
+            if (v >= 0) P[gbase + l] = P[gid_of_key(g, img, v)];
+        }
     }
 }
 
@@ -218,9 +256,11 @@ __global__ __launch_bounds__(NT) void k_ct_collect(Geo g, const uint16_t *__rest
                                                     CtComp *__restrict__ comps, uint8_t *__restrict__ acc,
                                                     uint64_t *__restrict__ fplane, CtCounters *__restrict__ ctr,
                                                     int *__restrict__ img_info, int64_t comp_cap) {
-    const int img = blockIdx.y, t = blockIdx.x;
-    const size_t tile = (size_t)img * g.ntiles + t, gbase = tile * TP;
-    const int n = nroots[tile];
+    for (int64_t tt = blockIdx.x; tt < (int64_t)g.ntiles * g.n; tt += gridDim.x) {
+    const int n = nroots[tt];
+    if (!n) continue;
+    const int img = (int)(tt / g.ntiles), t = (int)(tt % g.ntiles);
+    const size_t gbase = (size_t)tt * TP;
     const int tx0 = (t % g.ntx) * TW, ty0 = (t / g.ntx) * TH;
     for (int k = threadIdx.x; k < n; k += NT) {
         const int l = roots[gbase + k];
@@ -245,14 +285,13 @@ __global__ __launch_bounds__(NT) void k_ct_collect(Geo g, const uint16_t *__rest
         const int y = ty0 + (l >> 6), x = tx0 + (l & 63);
         atomicOr((unsigned long long *)&fplane[((size_t)img * g.H + y) * g.wpr + (x >> 6)], 1ull << (x & 63));
     }
+    }
 }
 
 __device__ __forceinline__ int slot_of_pixel(const Geo &g, const uint16_t *lab, const int *P, int img, int y, int x) {
     const int l = lab[((size_t)img * g.H + y) * g.W + x];
     const int t = (y / TH) * g.ntx + (x >> 6);
-    int v = P[((size_t)img * g.ntiles + t) * TP + l];
-    if (v >= 0) v = P[gid_of_key(g, img, v)];
-    return -v - 1;
+    return -P[((size_t)img * g.ntiles + t) * TP + l] - 1;  // k_ct_finalize: every tile root holds -(slot + 1)
 }
 
 // ---------------------------------------------------------------- border following
@@ -290,15 +329,19 @@ struct TraceCount {
 };
 
 struct TraceWrite {
-    int2 *pts;
-    uint64_t *mv, *mn;  // mark planes of the image (row stride wpr)
+    int2 *pts;          // vertex destination (capacity cap)
+    uint64_t *mv, *mn;  // mark planes of the image (row stride wpr), null: no marks
     int wpr;
+    bool on;            // this lane stores (the wave traces redundantly, lane 0 writes)
+    uint32_t cap;
     uint32_t nv = 0;
     int fx = 0, fy = 0, px = 0, py = 0;
     int64_t a2 = 0;
     int x0 = 1 << 30, y0 = 1 << 30, x1 = -1, y1 = -1;
+    int my = -1, mq = -1;  // marks of one 64-pixel word are OR-ed once per visit of the word
+    unsigned long long bv = 0, bn = 0;
     __device__ void vertex(int x, int y) {
-        pts[nv] = make_int2(x, y);
+        if (on && nv < cap) pts[nv] = make_int2(x, y);
         if (nv == 0) {
             fx = x;
             fy = y;
@@ -313,19 +356,100 @@ struct TraceWrite {
         y1 = max(y1, y);
         nv++;
     }
-    __device__ void mark(int x, int y, bool right) {
-        const size_t w = (size_t)y * wpr + (x >> 6);
-        const unsigned long long b = 1ull << (x & 63);
-        atomicOr((unsigned long long *)&mv[w], b);
-        if (right) atomicOr((unsigned long long *)&mn[w], b);
+    __device__ void flush() {
+        if (on && mv && bv) {
+            const size_t w = (size_t)my * wpr + mq;
+            atomicOr((unsigned long long *)&mv[w], bv);
+            if (bn) atomicOr((unsigned long long *)&mn[w], bn);
+        }
+        bv = bn = 0;
     }
-    __device__ void close() { a2 += (int64_t)px * fy - (int64_t)py * fx; }
+    __device__ void mark(int x, int y, bool right) {
+        if (y != my || (x >> 6) != mq) {
+            flush();
+            my = y;
+            mq = x >> 6;
+        }
+        const unsigned long long b = 1ull << (x & 63);
+        bv |= b;
+        if (right) bn |= b;
+    }
+    __device__ void close() {
+        a2 += (int64_t)px * fy - (int64_t)py * fx;
+        flush();
+    }
+};
+
+// neighbourhood providers: straight from the bit planes (one thread), or from a
+// 64-row x 256-pixel window of them that the whole wave stages in LDS (all lanes run
+// the trace in lockstep; a step that leaves the window -> one cooperative reload), with
+// the 3 x 3 words around the current word cached in registers
+struct NbGlobal {
+    const uint64_t *b;
+    const Geo &g;
+    int img;
+    __device__ uint32_t operator()(int x, int y) { return nbhd(b, g, img, x, y); }
+};
+
+constexpr int kWinRows = 64, kWinWords = 4;
+// wave-uniform copies (the trace state then lives in SGPRs and runs on the scalar ALU)
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+    return ((uint64_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+}
+struct NbWindow {
+    const uint64_t *b;
+    const Geo &g;
+    int img, lane;
+    uint64_t *win;  // kWinRows x kWinWords
+    int wy0 = -(1 << 30), wq0 = 0;
+    int cy = -(1 << 30), cq = 0;
+    uint64_t r0[3], r1[3], r2[3];  // rows cy-1, cy, cy+1 x words cq-1, cq, cq+1
+    __device__ void reload(int q, int y) {
+        wy0 = y - kWinRows / 2;
+        wq0 = q - 1;
+        __syncthreads();
+        const int row = wy0 + lane;
+        const bool rin = (unsigned)row < (unsigned)g.H;
+        const uint64_t *r = b + ((size_t)img * g.H + (rin ? row : 0)) * g.wpr;
+#pragma unroll
+        for (int k = 0; k < kWinWords; k++) {
+            const int qq = wq0 + k;
+            win[lane * kWinWords + k] = (rin && (unsigned)qq < (unsigned)g.wpr) ? r[qq] : 0ull;
+        }
+        __syncthreads();
+    }
+    __device__ static uint32_t bits3(const uint64_t *r, int s) {  // (x-1, x, x+1) as bits 0..2
+        uint32_t v = (uint32_t)((r[1] >> s) & 1ull) << 1;
+        v |= s > 0 ? (uint32_t)((r[1] >> (s - 1)) & 1ull) : (uint32_t)(r[0] >> 63);
+        v |= (s < 63 ? (uint32_t)((r[1] >> (s + 1)) & 1ull) : (uint32_t)(r[2] & 1ull)) << 2;
+        return v;
+    }
+    __device__ uint32_t operator()(int x, int y) {
+        const int q = x >> 6;
+        if (y != cy || q != cq) {
+            if (y - 1 < wy0 || y + 1 >= wy0 + kWinRows || q - 1 < wq0 || q + 1 >= wq0 + kWinWords) reload(q, y);
+            const uint64_t *w = win + (y - 1 - wy0) * kWinWords + (q - 1 - wq0);
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                r0[k] = uni64(w[k]);
+                r1[k] = uni64(w[kWinWords + k]);
+                r2[k] = uni64(w[2 * kWinWords + k]);
+            }
+            cy = y;
+            cq = q;
+        }
+        const int s = x & 63;
+        const uint32_t up = bits3(r0, s), mid = bits3(r1, s), dn = bits3(r2, s);
+        return ((mid >> 2) & 1u) | (((up >> 2) & 1u) << 1) | (((up >> 1) & 1u) << 2) | ((up & 1u) << 3) |
+               ((mid & 1u) << 4) | ((dn & 1u) << 5) | (((dn >> 1) & 1u) << 6) | (((dn >> 2) & 1u) << 7);
+    }
 };
 
 // returns false when the step bound is hit (malformed input; never for a real border)
-template <class F>
-__device__ bool trace_outer(const uint64_t *b, const Geo &g, int img, int x0, int y0, F &f) {
-    uint32_t nb = nbhd(b, g, img, x0, y0);
+template <class NB, class F>
+__device__ bool trace_outer(NB &nbh, const Geo &g, int x0, int y0, F &f) {
+    uint32_t nb = nbh(x0, y0);
     int s = 4;
     do {
         s = (s - 1) & 7;
@@ -340,7 +464,7 @@ __device__ bool trace_outer(const uint64_t *b, const Geo &g, int img, int x0, in
     const int64_t limit = 8ll * g.H * g.W + 16;
     for (int64_t it = 0; it < limit; it++) {
         const int s_end = s;
-        nb = nbhd(b, g, img, x3, y3);
+        nb = nbh(x3, y3);
         // counter-clockwise search from s_end + 1 (OpenCV: while (s < 15) i4 = i3 + d[++s])
         const uint32_t nb2 = nb | (nb << 8);
         const uint32_t cand = (nb2 >> (s_end + 1)) & ((1u << (15 - s_end)) - 1u);
@@ -359,36 +483,54 @@ __device__ bool trace_outer(const uint64_t *b, const Geo &g, int img, int x0, in
     return false;
 }
 
-// one thread per component: count pass (WRITE = false) allocates the vertex range,
-// write pass emits vertices, marks, twice-area and bbox
-template <bool WRITE>
-__global__ __launch_bounds__(NT) void k_ct_trace(const uint64_t *__restrict__ bits, Geo g, CtComp *__restrict__ comps,
+// one wave per component, one pass: vertices go to the block's staging area (exact
+// length known afterwards -> allocate -> copy), marks to the planes; a border longer
+// than the staging area is followed a second time straight into its allocation
+constexpr uint32_t kStage = kCtStage;
+__global__ __launch_bounds__(64) void k_ct_trace(const uint64_t *__restrict__ bits, Geo g, CtComp *__restrict__ comps,
                                                   int64_t comp_cap, int2 *__restrict__ pts, int64_t pts_cap,
-                                                  uint64_t *__restrict__ mv, uint64_t *__restrict__ mn,
-                                                  CtCounters *__restrict__ ctr) {
+                                                  int2 *__restrict__ stage, uint64_t *__restrict__ mv,
+                                                  uint64_t *__restrict__ mn, CtCounters *__restrict__ ctr) {
+    __shared__ uint64_t win[kWinRows * kWinWords];
+    __shared__ unsigned long long s_off;
+    const int lane = threadIdx.x;
     const int64_t ncomp = min((int64_t)ctr->comps, comp_cap);
-    for (int64_t slot = (int64_t)blockIdx.x * NT + threadIdx.x; slot < ncomp; slot += (int64_t)gridDim.x * NT) {
+    int2 *st = stage + (size_t)blockIdx.x * kStage;
+    for (int64_t slot = blockIdx.x; slot < ncomp; slot += gridDim.x) {
         CtComp c = comps[slot];
+        c.key = (uint32_t)__builtin_amdgcn_readfirstlane((int)c.key);
+        c.img = __builtin_amdgcn_readfirstlane(c.img);
         const int y = c.key / g.W, x = c.key - y * g.W;
-        if (!WRITE) {
-            TraceCount f;
-            if (!trace_outer(bits, g, c.img, x, y, f)) atomicOr(&ctr->flags, kCtBadTrace);
-            const unsigned long long off = atomicAdd(&ctr->pts, (unsigned long long)f.nv);
-            c.nv = f.nv;
-            c.off = (uint32_t)off;
-            if (off + f.nv > (unsigned long long)pts_cap) {
-                atomicOr(&ctr->flags, kCtOverflowPts);
-                c.nv = 0;
-                c.off = 0;
+        const size_t pb = (size_t)c.img * g.H * g.wpr;
+        NbWindow nbh{bits, g, c.img, lane, win};
+        TraceWrite f{st, mv + pb, mn + pb, g.wpr, lane == 0, kStage};
+        const bool ok = trace_outer(nbh, g, x, y, f);
+        f.close();
+        if (lane == 0) {
+            if (!ok) atomicOr(&ctr->flags, kCtBadTrace);
+            s_off = atomicAdd(&ctr->pts, (unsigned long long)f.nv);
+        }
+        __threadfence();  // lane 0's staged vertices, read back by every lane below
+        __syncthreads();
+        const unsigned long long off = s_off;
+        const bool fits = off + f.nv <= (unsigned long long)pts_cap;
+        if (fits) {
+            if (f.nv <= kStage) {
+                for (uint32_t i = lane; i < f.nv; i += 64) {
+                    const unsigned long long v = __hip_atomic_load((const unsigned long long *)(st + i),
+                                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    pts[off + i] = *(const int2 *)&v;
+                }
+            } else {
+                NbWindow nb2{bits, g, c.img, lane, win};
+                TraceWrite f2{pts + off, nullptr, nullptr, g.wpr, lane == 0, f.nv};
+                trace_outer(nb2, g, x, y, f2);
             }
-            comps[slot].nv = c.nv;
-            comps[slot].off = c.off;
-        } else {
-            if (ctr->flags & kCtOverflowPts) return;
-            const size_t pb = (size_t)c.img * g.H * g.wpr;
-            TraceWrite f{pts + c.off, mv + pb, mn + pb, g.wpr};
-            trace_outer(bits, g, c.img, x, y, f);
-            f.close();
+        }
+        if (lane == 0) {
+            if (!fits) atomicOr(&ctr->flags, kCtOverflowPts);
+            c.nv = fits ? f.nv : 0;
+            c.off = fits ? (uint32_t)off : 0;
             c.area2 = f.a2;
             c.x0 = (uint16_t)f.x0;
             c.y0 = (uint16_t)f.y0;
@@ -396,6 +538,7 @@ __global__ __launch_bounds__(NT) void k_ct_trace(const uint64_t *__restrict__ bi
             c.y1 = (uint16_t)f.y1;
             comps[slot] = c;
         }
+        __syncthreads();
     }
 }
 
@@ -512,23 +655,42 @@ __global__ __launch_bounds__(64) void k_ct_scan(const uint64_t *__restrict__ bit
     }
     __syncthreads();
     int nref = 0;
+    bool any_quirk = false;  // Q planes are all zero until a border starts off a first pixel
+    // the first window of row y + 1 is loaded while row y is scanned
+    const bool v0 = lane >= 1 && lane - 1 < g.wpr;
+    const size_t o0 = v0 ? lane - 1 : 0;
+    uint64_t n_nz = v0 ? sp.nz[o0] : 0ull, n_mv = v0 ? sp.mv[o0] : 0ull, n_mn = v0 ? sp.mn[o0] : 0ull,
+             n_fb = v0 ? sp.f[o0] : 0ull;
     for (int y = 0; y < g.H; y++) {
         int lnbd = -1;  // pixel position (x) of lnbd on this row, -1 = frame
         int seg = 0;    // first pixel position not yet scanned
+        const uint64_t c_nz = n_nz, c_mv = n_mv, c_mn = n_mn, c_fb = n_fb;
+        if (y + 1 < g.H) {
+            const size_t o = (size_t)(y + 1) * g.wpr + o0;
+            n_nz = v0 ? sp.nz[o] : 0ull;
+            n_mv = v0 ? sp.mv[o] : 0ull;
+            n_mn = v0 ? sp.mn[o] : 0ull;
+            n_fb = v0 ? sp.f[o] : 0ull;
+        }
         for (int w0 = 0; w0 < g.wpr; w0 += 63) {
             const int wk = w0 - 1 + lane;  // lane 0 holds the word left of the window
             const bool valid = wk >= 0 && wk < g.wpr;
             const size_t wi = (size_t)y * g.wpr + (valid ? wk : 0);
-            const uint64_t nz = valid ? sp.nz[wi] : 0ull;
+            const uint64_t nz = w0 == 0 ? c_nz : (valid ? sp.nz[wi] : 0ull);
             if (!__any(nz != 0ull)) {
                 seg = (w0 + 63) * 64;
                 continue;
             }
-            const uint64_t mv = valid ? sp.mv[wi] : 0ull, mn = valid ? sp.mn[wi] : 0ull;
-            const uint64_t fb = valid ? sp.f[wi] : 0ull;
+            const uint64_t mv = w0 == 0 ? c_mv : (valid ? sp.mv[wi] : 0ull);
+            const uint64_t mn = w0 == 0 ? c_mn : (valid ? sp.mn[wi] : 0ull);
+            const uint64_t fb = w0 == 0 ? c_fb : (valid ? sp.f[wi] : 0ull);
             const int wpos = wk * 64;
             for (;;) {
-                const uint64_t qv = valid ? ld_relaxed(sp.qv + wi) : 0ull, qn = valid ? ld_relaxed(sp.qn + wi) : 0ull;
+                uint64_t qv = 0ull, qn = 0ull;
+                if (any_quirk && valid) {
+                    qv = ld_relaxed(sp.qv + wi);
+                    qn = ld_relaxed(sp.qn + wi);
+                }
                 // marks of rejected components are not live
                 uint64_t live = ~0ull;
                 const int nrej = s_rej_n;
@@ -650,7 +812,8 @@ __global__ __launch_bounds__(64) void k_ct_scan(const uint64_t *__restrict__ bit
                         s_bcast[1] = 1;
                         // a border started away from a component's first pixel
                         TraceCount fc;
-                        bool ok = trace_outer(bits, g, img, bpos, y, fc);
+                        NbGlobal nbg{bits, g, img};
+                        bool ok = trace_outer(nbg, g, bpos, y, fc);
                         const unsigned slot = atomicAdd(&ctr->comps, 1u);
                         const unsigned long long off = atomicAdd(&ctr->pts, (unsigned long long)fc.nv);
                         if (!ok) atomicOr(&ctr->flags, kCtBadTrace);
@@ -660,7 +823,7 @@ __global__ __launch_bounds__(64) void k_ct_scan(const uint64_t *__restrict__ bit
                             s_bcast[1] = -1;
                         } else {
                             QuirkWrite fw{pts + off, sp.qv, sp.qn, g.wpr};
-                            trace_outer(bits, g, img, bpos, y, fw);
+                            trace_outer(nbg, g, bpos, y, fw);
                             fw.close();
                             CtComp c;
                             c.key = y * g.W + bpos;
@@ -685,6 +848,7 @@ __global__ __launch_bounds__(64) void k_ct_scan(const uint64_t *__restrict__ bit
                 if (kind < 0) return;
                 if (kind == 1) {
                     nref++;
+                    any_quirk = true;
                     atomicAdd(&ctr->quirks, 1u);
                 }
                 seg = bpos + 1;
@@ -747,10 +911,14 @@ __global__ __launch_bounds__(1024) void k_ct_bases(int n, int *__restrict__ img_
 }
 
 // ---------------------------------------------------------------- geometry
-struct GeoLds {
+constexpr int kDpOut = 1024;  // Douglas-Peucker output points kept in LDS
+struct GeoLds {  // ~49 KB: three waves per CU
     int2 stack[kDpStack];
-    uint32_t a[2 * kHullCols + 2];  // DP output / column minima+maxima / hull stack
-    uint32_t c[2 * kHullCols];  // hull candidates
+    uint32_t dpo[kDpOut];              // Douglas-Peucker output (x << 16 | y)
+    uint32_t col[kHullCols];           // per-column y extreme, then the merged hull chain
+    uint32_t ch[kHullCols + 64];       // per-lane chunk chains
+    int nl[64];
+    int2 pts[kPtsLds];
     int flags;
 };
 
@@ -758,18 +926,19 @@ __device__ __forceinline__ double wave_sum_d(double v) {
     for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
     return v;
 }
-
-// (d, k) argmax, earliest k on ties
-__device__ __forceinline__ void wave_argmax(double &d, int &k) {
-    for (int o = 32; o >= 1; o >>= 1) {
-        const double d2 = __shfl_xor(d, o);
-        const int k2 = __shfl_xor(k, o);
-        if (d2 > d || (d2 == d && k2 < k)) {
-            d = d2;
-            k = k2;
-        }
-    }
+__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return v;
 }
+// max of (d << 28 | (2^28 - 1 - k)): the largest d, earliest k on ties (d < 2^36, k < 2^28)
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+    for (int o = 32; o >= 1; o >>= 1) {
+        const uint64_t w = __shfl_xor(v, o);
+        v = w > v ? w : v;
+    }
+    return v;
+}
+constexpr uint64_t kKMask = (1ull << 28) - 1;
 
 __device__ __forceinline__ double perimeter_of(const int2 *p, int n, int lane) {
     if (n <= 1) return 0.0;
@@ -783,7 +952,8 @@ __device__ __forceinline__ double perimeter_of(const int2 *p, int n, int lane) {
 }
 
 // cv::approxPolyDP(closed) vertex count, OpenCV's iterative Douglas-Peucker
-// (contours.cpp dp_vertex_count): the farthest-point scans run across the wave
+// (contours.cpp dp_vertex_count): the farthest-point scans run across the wave; the
+// distances are exact integers (|coordinates| < 2^16, widths < 2^12)
 __device__ int dp_count(const int2 *p, int count, double eps, GeoLds &sm, int lane) {
     if (count == 0) return 0;
     eps *= eps;
@@ -794,19 +964,19 @@ __device__ int dp_count(const int2 *p, int count, double eps, GeoLds &sm, int la
         const int2 s0 = p[pos];
         sx = s0.x;
         sy = s0.y;
-        double best = 0.0;
-        int bk = 0x7fffffff;
+        uint64_t best = 0;
         for (int j = 1 + lane; j < count; j += 64) {
-            const int2 q = p[(pos + j) % count];
-            const double dx = q.x - sx, dy = q.y - sy, d = dx * dx + dy * dy;
-            if (d > best) {
-                best = d;
-                bk = j;
-            }
+            int idx = pos + j;
+            if (idx >= count) idx -= count;
+            const int2 q = p[idx];
+            const int64_t dx = q.x - sx, dy = q.y - sy, d = dx * dx + dy * dy;
+            const uint64_t key = ((uint64_t)d << 28) | (kKMask - (uint64_t)j);
+            if (d > 0 && key > best) best = key;
         }
-        wave_argmax(best, bk);
-        if (best > 0.0) rs_start = bk;
-        le_eps = best <= eps;
+        best = wave_max_u64(best);
+        const uint64_t dmax = best >> 28;
+        if (dmax > 0) rs_start = (int)(kKMask - (best & kKMask));
+        le_eps = (double)dmax <= eps;
     }
     int nout = 0, top = 0;
     if (!le_eps) {
@@ -817,7 +987,7 @@ __device__ int dp_count(const int2 *p, int count, double eps, GeoLds &sm, int la
         }
         top = 2;
     } else {
-        if (lane == 0) sm.a[0] = ((uint32_t)sx << 16) | (uint32_t)sy;
+        if (lane == 0) sm.dpo[0] = ((uint32_t)sx << 16) | (uint32_t)sy;
         nout = 1;
     }
     __syncthreads();
@@ -825,33 +995,37 @@ __device__ int dp_count(const int2 *p, int count, double eps, GeoLds &sm, int la
         const int2 sl = sm.stack[--top];
         const int sstart = sl.x, send = sl.y;
         const int2 e = p[send], s0 = p[sstart];
-        const int m = (send - sstart - 1 + 2 * count) % count;  // points strictly between
+        int m = send - sstart - 1;  // points strictly between (cyclic)
+        if (m < 0) m += count;
         bool ok = true;
         int split = 0;
         if (m > 0) {
-            const double dx = e.x - s0.x, dy = e.y - s0.y;
-            double best = 0.0;
-            int bk = 0x7fffffff;
+            const int dx = e.x - s0.x, dy = e.y - s0.y;
+            uint64_t best = 0;
             for (int j = 1 + lane; j <= m; j += 64) {
-                const int idx = (sstart + j) % count;
+                int idx = sstart + j;
+                if (idx >= count) idx -= count;
                 const int2 q = p[idx];
-                const double d = fabs((q.y - s0.y) * dx - (q.x - s0.x) * dy);
-                if (d > best) {
-                    best = d;
-                    bk = j;
-                }
+                int64_t d = (int64_t)(q.y - s0.y) * dx - (int64_t)(q.x - s0.x) * dy;
+                d = d < 0 ? -d : d;
+                const uint64_t key = ((uint64_t)d << 28) | (kKMask - (uint64_t)j);
+                if (d > 0 && key > best) best = key;
             }
-            wave_argmax(best, bk);
-            if (best > 0.0) split = (sstart + bk) % count;
-            ok = best * best <= eps * (dx * dx + dy * dy);
+            best = wave_max_u64(best);
+            const double dmax = (double)(best >> 28);
+            if (best >> 28) {
+                split = sstart + (int)(kKMask - (best & kKMask));
+                if (split >= count) split -= count;
+            }
+            ok = dmax * dmax <= eps * ((double)dx * dx + (double)dy * dy);
         }
         __syncthreads();
         if (ok) {
-            if (nout >= 2 * kHullCols) {
+            if (nout >= kDpOut) {
                 if (lane == 0) sm.flags |= 1;
                 return 0;
             }
-            if (lane == 0) sm.a[nout] = ((uint32_t)s0.x << 16) | (uint32_t)s0.y;
+            if (lane == 0) sm.dpo[nout] = ((uint32_t)s0.x << 16) | (uint32_t)s0.y;
             nout++;
         } else {
             if (top + 2 > kDpStack) {
@@ -871,7 +1045,7 @@ __device__ int dp_count(const int2 *p, int count, double eps, GeoLds &sm, int la
     int newc = nout;
     if (lane == 0) {
         const int cnt = nout;
-        uint32_t *dst = sm.a;
+        uint32_t *dst = sm.dpo;
         auto X = [](uint32_t v) { return (int)(v >> 16); };
         auto Y = [](uint32_t v) { return (int)(v & 0xffffu); };
         int rp = cnt - 1;
@@ -913,70 +1087,87 @@ __device__ int dp_count(const int2 *p, int count, double eps, GeoLds &sm, int la
     return newc;
 }
 
-// convex-hull area: the hull of the contour = the hull of each column's extreme
-// points; Andrew's monotone chain over those (x ascending, y ascending), serial in LDS
-__device__ double hull_area_of(const int2 *p, int n, int x0, int width, GeoLds &sm, int lane) {
-    if (n < 3) return 0.0;
-    uint32_t *ymin = sm.a, *ymax = sm.a + kHullCols;
-    for (int i = lane; i < width; i += 64) {
-        ymin[i] = 0xffffffffu;
-        ymax[i] = 0u;
-    }
+// One convex chain of the hull: UPPER = false -> the chain over each column's minimum y
+// (x ascending), UPPER = true -> over each column's maximum y (x descending), both with
+// Andrew's "pop while cross <= 0" rule.  Each lane first reduces its own run of columns
+// to its chain (points off it cannot be on the hull), lane 0 then merges the chunks.
+// Returns the chain's shoelace sum over its edges; *first / *last are its end points.
+template <bool UPPER>
+__device__ int64_t hull_chain(const int2 *p, int n, int x0, int width, GeoLds &sm, int lane, uint32_t *first,
+                              uint32_t *last) {
+    auto X = [](uint32_t v) { return (int)(v >> 16); };
+    auto Y = [](uint32_t v) { return (int)(v & 0xffffu); };
+    auto cross = [&](uint32_t o, uint32_t a, uint32_t b) {  // 32 x 32 -> 64-bit products
+        return (int64_t)(X(a) - X(o)) * (Y(b) - Y(o)) - (int64_t)(Y(a) - Y(o)) * (X(b) - X(o));
+    };
+    for (int i = lane; i < width; i += 64) sm.col[i] = UPPER ? 0u : 0xffffffffu;
     __syncthreads();
     for (int i = lane; i < n; i += 64) {
         const int2 q = p[i];
-        atomicMin(&ymin[q.x - x0], (uint32_t)q.y);
-        atomicMax(&ymax[q.x - x0], (uint32_t)q.y + 1u);
+        if (UPPER) atomicMax(&sm.col[q.x - x0], (uint32_t)q.y + 1u);
+        else atomicMin(&sm.col[q.x - x0], (uint32_t)q.y);
     }
     __syncthreads();
-    // compact the candidates in (x, y) order
-    int m = 0;
-    for (int c0 = 0; c0 < width; c0 += 64) {
-        const int i = c0 + lane;
-        int cnt = 0;
-        uint32_t lo = 0, hi = 0;
-        if (i < width && ymin[i] != 0xffffffffu) {
-            lo = ymin[i];
-            hi = ymax[i] - 1u;
-            cnt = hi != lo ? 2 : 1;
+    {
+        const int clo = (int)((int64_t)width * lane / 64), chi = (int)((int64_t)width * (lane + 1) / 64);
+        uint32_t *C = sm.ch + clo + lane;  // room for chi - clo + 1 entries
+        int k = 0;
+        for (int t = 0; t < chi - clo; t++) {
+            const int c = UPPER ? chi - 1 - t : clo + t;
+            const uint32_t v = sm.col[c];
+            if (UPPER ? v == 0u : v == 0xffffffffu) continue;
+            const uint32_t q = ((uint32_t)(x0 + c) << 16) | (UPPER ? v - 1u : v);
+            while (k >= 2 && cross(C[k - 2], C[k - 1], q) <= 0) k--;
+            C[k++] = q;
         }
-        const int pre = wave_excl_sum(cnt, lane);
-        const uint32_t xx = (uint32_t)(x0 + i);
-        if (cnt >= 1) sm.c[m + pre] = (xx << 16) | lo;
-        if (cnt == 2) sm.c[m + pre + 1] = (xx << 16) | hi;
-        m += __shfl(pre + cnt, 63);
+        sm.nl[lane] = k;
     }
     __syncthreads();
+    int64_t sum = 0;
+    if (lane == 0) {
+        uint32_t *H = sm.col;  // the column extremes are dead now
+        int k = 0;
+        uint32_t t1 = 0, t2 = 0;  // H[k - 1], H[k - 2]
+        for (int li = 0; li < 64; li++) {
+            const int l = UPPER ? 63 - li : li;
+            const int clo = (int)((int64_t)width * l / 64);
+            const uint32_t *C = sm.ch + clo + l;
+            for (int j = 0, nj = sm.nl[l]; j < nj; j++) {
+                const uint32_t q = C[j];
+                while (k >= 2 && cross(t2, t1, q) <= 0) {
+                    k--;
+                    t1 = t2;
+                    t2 = k >= 2 ? H[k - 2] : 0u;
+                }
+                H[k++] = q;
+                t2 = t1;
+                t1 = q;
+            }
+        }
+        for (int i = 1; i < k; i++)
+            sum += (int64_t)X(H[i - 1]) * Y(H[i]) - (int64_t)Y(H[i - 1]) * X(H[i]);
+        *first = H[0];
+        *last = H[k - 1];
+    }
+    __syncthreads();
+    return sum;
+}
+
+// convex-hull area of the contour: lower chain (column minima) + upper chain (column
+// maxima) closed by the two vertical sides; exact integer shoelace
+__device__ double hull_area_of(const int2 *p, int n, int x0, int width, GeoLds &sm, int lane) {
+    if (n < 3) return 0.0;
+    uint32_t lf = 0, ll = 0, uf = 0, ul = 0;
+    const int64_t sl = hull_chain<false>(p, n, x0, width, sm, lane, &lf, &ll);
+    const int64_t su = hull_chain<true>(p, n, x0, width, sm, lane, &uf, &ul);
     double area = 0.0;
     if (lane == 0) {
-        uint32_t *H = sm.a;  // the column arrays are dead now
         auto X = [](uint32_t v) { return (int64_t)(v >> 16); };
         auto Y = [](uint32_t v) { return (int64_t)(v & 0xffffu); };
-        auto cross = [&](uint32_t o, uint32_t a, uint32_t b) {
-            return (X(a) - X(o)) * (Y(b) - Y(o)) - (Y(a) - Y(o)) * (X(b) - X(o));
-        };
-        int k = 0;
-        for (int i = 0; i < m; i++) {
-            while (k >= 2 && cross(H[k - 2], H[k - 1], sm.c[i]) <= 0) k--;
-            H[k++] = sm.c[i];
-        }
-        for (int i = m - 2, t = k + 1; i >= 0; i--) {
-            while (k >= t && cross(H[k - 2], H[k - 1], sm.c[i]) <= 0) k--;
-            H[k++] = sm.c[i];
-        }
-        const int mm = k - 1;
-        if (mm >= 3) {
-            double a = 0.0;
-            for (int i = 0; i < mm; i++) {
-                const int j = (i + mm - 1) % mm;
-                a += (double)X(H[j]) * (double)Y(H[i]) - (double)Y(H[j]) * (double)X(H[i]);
-            }
-            area = fabs(a * 0.5);
-        }
+        const int64_t a2 = sl + su + (X(ll) * Y(uf) - Y(ll) * X(uf)) + (X(ul) * Y(lf) - Y(ul) * X(lf));
+        area = fabs((double)a2 * 0.5);
     }
-    area = __shfl(area, 0);
-    __syncthreads();
-    return area;
+    return __shfl(area, 0);
 }
 
 // grid (G, n), one wave per block: the kept contours of image blockIdx.y
@@ -994,8 +1185,13 @@ __global__ __launch_bounds__(64) void k_ct_shapes(const CtComp *__restrict__ com
         const int2 r = refs[base + i];
         if (r.y < 0) continue;
         const CtComp c = comps[r.x];
-        const int2 *p = pts + c.off;
         const int n = (int)c.nv;
+        const int2 *p = pts + c.off;
+        if (n <= kPtsLds) {  // stage the vertices in LDS
+            for (int i = lane; i < n; i += 64) sm.pts[i] = p[i];
+            __syncthreads();
+            p = sm.pts;
+        }
         const double area = fabs((double)c.area2 * 0.5);
         const double per = perimeter_of(p, n, lane);
         const int width = c.x1 - c.x0 + 1;
@@ -1036,6 +1232,7 @@ __global__ __launch_bounds__(64) void k_ct_shapes(const CtComp *__restrict__ com
             s.area = area;
             shapes[sbase + r.y] = s;
         }
+        __syncthreads();
     }
 }
 
@@ -1056,23 +1253,21 @@ size_t contours_plane_words(int n, int h, int w) { return (size_t)n * h * words_
 
 hipError_t launch_contours(const uint64_t *bits, int n, int h, int w, const CtWork &wk, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    Geo g{h, w, words_per_row(w), tiles_x(w), tiles_x(w) * tiles_y(h)};
+    Geo g{h, w, words_per_row(w), tiles_x(w), tiles_x(w) * tiles_y(h), n};
     const size_t pw = contours_plane_words(n, h, w);
     hipError_t e;
     if ((e = hipMemsetAsync(wk.planes, 0, sizeof(uint64_t) * pw * 5, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(wk.ctr, 0, sizeof(CtCounters), s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(wk.img_info, 0, sizeof(int) * kCtInfo * n, s)) != hipSuccess) return e;
-    dim3 grid(g.ntiles, n);
+    const dim3 grid((unsigned)std::min<int64_t>((int64_t)g.ntiles * n, 65536));  // tile loops
     hipLaunchKernelGGL(k_ct_local, grid, dim3(NT), 0, s, bits, g, wk.lab, wk.parent, wk.roots, wk.nroots);
-    hipLaunchKernelGGL(k_ct_border, grid, dim3(128), 0, s, bits, g, wk.lab, wk.parent);
+    hipLaunchKernelGGL(k_ct_border, grid, dim3(128), 0, s, bits, g, wk.lab, wk.nroots, wk.parent);
     hipLaunchKernelGGL(k_ct_flatten, grid, dim3(NT), 0, s, g, wk.roots, wk.nroots, wk.parent);
     hipLaunchKernelGGL(k_ct_collect, grid, dim3(NT), 0, s, g, wk.roots, wk.nroots, wk.parent, wk.comps, wk.acc,
                        wk.planes + 4 * pw, wk.ctr, wk.img_info, wk.caps.comps);
-    const int tblocks = (int)std::min<int64_t>((wk.caps.comps + NT - 1) / NT, 4096);
-    hipLaunchKernelGGL(k_ct_trace<false>, dim3(tblocks), dim3(NT), 0, s, bits, g, wk.comps, wk.caps.comps, wk.pts,
-                       wk.caps.pts, wk.planes, wk.planes + pw, wk.ctr);
-    hipLaunchKernelGGL(k_ct_trace<true>, dim3(tblocks), dim3(NT), 0, s, bits, g, wk.comps, wk.caps.comps, wk.pts,
-                       wk.caps.pts, wk.planes, wk.planes + pw, wk.ctr);
+    hipLaunchKernelGGL(k_ct_finalize, grid, dim3(NT), 0, s, g, wk.roots, wk.nroots, wk.parent);
+    hipLaunchKernelGGL(k_ct_trace, dim3(kCtTraceBlocks), dim3(64), 0, s, bits, g, wk.comps, wk.caps.comps, wk.pts,
+                       wk.caps.pts, wk.stage, wk.planes, wk.planes + pw, wk.ctr);
     hipLaunchKernelGGL(k_ct_scan, dim3(n), dim3(64), 0, s, bits, g, wk.lab, wk.parent, wk.planes, pw, wk.comps,
                        wk.caps.comps, wk.acc, wk.pts, wk.caps.pts, wk.refs, wk.caps.refs, wk.ctr, wk.img_info);
     hipLaunchKernelGGL(k_ct_bases, dim3(1), dim3(1024), 0, s, n, wk.img_info, wk.ctr, wk.caps.shapes);

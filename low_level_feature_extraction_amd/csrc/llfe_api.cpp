@@ -216,7 +216,7 @@ struct Work {
     DevBuf<uint64_t> d_ct_planes;
     DevBuf<CtComp> d_ct_comps;
     DevBuf<uint8_t> d_ct_acc;
-    DevBuf<int2> d_ct_pts, d_ct_refs;
+    DevBuf<int2> d_ct_pts, d_ct_refs, d_ct_stage;
     DevBuf<CtCounters> d_ct_ctr;
     DevBuf<int> d_ct_info;
     DevBuf<llfe_shape> d_ct_shapes;
@@ -368,7 +368,11 @@ struct llfe_ctx {
     HostBuf<uint64_t> h_bits_s[2];
     // GPU contours: per-image (components, ref base, contours, kept, shape base),
     // counters and shape records of each slot
-    bool gpu_contours = true;  // LLFE_CONTOURS=host: contours on the host thread pool
+    // contours on the GPU (contours_gpu.hip) or on the host pool from the D2H'd mask
+    // (default: the host pool runs them while the GPU is in k-means, which measured
+    // faster on one MI355X; LLFE_CONTOURS=gpu or llfe_set_contour_mode switch)
+    bool gpu_contours = false;
+    bool slot_gpu_ct[2] = {false, false};  // mode each in-flight slot was enqueued with
     HostBuf<int> h_ct_info_s[2];
     HostBuf<CtCounters> h_ct_ctr_s[2];
     HostBuf<llfe_shape> h_ct_shapes_s[2];
@@ -480,11 +484,12 @@ int run_contours(llfe_ctx *ctx, Work &W, int n, int h, int w, const uint64_t *bi
     HIPCHK(ctx, W.d_ct_acc.ensure(c.comps));
     HIPCHK(ctx, W.d_ct_pts.ensure(c.pts));
     HIPCHK(ctx, W.d_ct_refs.ensure(c.refs));
+    HIPCHK(ctx, W.d_ct_stage.ensure((size_t)kCtTraceBlocks * kCtStage));
     HIPCHK(ctx, W.d_ct_ctr.ensure(1));
     HIPCHK(ctx, W.d_ct_info.ensure((size_t)n * kCtInfo));
     HIPCHK(ctx, W.d_ct_shapes.ensure(c.shapes));
     CtWork wk{W.d_lab.p, W.d_parent.p, W.d_roots.p, W.d_nroots.p, W.d_ct_planes.p, W.d_ct_comps.p, W.d_ct_acc.p,
-              W.d_ct_pts.p, W.d_ct_refs.p, W.d_ct_ctr.p, W.d_ct_info.p, W.d_ct_shapes.p, c};
+              W.d_ct_pts.p, W.d_ct_refs.p, W.d_ct_stage.p, W.d_ct_ctr.p, W.d_ct_info.p, W.d_ct_shapes.p, c};
     // algorithmic bytes: mask bits read by components + scan, labels written and read
     TIMED(ctx, s, "k_contours", (double)n * h * w * (0.25 + 4.0), launch_contours(bits, n, h, w, wk, s));
     return LLFE_OK;
@@ -642,7 +647,8 @@ int enqueue_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_
     }
     // shapes + shadows go to the host (event mask_done) while the GPU is still in this
     // chunk's colour stage, so contour tracing overlaps k-means
-    const bool gpu_ct = ctx->gpu_contours && w <= kCtMaxWidth;
+    const bool gpu_ct = ctx->gpu_contours && w <= kCtMaxWidth && h <= kCtMaxHeight;
+    ctx->slot_gpu_ct[slot] = gpu_ct;
     if (want_shp) {
         HIPCHK(ctx, W.d_bits.ensure((size_t)n * h * wpr));
         if (!gpu_ct) HIPCHK(ctx, ctx->h_bits_s[slot].ensure((size_t)n * h * wpr));
@@ -763,7 +769,7 @@ int finish_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, int i0, 
             r.shadow_count = sh[n + i];
         }
     }
-    if (want_shp && ctx->gpu_contours && w <= kCtMaxWidth) {
+    if (want_shp && ctx->slot_gpu_ct[slot]) {
         int rc = gpu_shapes_of_chunk(ctx, b, i0, n, slot, results, shapes, shape_capacity, total_shapes);
         if (rc) return rc;
     } else if (want_shp) {
@@ -827,15 +833,24 @@ int llfe_init(int device, llfe_ctx **out) {
             llfe_destroy(c);
             return LLFE_ERR_HIP;
         }
-    for (hipStream_t *st : {&c->streams[0], &c->streams[1], &c->col_streams[0], &c->col_streams[1], &c->copy_stream})
-        if (hipStreamCreateWithFlags(st, hipStreamNonBlocking) != hipSuccess) {
+    // LLFE_SHAPES_PRIORITY=1: the shapes / shadows streams get the higher priority
+    // (k-means on the colour stream fills every CU's register file; the GPU contour
+    // kernels then take the slots its retiring workgroups free).  Measured neutral.
+    int prio_lo = 0, prio_hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    if (const char *sp = getenv("LLFE_SHAPES_PRIORITY"); !sp || atoi(sp) != 1) prio_hi = prio_lo;
+    for (hipStream_t *st : {&c->streams[0], &c->streams[1], &c->col_streams[0], &c->col_streams[1], &c->copy_stream}) {
+        const int prio = (st == &c->streams[0] || st == &c->streams[1]) ? prio_hi : prio_lo;
+        if (hipStreamCreateWithPriority(st, hipStreamNonBlocking, prio) != hipSuccess) {
             llfe_destroy(c);
             return LLFE_ERR_HIP;
         }
+    }
     if (const char *ch = getenv("LLFE_CHUNK"); ch && atoi(ch) > 0) c->chunk = std::min(atoi(ch), kMaxKmeansBatch);
     if (const char *ns = getenv("LLFE_STREAMS"); ns && atoi(ns) == 2) c->nstreams = 2;
     if (const char *sa = getenv("LLFE_SHAPES_AFTER_FRONT"); sa && atoi(sa) == 1) c->shapes_after_front = true;
-    if (const char *cm = getenv("LLFE_CONTOURS"); cm && !strcmp(cm, "host")) c->gpu_contours = false;
+    if (const char *cm = getenv("LLFE_CONTOURS"); cm && !strcmp(cm, "gpu")) c->gpu_contours = true;
+    if (const char *cc = getenv("LLFE_CONCURRENT"); cc && atoi(cc) == 0) c->concurrent = false;
     gauss_kernel_f32(11, c->sp.k11);
     c->pool = new Pool(default_threads() - 1);
     int nt = c->pool->size() + 1;
@@ -868,6 +883,14 @@ int llfe_set_profiling(llfe_ctx *ctx, int enable) {
     if (!ctx) return LLFE_ERR_INVALID;
     if (enable) ctx->prof.reset();
     ctx->prof.on = enable != 0;
+    return LLFE_OK;
+}
+
+int llfe_set_contour_mode(llfe_ctx *ctx, int mode) {
+    if (!ctx || (mode != LLFE_CONTOURS_HOST && mode != LLFE_CONTOURS_GPU)) return LLFE_ERR_INVALID;
+    if (ctx->inflight[0].busy || ctx->inflight[1].busy)
+        return ctx->fail(LLFE_ERR_INVALID, "llfe_set_contour_mode with submitted batches not yet collected");
+    ctx->gpu_contours = mode == LLFE_CONTOURS_GPU;
     return LLFE_OK;
 }
 
@@ -1302,7 +1325,9 @@ namespace {
 // capacities grown until nothing overflows).  Leaves the results in W.d_ct_* and
 // slot 0's host copies.
 int gpu_contours_of_masks(llfe_ctx *ctx, const uint8_t *masks, int n, int h, int w) {
-    if (w > kCtMaxWidth) return ctx->fail(LLFE_ERR_UNSUPPORTED, "GPU contours need width <= %d", kCtMaxWidth);
+    if (w > kCtMaxWidth || h > kCtMaxHeight)
+        return ctx->fail(LLFE_ERR_UNSUPPORTED, "GPU contours need width <= %d and height <= %d", kCtMaxWidth,
+                         kCtMaxHeight);
     HIPCHK(ctx, hipSetDevice(ctx->device));
     HIPCHK(ctx, hipDeviceSynchronize());
     Work &W = ctx->ws[0];

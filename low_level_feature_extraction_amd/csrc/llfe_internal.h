@@ -71,7 +71,9 @@ constexpr unsigned kCtBadTrace = 16, kCtTooWide = 32, kCtDpOverflow = 64;
 constexpr unsigned kCtOverflowMask = 15;  // capacity flags: the host grows and reruns
 constexpr int kCtInfo = 5;       // per image: components, ref base, contours, kept, shape base
 constexpr int kCtQuirkCap = 64;  // borders per image started away from a first pixel
-constexpr int kCtMaxWidth = 4096;  // GPU contours: widest image (hull columns in LDS)
+constexpr int kCtTraceBlocks = 2048, kCtStage = 8192;  // border-following waves, vertices staged per wave
+constexpr int kCtMaxWidth = 4096;   // GPU contours: widest image (hull columns in LDS)
+constexpr int kCtMaxHeight = 65535; // and tallest (16-bit y in the hull candidates)
 struct CtCaps {
     int64_t comps, pts, refs, shapes;
 };
@@ -85,6 +87,7 @@ struct CtWork {
     uint8_t *acc;      // caps.comps
     int2 *pts;         // caps.pts
     int2 *refs;        // caps.refs: (component slot, shape index or -1) in start order
+    int2 *stage;       // kCtTraceBlocks * kCtStage vertex staging
     CtCounters *ctr;
     int *img_info;     // n * kCtInfo
     llfe_shape *shapes;  // caps.shapes

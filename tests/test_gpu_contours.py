@@ -135,3 +135,37 @@ def test_shapes_gpu_on_oracle_masks_of_synthetic_images(backend, orc, kind, seed
     want = orc.analyze_shapes(img)["shapes"]
     assert got[0] == want
     assert ncont[0] == len(orc.find_contours_external(m))
+
+
+@pytest.mark.parametrize("h,w,n", [(270, 480, 6), (1080, 1920, 4)])
+def test_batch_gpu_contour_mode_matches_host_mode_and_oracle(backend, orc, h, w, n):
+    # llfe_process_batch with LLFE_CONTOURS_GPU: same shapes / n_contours as the host pool
+    from low_level_feature_extraction_amd.synth import synth_numpy
+
+    x = np.stack([synth_numpy(i, h, w, kind="ui" if i % 2 == 0 else "photo") for i in range(n)])
+    try:
+        backend.set_contour_mode("gpu")
+        got = backend.process(x, ("shapes", "shadows"), seed=5)
+    finally:
+        backend.set_contour_mode("host")
+    ref = backend.process(x, ("shapes", "shadows"), seed=5)
+    for i in range(n):
+        assert got[i].shapes == ref[i].shapes == orc.analyze_shapes(x[i])["shapes"]
+        assert got[i].n_contours == ref[i].n_contours
+        assert (got[i].shadow_sum, got[i].shadow_count) == (ref[i].shadow_sum, ref[i].shadow_count)
+
+
+def test_batch_gpu_contour_mode_capacity_regrowth(backend, orc):
+    # ~880 shapes in one image: more than the default per-pass shape capacity, so the
+    # chunk is redone with grown capacities
+    x = np.full((1, 540, 960, 3), 255, np.uint8)
+    for y in range(6, 530, 24):
+        for xx in range(6, 950, 24):
+            x[0, y:y + 12, xx:xx + 12] = 0
+    try:
+        backend.set_contour_mode("gpu")
+        r = backend.process(x, ("shapes",))[0]
+    finally:
+        backend.set_contour_mode("host")
+    assert r.shapes == orc.analyze_shapes(x[0])["shapes"]
+    assert len(r.shapes) > 320
