@@ -87,15 +87,22 @@ __global__ __launch_bounds__(NT) void k_ccl_local(const uint8_t *__restrict__ cl
     const int tx0 = (t % ntx) * TW, ty0 = (t / ntx) * TH;
     const uint8_t *c = cls + (size_t)img * H * W;
     uint8_t v[TP / NT];
+    bool any = false;
 #pragma unroll
     for (int k = 0; k < TP / NT; k++) {
         int i = tid + k * NT, ly = i >> 6, lx = i & 63, y = ty0 + ly, x = tx0 + lx;
         v[k] = (y < H && x < W) ? c[(size_t)y * W + x] : 1;
         L[i] = v[k] != 1 ? i : -1;
+        any |= v[k] != 1;
     }
     if (tid < TP / 32) sflag[tid] = 0;
     if (tid == 0) cnt = 0;
-    __syncthreads();
+    // most tiles hold no Canny candidate (85 % over the ui / photo mix): no roots, and
+    // the later kernels skip the tile on nroots == 0
+    if (!__syncthreads_or(any)) {
+        if (tid == 0) nroots[(size_t)img * ntiles + t] = 0;
+        return;
+    }
 #pragma unroll
     for (int k = 0; k < TP / NT; k++) {
         if (v[k] == 1) continue;
@@ -142,9 +149,11 @@ __device__ __forceinline__ int gid_of(const uint16_t *lab, int img, int H, int W
 
 // grid (ntiles, n): threads 0..31 right column, 32..95 bottom row of the tile
 __global__ __launch_bounds__(128) void k_ccl_border(const uint8_t *__restrict__ cls, const uint16_t *__restrict__ lab,
-                                                    int H, int W, int ntx, int nty, int *__restrict__ parent) {
+                                                    int H, int W, int ntx, int nty, const int *__restrict__ nroots,
+                                                    int *__restrict__ parent) {
     const int tid = threadIdx.x, img = blockIdx.y, t = blockIdx.x;
     const int ntiles = ntx * nty;
+    if (!nroots[(size_t)img * ntiles + t]) return;  // no candidates on this tile's seams
     const int tx0 = (t % ntx) * TW, ty0 = (t / ntx) * TH;
     const uint8_t *c = cls + (size_t)img * H * W;
     int x, y;
@@ -193,6 +202,7 @@ __global__ __launch_bounds__(NT) void k_ccl_strong(int ntiles, const uint16_t *_
     __shared__ uint32_t rs[TP / 32];
     const size_t tile = (size_t)blockIdx.y * ntiles + blockIdx.x, gbase = tile * TP;
     const int tid = threadIdx.x, n = nroots[tile];
+    if (!n) return;  // k_ccl_edge does not read this tile's bits
     if (tid < TP / 32) rs[tid] = 0;
     __syncthreads();
     for (int k = tid; k < n; k += NT) {
@@ -206,14 +216,23 @@ __global__ __launch_bounds__(NT) void k_ccl_strong(int ntiles, const uint16_t *_
 // per tile, no halo: edge = strong || (maybe && strong local root); one wave per
 // 64-pixel row segment packs the row's edge word with __ballot
 __global__ __launch_bounds__(NT) void k_ccl_edge(const uint8_t *__restrict__ cls, const uint16_t *__restrict__ lab,
-                                                  int H, int W, int ntx, int nty, const uint32_t *__restrict__ tstrong,
-                                                  uint64_t *__restrict__ ebits) {
+                                                  int H, int W, int ntx, int nty, const int *__restrict__ nroots,
+                                                  const uint32_t *__restrict__ tstrong, uint64_t *__restrict__ ebits) {
     __shared__ uint32_t rs[TP / 32];
     constexpr int RPW = TH / (NT / 64);  // rows per wave
     const int tid = threadIdx.x, img = blockIdx.y, t = blockIdx.x, lane = tid & 63, wid = tid >> 6;
     const int ntiles = ntx * nty;
     const int tx0 = (t % ntx) * TW, ty0 = (t / ntx) * TH, x = tx0 + lane;
     const size_t tile = (size_t)img * ntiles + t;
+    const int wpr = (W + 63) / 64;
+    if (!nroots[tile]) {  // every pixel suppressed: zero edge words, no class / label reads
+        if (lane == 0)
+            for (int r = 0; r < RPW; r++) {
+                const int y = ty0 + wid + r * (NT / 64);
+                if (y < H) ebits[((size_t)img * H + y) * wpr + (tx0 >> 6)] = 0ull;
+            }
+        return;
+    }
     const uint8_t *c = cls + (size_t)img * H * W;
     const uint16_t *lb = lab + (size_t)img * H * W;
     uint32_t v[RPW], l[RPW];
@@ -226,7 +245,6 @@ __global__ __launch_bounds__(NT) void k_ccl_edge(const uint8_t *__restrict__ cls
     }
     if (tid < TP / 32) rs[tid] = tstrong[tile * (TP / 32) + tid];
     __syncthreads();
-    const int wpr = (W + 63) / 64;
 #pragma unroll
     for (int r = 0; r < RPW; r++) {
         const int y = ty0 + wid + r * (NT / 64);
@@ -274,11 +292,11 @@ hipError_t launch_hysteresis_dilate(const uint8_t *cls, int n, int h, int w, con
     dim3 grid(ntiles, n);
     hipLaunchKernelGGL(k_ccl_local, grid, dim3(NT), 0, s, cls, h, w, ntx, nty, wk.lab, wk.parent, wk.sroot, wk.roots,
                        wk.nroots);
-    hipLaunchKernelGGL(k_ccl_border, grid, dim3(128), 0, s, cls, wk.lab, h, w, ntx, nty, wk.parent);
+    hipLaunchKernelGGL(k_ccl_border, grid, dim3(128), 0, s, cls, wk.lab, h, w, ntx, nty, wk.nroots, wk.parent);
     hipLaunchKernelGGL(k_ccl_flatten, grid, dim3(NT), 0, s, ntiles, wk.roots, wk.nroots, wk.parent, wk.sroot);
     hipLaunchKernelGGL(k_ccl_strong, grid, dim3(NT), 0, s, ntiles, wk.roots, wk.nroots, wk.parent, wk.sroot,
                        wk.tstrong);
-    hipLaunchKernelGGL(k_ccl_edge, grid, dim3(NT), 0, s, cls, wk.lab, h, w, ntx, nty, wk.tstrong, wk.ebits);
+    hipLaunchKernelGGL(k_ccl_edge, grid, dim3(NT), 0, s, cls, wk.lab, h, w, ntx, nty, wk.nroots, wk.tstrong, wk.ebits);
     const size_t words = (size_t)n * h * words_per_row(w);
     const int blocks = (int)std::min<size_t>((words + NT - 1) / NT, 65536);
     hipLaunchKernelGGL(k_bits_dilate, dim3(blocks), dim3(NT), 0, s, wk.ebits, n, h, w, bits, mask_u8);
