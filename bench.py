@@ -147,9 +147,10 @@ def main():
     ap.add_argument("--cpu-workers", type=int, default=16)
     ap.add_argument("--seed", type=int, default=2025)
     ap.add_argument("--e2e-png-steps", type=int, default=2, help="0 disables the PNG end-to-end line")
-    ap.add_argument("--contours", choices=["host", "gpu"], default="host",
+    ap.add_argument("--contours", choices=["auto", "host", "gpu"], default="auto",
                     help="where findContours + the shape loop run: the host pool from the copied-back mask "
-                         "(default, overlaps k-means) or the GPU (contours_gpu.hip)")
+                         "(overlaps k-means), the GPU (contours_gpu.hip), or auto (the library's choice: "
+                         "host unless the rank has < 8 host cores)")
     ap.add_argument("--pipeline", choices=["on", "off"], default="off",
                     help="on: two batches in flight (submit / collect; measured +1 %% images/s, and the "
                          "overlap stretches the event-timed k-means span); off: one llfe_process_batch per step")
@@ -172,7 +173,8 @@ def main():
     from low_level_feature_extraction_amd.backend import Backend
 
     be = Backend.get(local)
-    be.set_contour_mode(args.contours)
+    if args.contours != "auto":
+        be.set_contour_mode(args.contours)
     feats = tuple(f for f in args.features.split(",") if f)
     B, H, W = args.batch, args.height, args.width
     base, _ = shard.shard_bounds(B * world, rank, world)  # weak scaling: B images per rank
@@ -308,7 +310,7 @@ def main():
             "width": W,
             "features": list(feats),
             "parallelism": f"replicas x{world} (host-side shard, no collective)",
-            "contours": args.contours,
+            "contours": be.contour_mode(),
         },
         "roofline": roofline,
         "roofline_stencil": roofline_stencil,

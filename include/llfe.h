@@ -123,11 +123,13 @@ int llfe_set_concurrency(llfe_ctx *ctx, int enable);
  * ShapeAnalyzer.analyze_shapes (shape pyc @L140-181): LLFE_CONTOURS_HOST (default) on the
  * context's host thread pool from the bit-packed mask copied back, overlapping the
  * GPU's k-means; LLFE_CONTOURS_GPU on the GPU (contours_gpu.hip; images up to 4096 wide
- * and 65535 tall, wider ones stay on the host).  Identical results either way.  The
- * environment variable LLFE_CONTOURS=gpu sets the initial mode. */
+ * and 65535 tall, wider ones stay on the host).  Identical results either way.  Initial
+ * mode: GPU when the process has fewer than 8 host cores (hardware threads /
+ * LOCAL_WORLD_SIZE), else host; LLFE_CONTOURS=host|gpu overrides. */
 #define LLFE_CONTOURS_HOST 0
 #define LLFE_CONTOURS_GPU 1
 int llfe_set_contour_mode(llfe_ctx *ctx, int mode);
+int llfe_get_contour_mode(llfe_ctx *ctx); /* the current mode (or < 0) */
 /* copies up to cap entries, returns the number of kernels with statistics */
 int llfe_kernel_stats(llfe_ctx *ctx, llfe_kernel_stat *out, int32_t cap);
 

@@ -114,6 +114,9 @@ class Backend:
         runs k-means; "gpu": on the GPU (contours_gpu.hip).  Identical results."""
         self._chk(self._lib.llfe_set_contour_mode(self.ctx, {"host": 0, "gpu": 1}[mode]))
 
+    def contour_mode(self) -> str:
+        return {0: "host", 1: "gpu"}[self._chk(self._lib.llfe_get_contour_mode(self.ctx))]
+
     def kernel_stats(self) -> dict:
         """{kernel: {"launches", "total_ms", "bytes"}} accumulated while profiling."""
         arr = (L.LlfeKernelStat * 64)()

@@ -326,11 +326,19 @@ int chunk_for(int explicit_chunk, int h, int w) {
     return (int)std::max(1.0, std::min(n, (double)kMaxKmeansBatch));
 }
 
+// host cores per GPU process: the node's cores shared by the LOCAL_WORLD_SIZE ranks
+// torchrun starts on it
+int cores_per_process() {
+    unsigned hc = std::thread::hardware_concurrency();
+    int local = 1;
+    if (const char *lw = getenv("LOCAL_WORLD_SIZE"); lw && atoi(lw) > 0) local = atoi(lw);
+    return std::max(1, (int)(hc ? hc : 4u) / local);
+}
+
 int default_threads() {
     const char *e = getenv("LLFE_HOST_THREADS");
     if (e && atoi(e) > 0) return atoi(e);
-    unsigned hc = std::thread::hardware_concurrency();
-    return (int)std::max(1u, std::min(hc ? hc : 4u, 16u));
+    return std::max(1, std::min(cores_per_process(), 16));
 }
 
 }  // namespace
@@ -849,7 +857,14 @@ int llfe_init(int device, llfe_ctx **out) {
     if (const char *ch = getenv("LLFE_CHUNK"); ch && atoi(ch) > 0) c->chunk = std::min(atoi(ch), kMaxKmeansBatch);
     if (const char *ns = getenv("LLFE_STREAMS"); ns && atoi(ns) == 2) c->nstreams = 2;
     if (const char *sa = getenv("LLFE_SHAPES_AFTER_FRONT"); sa && atoi(sa) == 1) c->shapes_after_front = true;
-    if (const char *cm = getenv("LLFE_CONTOURS"); cm && !strcmp(cm, "gpu")) c->gpu_contours = true;
+    // contours on the host pool unless the process has too few host cores for them
+    // (~5 cores per MI355X at 14k images/s, half of them "ui" at 0.7 ms each): then on
+    // the GPU.  LLFE_CONTOURS=host / gpu overrides.
+    c->gpu_contours = cores_per_process() < 8;
+    if (const char *cm = getenv("LLFE_CONTOURS")) {
+        if (!strcmp(cm, "gpu")) c->gpu_contours = true;
+        if (!strcmp(cm, "host")) c->gpu_contours = false;
+    }
     if (const char *cc = getenv("LLFE_CONCURRENT"); cc && atoi(cc) == 0) c->concurrent = false;
     gauss_kernel_f32(11, c->sp.k11);
     c->pool = new Pool(default_threads() - 1);
@@ -892,6 +907,11 @@ int llfe_set_contour_mode(llfe_ctx *ctx, int mode) {
         return ctx->fail(LLFE_ERR_INVALID, "llfe_set_contour_mode with submitted batches not yet collected");
     ctx->gpu_contours = mode == LLFE_CONTOURS_GPU;
     return LLFE_OK;
+}
+
+int llfe_get_contour_mode(llfe_ctx *ctx) {
+    if (!ctx) return LLFE_ERR_INVALID;
+    return ctx->gpu_contours ? LLFE_CONTOURS_GPU : LLFE_CONTOURS_HOST;
 }
 
 int llfe_set_concurrency(llfe_ctx *ctx, int enable) {

@@ -92,6 +92,8 @@ __global__ __launch_bounds__(KB) void k_uq_keys(const uint8_t *__restrict__ bgr,
         }
         uint32_t kv[PPT];
         uint32_t run_bin = 0xFFFFFFFFu, run_len = 0;
+        // splitmix64 input of pixel p: stream + golden * (p + 1), stepped by one add per pixel
+        uint64_t hin = stream + 0x9E3779B97F4A7C15ull * (uint64_t)(p0 + 1);
 #pragma unroll
         for (int i = 0; i < PPT; i++) {
             int nr, ng, nb;
@@ -100,7 +102,8 @@ __global__ __launch_bounds__(KB) void k_uq_keys(const uint8_t *__restrict__ bgr,
                 ng = nv[3 * i + 1];
                 nb = nv[3 * i + 2];
             } else {
-                const uint64_t hsh = mix64(stream + 0x9E3779B97F4A7C15ull * (uint64_t)(p0 + i + 1));
+                const uint64_t hsh = mix64(hin);
+                hin += 0x9E3779B97F4A7C15ull;
                 nr = noise21((uint32_t)hsh & 0x1FFFFFu);
                 ng = noise21((uint32_t)(hsh >> 21) & 0x1FFFFFu);
                 nb = noise21((uint32_t)(hsh >> 42) & 0x1FFFFFu);
