@@ -78,7 +78,8 @@ __device__ __forceinline__ void g_union(int *P, int a, int b) {
 __global__ __launch_bounds__(NT) void k_ccl_local(const uint8_t *__restrict__ cls, int H, int W, int ntx, int nty,
                                                   uint16_t *__restrict__ lab, int *__restrict__ parent,
                                                   uint8_t *__restrict__ sroot, uint16_t *__restrict__ roots,
-                                                  int *__restrict__ nroots) {
+                                                  int *__restrict__ nroots, int *__restrict__ tlist,
+                                                  int *__restrict__ tcount) {
     __shared__ int L[TP];
     __shared__ uint32_t sflag[TP / 32];
     __shared__ int cnt;
@@ -139,7 +140,10 @@ __global__ __launch_bounds__(NT) void k_ccl_local(const uint8_t *__restrict__ cl
         }
     }
     __syncthreads();
-    if (tid == 0) nroots[(size_t)img * ntiles + t] = cnt;
+    if (tid == 0) {
+        nroots[(size_t)img * ntiles + t] = cnt;
+        tlist[atomicAdd(tcount, 1)] = img * ntiles + t;  // the later passes visit only these
+    }
 }
 
 __device__ __forceinline__ int gid_of(const uint16_t *lab, int img, int H, int W, int ntx, int ntiles, int y, int x) {
@@ -147,111 +151,119 @@ __device__ __forceinline__ int gid_of(const uint16_t *lab, int img, int H, int W
     return (int)(((size_t)img * ntiles + t) * TP) + lab[((size_t)img * H + y) * W + x];
 }
 
-// grid (ntiles, n): threads 0..31 right column, 32..95 bottom row of the tile
+// The passes after k_ccl_local visit only the tiles it listed (those with a candidate;
+// 15 % of the ui / photo mix): a fixed grid loops over tlist instead of launching one
+// workgroup per tile.  Edge words of unlisted tiles stay zero (memset).
+constexpr int kListBlocks = 4096;
+
+// threads 0..31 the tile's right column (look east), 32..95 its bottom row (look south)
 __global__ __launch_bounds__(128) void k_ccl_border(const uint8_t *__restrict__ cls, const uint16_t *__restrict__ lab,
-                                                    int H, int W, int ntx, int nty, const int *__restrict__ nroots,
-                                                    int *__restrict__ parent) {
-    const int tid = threadIdx.x, img = blockIdx.y, t = blockIdx.x;
-    const int ntiles = ntx * nty;
-    if (!nroots[(size_t)img * ntiles + t]) return;  // no candidates on this tile's seams
-    const int tx0 = (t % ntx) * TW, ty0 = (t / ntx) * TH;
-    const uint8_t *c = cls + (size_t)img * H * W;
-    int x, y;
-    if (tid < TH) {
-        x = tx0 + TW - 1;
-        y = ty0 + tid;
-    } else if (tid < TH + TW) {
-        x = tx0 + tid - TH;
-        y = ty0 + TH - 1;
-    } else {
-        return;
-    }
-    if (x >= W || y >= H || c[(size_t)y * W + x] == 1) return;
-    const int a = gid_of(lab, img, H, W, ntx, ntiles, y, x);
-    const int ty = y / TH, txi = x / TW;
-    for (int dy = -1; dy <= 1; dy++)
-        for (int dx = -1; dx <= 1; dx++) {
-            if (!dx && !dy) continue;
-            const int yy = y + dy, xx = x + dx;
-            if (yy < 0 || yy >= H || xx < 0 || xx >= W) continue;
-            if (yy / TH == ty && xx / TW == txi) continue;  // same tile: already merged locally
-            if (tid < TH ? dx != 1 : dy != 1) continue;     // right column looks east, bottom row south
-            if (c[(size_t)yy * W + xx] == 1) continue;
-            g_union(parent, a, gid_of(lab, img, H, W, ntx, ntiles, yy, xx));
+                                                    int H, int W, int ntx, int nty, const int *__restrict__ tlist,
+                                                    const int *__restrict__ tcount, int *__restrict__ parent) {
+    const int tid = threadIdx.x, ntiles = ntx * nty, ntl = *tcount;
+    for (int it = blockIdx.x; it < ntl; it += gridDim.x) {
+        const int tt = tlist[it], img = tt / ntiles, t = tt % ntiles;
+        const int tx0 = (t % ntx) * TW, ty0 = (t / ntx) * TH;
+        const uint8_t *c = cls + (size_t)img * H * W;
+        int x, y;
+        if (tid < TH) {
+            x = tx0 + TW - 1;
+            y = ty0 + tid;
+        } else if (tid < TH + TW) {
+            x = tx0 + tid - TH;
+            y = ty0 + TH - 1;
+        } else {
+            continue;
         }
-}
-
-__global__ __launch_bounds__(NT) void k_ccl_flatten(int ntiles, const uint16_t *__restrict__ roots,
-                                                     const int *__restrict__ nroots, int *__restrict__ parent,
-                                                     uint8_t *__restrict__ sroot) {
-    const size_t tile = (size_t)blockIdx.y * ntiles + blockIdx.x;
-    const int n = nroots[tile];
-    const size_t gbase = tile * TP;
-    for (int k = threadIdx.x; k < n; k += NT) {
-        const int g = (int)(gbase + roots[gbase + k]);
-        const int r = g_find(parent, g);
-        if (sroot[g]) sroot[r] = 1;
-        if (r != g) parent[g] = r;
+        if (x >= W || y >= H || c[(size_t)y * W + x] == 1) continue;
+        const int a = gid_of(lab, img, H, W, ntx, ntiles, y, x);
+        const int ty = y / TH, txi = x / TW;
+        for (int dy = -1; dy <= 1; dy++)
+            for (int dx = -1; dx <= 1; dx++) {
+                if (!dx && !dy) continue;
+                const int yy = y + dy, xx = x + dx;
+                if (yy < 0 || yy >= H || xx < 0 || xx >= W) continue;
+                if (yy / TH == ty && xx / TW == txi) continue;  // same tile: already merged locally
+                if (tid < TH ? dx != 1 : dy != 1) continue;     // right column looks east, bottom row south
+                if (c[(size_t)yy * W + xx] == 1) continue;
+                g_union(parent, a, gid_of(lab, img, H, W, ntx, ntiles, yy, xx));
+            }
     }
 }
 
-// per tile: one bit per local root, set when its global root is strong
-__global__ __launch_bounds__(NT) void k_ccl_strong(int ntiles, const uint16_t *__restrict__ roots,
-                                                    const int *__restrict__ nroots, const int *__restrict__ parent,
-                                                    const uint8_t *__restrict__ sroot, uint32_t *__restrict__ tstrong) {
+__global__ __launch_bounds__(NT) void k_ccl_flatten(const int *__restrict__ tlist, const int *__restrict__ tcount,
+                                                     const uint16_t *__restrict__ roots, const int *__restrict__ nroots,
+                                                     int *__restrict__ parent, uint8_t *__restrict__ sroot) {
+    const int ntl = *tcount;
+    for (int it = blockIdx.x; it < ntl; it += gridDim.x) {
+        const size_t tile = (size_t)tlist[it], gbase = tile * TP;
+        const int n = nroots[tile];
+        for (int k = threadIdx.x; k < n; k += NT) {
+            const int g = (int)(gbase + roots[gbase + k]);
+            const int r = g_find(parent, g);
+            if (sroot[g]) sroot[r] = 1;
+            if (r != g) parent[g] = r;
+        }
+    }
+}
+
+// per listed tile: one bit per local root, set when its global root is strong
+__global__ __launch_bounds__(NT) void k_ccl_strong(const int *__restrict__ tlist, const int *__restrict__ tcount,
+                                                    const uint16_t *__restrict__ roots, const int *__restrict__ nroots,
+                                                    const int *__restrict__ parent, const uint8_t *__restrict__ sroot,
+                                                    uint32_t *__restrict__ tstrong) {
     __shared__ uint32_t rs[TP / 32];
-    const size_t tile = (size_t)blockIdx.y * ntiles + blockIdx.x, gbase = tile * TP;
-    const int tid = threadIdx.x, n = nroots[tile];
-    if (!n) return;  // k_ccl_edge does not read this tile's bits
-    if (tid < TP / 32) rs[tid] = 0;
-    __syncthreads();
-    for (int k = tid; k < n; k += NT) {
-        const int i = roots[gbase + k];
-        if (sroot[parent[gbase + i]]) atomicOr(&rs[i >> 5], 1u << (i & 31));
+    const int tid = threadIdx.x, ntl = *tcount;
+    for (int it = blockIdx.x; it < ntl; it += gridDim.x) {
+        const size_t tile = (size_t)tlist[it], gbase = tile * TP;
+        const int n = nroots[tile];
+        if (tid < TP / 32) rs[tid] = 0;
+        __syncthreads();
+        for (int k = tid; k < n; k += NT) {
+            const int i = roots[gbase + k];
+            if (sroot[parent[gbase + i]]) atomicOr(&rs[i >> 5], 1u << (i & 31));
+        }
+        __syncthreads();
+        if (tid < TP / 32) tstrong[tile * (TP / 32) + tid] = rs[tid];
+        __syncthreads();
     }
-    __syncthreads();
-    if (tid < TP / 32) tstrong[tile * (TP / 32) + tid] = rs[tid];
 }
 
-// per tile, no halo: edge = strong || (maybe && strong local root); one wave per
-// 64-pixel row segment packs the row's edge word with __ballot
+// per listed tile, no halo: edge = strong || (maybe && strong local root); one wave
+// per 64-pixel row segment packs the row's edge word with __ballot
 __global__ __launch_bounds__(NT) void k_ccl_edge(const uint8_t *__restrict__ cls, const uint16_t *__restrict__ lab,
-                                                  int H, int W, int ntx, int nty, const int *__restrict__ nroots,
-                                                  const uint32_t *__restrict__ tstrong, uint64_t *__restrict__ ebits) {
+                                                  int H, int W, int ntx, int nty, const int *__restrict__ tlist,
+                                                  const int *__restrict__ tcount, const uint32_t *__restrict__ tstrong,
+                                                  uint64_t *__restrict__ ebits) {
     __shared__ uint32_t rs[TP / 32];
     constexpr int RPW = TH / (NT / 64);  // rows per wave
-    const int tid = threadIdx.x, img = blockIdx.y, t = blockIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int ntiles = ntx * nty;
-    const int tx0 = (t % ntx) * TW, ty0 = (t / ntx) * TH, x = tx0 + lane;
-    const size_t tile = (size_t)img * ntiles + t;
-    const int wpr = (W + 63) / 64;
-    if (!nroots[tile]) {  // every pixel suppressed: zero edge words, no class / label reads
-        if (lane == 0)
-            for (int r = 0; r < RPW; r++) {
-                const int y = ty0 + wid + r * (NT / 64);
-                if (y < H) ebits[((size_t)img * H + y) * wpr + (tx0 >> 6)] = 0ull;
-            }
-        return;
-    }
-    const uint8_t *c = cls + (size_t)img * H * W;
-    const uint16_t *lb = lab + (size_t)img * H * W;
-    uint32_t v[RPW], l[RPW];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int ntiles = ntx * nty, ntl = *tcount, wpr = (W + 63) / 64;
+    for (int it = blockIdx.x; it < ntl; it += gridDim.x) {
+        const int tt = tlist[it], img = tt / ntiles, t = tt % ntiles;
+        const int tx0 = (t % ntx) * TW, ty0 = (t / ntx) * TH, x = tx0 + lane;
+        const size_t tile = (size_t)tt;
+        const uint8_t *c = cls + (size_t)img * H * W;
+        const uint16_t *lb = lab + (size_t)img * H * W;
+        uint32_t v[RPW], l[RPW];
 #pragma unroll
-    for (int r = 0; r < RPW; r++) {
-        const int y = ty0 + wid + r * (NT / 64);
-        const bool in = y < H && x < W;
-        v[r] = in ? c[(size_t)y * W + x] : 1u;
-        l[r] = in ? lb[(size_t)y * W + x] : 0u;  // meaningful only where v == 0
-    }
-    if (tid < TP / 32) rs[tid] = tstrong[tile * (TP / 32) + tid];
-    __syncthreads();
+        for (int r = 0; r < RPW; r++) {
+            const int y = ty0 + wid + r * (NT / 64);
+            const bool in = y < H && x < W;
+            v[r] = in ? c[(size_t)y * W + x] : 1u;
+            l[r] = in ? lb[(size_t)y * W + x] : 0u;  // meaningful only where v == 0
+        }
+        if (tid < TP / 32) rs[tid] = tstrong[tile * (TP / 32) + tid];
+        __syncthreads();
 #pragma unroll
-    for (int r = 0; r < RPW; r++) {
-        const int y = ty0 + wid + r * (NT / 64);
-        const uint32_t li = l[r] & (TP - 1);
-        const bool on = v[r] == 2u || (v[r] == 0u && ((rs[li >> 5] >> (li & 31)) & 1u));
-        const unsigned long long b = __ballot(on);
-        if (lane == 0 && y < H) ebits[((size_t)img * H + y) * wpr + (tx0 >> 6)] = b;
+        for (int r = 0; r < RPW; r++) {
+            const int y = ty0 + wid + r * (NT / 64);
+            const uint32_t li = l[r] & (TP - 1);
+            const bool on = v[r] == 2u || (v[r] == 0u && ((rs[li >> 5] >> (li & 31)) & 1u));
+            const unsigned long long b = __ballot(on);
+            if (lane == 0 && y < H) ebits[((size_t)img * H + y) * wpr + (tx0 >> 6)] = b;
+        }
+        __syncthreads();
     }
 }
 
@@ -290,14 +302,21 @@ hipError_t launch_hysteresis_dilate(const uint8_t *cls, int n, int h, int w, con
                                     uint8_t *mask_u8, hipStream_t s) {
     const int ntx = tiles_x(w), nty = tiles_y(h), ntiles = ntx * nty;
     dim3 grid(ntiles, n);
-    hipLaunchKernelGGL(k_ccl_local, grid, dim3(NT), 0, s, cls, h, w, ntx, nty, wk.lab, wk.parent, wk.sroot, wk.roots,
-                       wk.nroots);
-    hipLaunchKernelGGL(k_ccl_border, grid, dim3(128), 0, s, cls, wk.lab, h, w, ntx, nty, wk.nroots, wk.parent);
-    hipLaunchKernelGGL(k_ccl_flatten, grid, dim3(NT), 0, s, ntiles, wk.roots, wk.nroots, wk.parent, wk.sroot);
-    hipLaunchKernelGGL(k_ccl_strong, grid, dim3(NT), 0, s, ntiles, wk.roots, wk.nroots, wk.parent, wk.sroot,
-                       wk.tstrong);
-    hipLaunchKernelGGL(k_ccl_edge, grid, dim3(NT), 0, s, cls, wk.lab, h, w, ntx, nty, wk.nroots, wk.tstrong, wk.ebits);
     const size_t words = (size_t)n * h * words_per_row(w);
+    hipError_t e;
+    if ((e = hipMemsetAsync(wk.tcount, 0, sizeof(int), s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(wk.ebits, 0, sizeof(uint64_t) * words, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_ccl_local, grid, dim3(NT), 0, s, cls, h, w, ntx, nty, wk.lab, wk.parent, wk.sroot, wk.roots,
+                       wk.nroots, wk.tlist, wk.tcount);
+    const dim3 lgrid((unsigned)std::min<int64_t>((int64_t)ntiles * n, kListBlocks));
+    hipLaunchKernelGGL(k_ccl_border, lgrid, dim3(128), 0, s, cls, wk.lab, h, w, ntx, nty, wk.tlist, wk.tcount,
+                       wk.parent);
+    hipLaunchKernelGGL(k_ccl_flatten, lgrid, dim3(NT), 0, s, wk.tlist, wk.tcount, wk.roots, wk.nroots, wk.parent,
+                       wk.sroot);
+    hipLaunchKernelGGL(k_ccl_strong, lgrid, dim3(NT), 0, s, wk.tlist, wk.tcount, wk.roots, wk.nroots, wk.parent,
+                       wk.sroot, wk.tstrong);
+    hipLaunchKernelGGL(k_ccl_edge, lgrid, dim3(NT), 0, s, cls, wk.lab, h, w, ntx, nty, wk.tlist, wk.tcount, wk.tstrong,
+                       wk.ebits);
     const int blocks = (int)std::min<size_t>((words + NT - 1) / NT, 65536);
     hipLaunchKernelGGL(k_bits_dilate, dim3(blocks), dim3(NT), 0, s, wk.ebits, n, h, w, bits, mask_u8);
     return hipGetLastError();

@@ -204,7 +204,7 @@ struct Work {
     DevBuf<int8_t> d_noise;
     DevBuf<uint64_t> d_bits, d_ebits;
     DevBuf<unsigned long long> d_shadow;
-    DevBuf<int> d_order, d_parent, d_nroots;
+    DevBuf<int> d_order, d_parent, d_nroots, d_tlist;
     DevBuf<uint16_t> d_lab, d_roots;
     DevBuf<uint32_t> d_raw, d_keys, d_kscratch, d_pmeta, d_tstrong;
     DevBuf<CubeEnt> d_segcubes, d_cubes;
@@ -469,7 +469,9 @@ int run_hysteresis_dilate(llfe_ctx *ctx, Work &W, int n, int h, int w, uint64_t 
     HIPCHK(ctx, W.d_nroots.ensure(tiles));
     HIPCHK(ctx, W.d_tstrong.ensure(tiles * (kTileW * kTileH / 32)));
     HIPCHK(ctx, W.d_ebits.ensure((size_t)n * h * words_per_row(w)));
-    HystWork wk{W.d_lab.p, W.d_parent.p, W.d_sroot.p, W.d_roots.p, W.d_nroots.p, W.d_tstrong.p, W.d_ebits.p};
+    HIPCHK(ctx, W.d_tlist.ensure(tiles + 1));
+    HystWork wk{W.d_lab.p,     W.d_parent.p, W.d_sroot.p,       W.d_roots.p,   W.d_nroots.p,
+                W.d_tstrong.p, W.d_ebits.p,  W.d_tlist.p + 1, W.d_tlist.p};
     TIMED(ctx, s, "k_hysteresis_dilate", (double)n * h * w * (1 + 2 + 1 + 2 + 3 * 0.125),
           launch_hysteresis_dilate(W.d_cls.p, n, h, w, wk, bits, mask_u8, s));
     return LLFE_OK;

@@ -45,6 +45,8 @@ struct HystWork {
     int *nroots;
     uint32_t *tstrong;  // per tile TP / 32 words
     uint64_t *ebits;    // n x h x words_per_row, edges before the dilate
+    int *tlist;         // tiles with a Canny candidate (n * tiles) and their count
+    int *tcount;
 };
 size_t hysteresis_ids(int n, int h, int w);
 hipError_t launch_hysteresis_dilate(const uint8_t *cls, int n, int h, int w, const HystWork &wk, uint64_t *bits,
