@@ -82,19 +82,25 @@ __global__ __launch_bounds__(NT) void k_ccl_local(const uint8_t *__restrict__ cl
                                                   int *__restrict__ tcount) {
     __shared__ int L[TP];
     __shared__ uint32_t sflag[TP / 32];
+    __shared__ __attribute__((aligned(8))) uint8_t cb[TP];
     __shared__ int cnt;
     const int tid = threadIdx.x, img = blockIdx.y, t = blockIdx.x;
     const int ntiles = ntx * nty;
     const int tx0 = (t % ntx) * TW, ty0 = (t / ntx) * TH;
     const uint8_t *c = cls + (size_t)img * H * W;
-    uint8_t v[TP / NT];
     bool any = false;
-#pragma unroll
-    for (int k = 0; k < TP / NT; k++) {
-        int i = tid + k * NT, ly = i >> 6, lx = i & 63, y = ty0 + ly, x = tx0 + lx;
-        v[k] = (y < H && x < W) ? c[(size_t)y * W + x] : 1;
-        L[i] = v[k] != 1 ? i : -1;
-        any |= v[k] != 1;
+    if ((W & 7) == 0 && tx0 + TW <= W) {  // one 8-byte load per thread, through LDS
+        const int row = tid >> 3, col = (tid & 7) * 8, y = ty0 + row;
+        const uint64_t ones = 0x0101010101010101ull;
+        const uint64_t w = y < H ? *(const uint64_t *)(c + (size_t)y * W + tx0 + col) : ones;
+        any = w != ones;
+        *(uint64_t *)&cb[row * TW + col] = w;
+    } else {
+        for (int k = 0; k < TP / NT; k++) {
+            const int i = tid + k * NT, y = ty0 + (i >> 6), x = tx0 + (i & 63);
+            cb[i] = (y < H && x < W) ? c[(size_t)y * W + x] : 1;
+            any |= cb[i] != 1;
+        }
     }
     if (tid < TP / 32) sflag[tid] = 0;
     if (tid == 0) cnt = 0;
@@ -104,6 +110,14 @@ __global__ __launch_bounds__(NT) void k_ccl_local(const uint8_t *__restrict__ cl
         if (tid == 0) nroots[(size_t)img * ntiles + t] = 0;
         return;
     }
+    uint8_t v[TP / NT];
+#pragma unroll
+    for (int k = 0; k < TP / NT; k++) {
+        const int i = tid + k * NT;
+        v[k] = cb[i];
+        L[i] = v[k] != 1 ? i : -1;
+    }
+    __syncthreads();
 #pragma unroll
     for (int k = 0; k < TP / NT; k++) {
         if (v[k] == 1) continue;

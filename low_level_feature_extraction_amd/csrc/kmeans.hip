@@ -1406,41 +1406,25 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
     }
 }
 
-// LPT order: images sorted by U descending (bitonic sort in LDS, n <= 4096)
+// LPT order: images sorted by U descending, index ascending on ties (n <= 4096): each
+// image's rank is the number of images before it in that order (LDS broadcast reads;
+// one pass instead of the 45 barrier-separated stages of a bitonic sort)
 constexpr int OT = 1024;
 constexpr int OMAX = 4096;
 __global__ __launch_bounds__(OT) void k_kmeans_order(const long long *__restrict__ n_unique, int n,
                                                      int *__restrict__ order) {
     __shared__ long long key[OMAX];
-    __shared__ int idx[OMAX];
-    int np2 = 1;
-    while (np2 < n) np2 <<= 1;
-    for (int i = threadIdx.x; i < np2; i += OT) {
-        key[i] = i < n ? n_unique[i] : -1;
-        idx[i] = i;
-    }
+    for (int i = threadIdx.x; i < n; i += OT) key[i] = n_unique[i];
     __syncthreads();
-    for (int k = 2; k <= np2; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < np2; i += OT) {
-                int l = i ^ j;
-                if (l > i) {
-                    bool desc = (i & k) == 0;
-                    bool sw = desc ? (key[i] < key[l] || (key[i] == key[l] && idx[i] > idx[l]))
-                                   : (key[i] > key[l] || (key[i] == key[l] && idx[i] < idx[l]));
-                    if (sw) {
-                        long long tk = key[i];
-                        key[i] = key[l];
-                        key[l] = tk;
-                        int ti = idx[i];
-                        idx[i] = idx[l];
-                        idx[l] = ti;
-                    }
-                }
-            }
-            __syncthreads();
+    for (int i = threadIdx.x; i < n; i += OT) {
+        const long long ki = key[i];
+        int r = 0;
+        for (int j = 0; j < n; j++) {
+            const long long kj = key[j];
+            r += (kj > ki) | ((kj == ki) & (j < i));
         }
-    for (int i = threadIdx.x; i < n; i += OT) order[i] = idx[i];
+        order[r] = i;
+    }
 }
 
 __global__ void k_kmeans_finalize(const uint32_t *__restrict__ keys, long long key_stride,
