@@ -67,7 +67,7 @@ typedef struct {
     int32_t on_device;     /* 1: device pointer, 0: host pointer */
     /* optional "parity mode" noise: N x H x W x 3 int8 in RGB channel order, i.e.
      * exactly np.random.normal(0, 0.5, (H*W, 3)).astype(np.int8) per image
-     * (color_extractor.py:224).  NULL -> on-device counter-based (splitmix64) noise of the same
+     * (color_extractor.py:224).  NULL -> on-device counter-based (hashed) noise of the same
      * distribution. */
     const int8_t *noise;
     int32_t noise_on_device;

@@ -70,6 +70,16 @@ class Backend:
         if device is None:
             device = int(os.environ.get("LLFE_DEVICE", os.environ.get("LOCAL_RANK", "0")))
         self.device = device
+        # PyTorch-ROCm ships its own HIP runtime (torch/lib/libamdhip64.so) beside the
+        # /opt/rocm one libllfe links: torch's must initialise first, or its later
+        # lazy init finds "no HIP GPUs" once libllfe holds the device
+        try:
+            import torch
+
+            if torch.cuda.is_available():
+                torch.cuda.init()
+        except ImportError:  # pragma: no cover
+            pass
         self._lib = L.lib()
         ctx = C.c_void_p()
         rc = self._lib.llfe_init(device, C.byref(ctx))

@@ -35,6 +35,16 @@ __device__ __forceinline__ int noise21(uint32_t u) {
     return neg ? -mag : mag;
 }
 
+// 32-bit avalanche hash (lowbias32: two multiplies, three xor-shifts)
+__device__ __forceinline__ uint32_t hash32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7FEB352Du;
+    x ^= x >> 15;
+    x *= 0x846CA68Bu;
+    x ^= x >> 16;
+    return x;
+}
+
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
@@ -53,7 +63,7 @@ __device__ __forceinline__ uint32_t key_of(int b, int g, int r, int nb, int ng, 
 }
 
 // grid (blocks, n).  noise: parity-mode int8 stream in RGB order (p*3 + c) or null
-// (counter-based: h = splitmix64(image stream + pixel), three 21-bit uniforms).
+// (counter-based: two 32-bit hashes of (image stream, pixel) -> three 21-bit uniforms).
 __global__ __launch_bounds__(KB) void k_uq_keys(const uint8_t *__restrict__ bgr, const int8_t *__restrict__ noise,
                                                 long long P, long long key_stride, unsigned long long seed,
                                                 long long index_base, uint32_t *__restrict__ keys,
@@ -92,8 +102,10 @@ __global__ __launch_bounds__(KB) void k_uq_keys(const uint8_t *__restrict__ bgr,
         }
         uint32_t kv[PPT];
         uint32_t run_bin = 0xFFFFFFFFu, run_len = 0;
-        // splitmix64 input of pixel p: stream + golden * (p + 1), stepped by one add per pixel
-        uint64_t hin = stream + 0x9E3779B97F4A7C15ull * (uint64_t)(p0 + 1);
+        // counter of pixel p: lo(stream) + golden32 * (p + 1), stepped by one add per pixel;
+        // two hash32 of it (the second keyed by hi(stream)) give the 63 noise bits
+        uint32_t ctr = (uint32_t)stream + 0x9E3779B9u * (uint32_t)(p0 + 1);
+        const uint32_t key2 = (uint32_t)(stream >> 32) | 1u;
 #pragma unroll
         for (int i = 0; i < PPT; i++) {
             int nr, ng, nb;
@@ -102,11 +114,11 @@ __global__ __launch_bounds__(KB) void k_uq_keys(const uint8_t *__restrict__ bgr,
                 ng = nv[3 * i + 1];
                 nb = nv[3 * i + 2];
             } else {
-                const uint64_t hsh = mix64(hin);
-                hin += 0x9E3779B97F4A7C15ull;
-                nr = noise21((uint32_t)hsh & 0x1FFFFFu);
-                ng = noise21((uint32_t)(hsh >> 21) & 0x1FFFFFu);
-                nb = noise21((uint32_t)(hsh >> 42) & 0x1FFFFFu);
+                const uint32_t h1 = hash32(ctr), h2 = hash32(ctr ^ key2);
+                ctr += 0x9E3779B9u;
+                nr = noise21(h1 & 0x1FFFFFu);
+                ng = noise21((h1 >> 21) | ((h2 & 0x3FFu) << 11));
+                nb = noise21(h2 >> 11);
             }
             kv[i] = key_of(px[3 * i], px[3 * i + 1], px[3 * i + 2], nb, ng, nr);
             if (i < cnt) {  // run-length histogram: neighbouring pixels share a partition
