@@ -309,3 +309,20 @@ def test_empty_batch(backend):
     assert backend.process(np.zeros((0, 32, 48, 3), np.uint8)) == []
     t = backend.submit(np.zeros((0, 32, 48, 3), np.uint8))
     assert backend.collect(t) == []
+
+
+def test_backend_before_torch_in_a_fresh_process():
+    # libllfe and PyTorch-ROCm each load a HIP runtime: a Backend created before any
+    # torch call must still leave torch's device usable (Backend initialises it first)
+    import subprocess
+    import sys
+
+    code = ("import numpy as np\n"
+            "from low_level_feature_extraction_amd.backend import Backend\n"
+            "be = Backend.get(0)\n"
+            "keys, nu = be.color_unique(np.zeros((1, 8, 8, 3), np.uint8), noise=np.zeros(192, np.int8))\n"
+            "print(int(nu[0]))\n")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert out.stdout.strip().splitlines()[-1] == "1"
