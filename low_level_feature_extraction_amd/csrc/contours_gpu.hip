@@ -404,7 +404,7 @@ struct NbWindow {
     uint64_t *win;  // kWinRows x kWinWords
     int wy0 = -(1 << 30), wq0 = 0;
     int cy = -(1 << 30), cq = 0;
-    uint64_t r0[3], r1[3], r2[3];  // rows cy-1, cy, cy+1 x words cq-1, cq, cq+1
+    uint64_t r0[3] = {0, 0, 0}, r1[3] = {0, 0, 0}, r2[3] = {0, 0, 0};  // rows cy-1..cy+1 x words cq-1..cq+1
     __device__ void reload(int q, int y) {
         wy0 = y - kWinRows / 2;
         wq0 = q - 1;
@@ -894,7 +894,7 @@ __global__ __launch_bounds__(1024) void k_ct_bases(int n, int *__restrict__ img_
         s[threadIdx.x] = v;
         __syncthreads();
         for (int o = 1; o < 1024; o <<= 1) {
-            const int add = threadIdx.x >= o ? s[threadIdx.x - o] : 0;
+            const int add = (int)threadIdx.x >= o ? s[threadIdx.x - o] : 0;
             __syncthreads();
             s[threadIdx.x] += add;
             __syncthreads();
@@ -923,10 +923,6 @@ struct GeoLds {  // ~49 KB: three waves per CU
 };
 
 __device__ __forceinline__ double wave_sum_d(double v) {
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
-__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
     for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
     return v;
 }
