@@ -77,7 +77,10 @@ typedef struct {
 
 typedef struct {
     /* colors: _get_dominant_colors + bincount (color_extractor.py:174-236) */
-    int32_t n_colors;          /* K = min(n_colors, U) centres (U when U <= 1) */
+    int32_t n_colors;          /* centres written: K = min(n_colors, U) when K > 1; when K <= 1
+                                  (n_colors = 1 or U <= 1) the reference returns every unique
+                                  colour with labels [0]*U (color_extractor.py:185-186): here
+                                  the first min(U, 5) in np.unique order, counts [U, 0, ...] */
     int32_t counts[5];         /* np.bincount(labels) per centre, k-means order */
     uint8_t centers_rgb[5][3]; /* centers.astype(np.uint8), k-means order */
     uint8_t pad_[1];
@@ -114,6 +117,10 @@ int llfe_init(int device, llfe_ctx **out);
 int llfe_destroy(llfe_ctx *ctx);
 const char *llfe_last_error(llfe_ctx *ctx);
 int llfe_abi_version(void);
+/* file path of the HIP runtime (libamdhip64) the library is bound to.  Device pointers
+ * and `stream` handles passed in must come from this same runtime: a process that
+ * also uses PyTorch-ROCm loads libllfe after torch, so both share torch's runtime. */
+const char *llfe_hip_runtime(void);
 /* enable (1) / disable (0) event timing; enabling resets the statistics */
 int llfe_set_profiling(llfe_ctx *ctx, int enable);
 /* llfe_process_batch runs the colour path on a second stream beside shapes / shadows
@@ -241,18 +248,26 @@ int llfe_shapes_from_masks_gpu(llfe_ctx *ctx, const uint8_t *masks, int32_t n, i
                                llfe_shape *shapes, int64_t capacity, int32_t *n_shapes, int32_t *n_contours,
                                int64_t *needed);
 
-/* ---- host PNG decode (cv2.imdecode(buf, IMREAD_COLOR), utils.py:108-109 and
- * image_processor.py:208-211).  Host only, no ctx.  IMREAD_COLOR semantics: BGR u8,
- * alpha dropped, grey expanded, palette looked up, 16-bit -> high byte; critical-chunk
- * CRCs checked.  Interlaced and sub-byte-depth images return LLFE_ERR_UNSUPPORTED
- * (the caller decodes those another way); corrupt data LLFE_ERR_INVALID. */
-/* size of a PNG from its IHDR */
+/* ---- host decode (cv2.imdecode(buf, IMREAD_COLOR), utils.py:108-109 and
+ * image_processor.py:208-211).  Host only, no ctx.  IMREAD_COLOR semantics: BGR u8.
+ * PNG (native decoder): alpha dropped, grey expanded, palette looked up, 16-bit -> high
+ * byte, critical-chunk CRCs checked.  JPEG (system libjpeg-turbo via dlopen, OpenCV's
+ * settings: ISLOW IDCT, fancy upsampling, JCS_EXT_BGR out).  Images above
+ * LLFE_MAX_PIXELS (default 2^30, cv2's CV_IO_MAX_IMAGE_PIXELS) are refused before
+ * anything is allocated.  LLFE_ERR_UNSUPPORTED hands an image back to the caller's
+ * other decoder: interlaced / sub-byte-depth PNG, CMYK / YCCK JPEG, JPEG with an EXIF
+ * orientation other than 1, other formats; corrupt data is LLFE_ERR_INVALID. */
+/* size of a PNG from its IHDR; LLFE_ERR_CAPACITY (size still written) above the pixel limit */
 int llfe_png_info(const uint8_t *data, uint64_t size, int32_t *width, int32_t *height);
 /* n PNGs of one size into out_bgr (n x height x width x 3, host), `threads` host
  * threads.  status[i] per image (LLFE_OK, LLFE_ERR_UNSUPPORTED, LLFE_ERR_INVALID, or
  * LLFE_ERR_CAPACITY when its size differs); returns the first non-OK status. */
 int llfe_decode_png_batch(const uint8_t *const *data, const uint64_t *sizes, int32_t n, int32_t height,
                           int32_t width, uint8_t *out_bgr, int32_t *status, int32_t threads);
+/* the same two for PNG and JPEG, by signature (LLFE_ERR_UNSUPPORTED for other formats) */
+int llfe_image_info(const uint8_t *data, uint64_t size, int32_t *width, int32_t *height);
+int llfe_decode_batch(const uint8_t *const *data, const uint64_t *sizes, int32_t n, int32_t height, int32_t width,
+                      uint8_t *out_bgr, int32_t *status, int32_t threads);
 
 #ifdef __cplusplus
 }

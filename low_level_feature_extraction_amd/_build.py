@@ -14,7 +14,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libllfe.so")
-SOURCES = ["llfe_api.cpp", "contours.cpp", "png_decode.cpp", "stencil.hip", "hysteresis.hip", "unique.hip", "kmeans.hip", "resize.hip", "contours_gpu.hip",
+SOURCES = ["llfe_api.cpp", "contours.cpp", "png_decode.cpp", "jpeg_decode.cpp", "stencil.hip", "hysteresis.hip", "unique.hip", "kmeans.hip", "resize.hip", "contours_gpu.hip",
            "cvresize.hip"]
 HEADERS = ["llfe_internal.h", "contours.h"]
 ARCH = os.environ.get("LLFE_OFFLOAD_ARCH", "gfx950")
@@ -49,7 +49,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     for src in SOURCES:
         obj = os.path.join(tmpdir, src + ".o")
         objs.append(obj)
-        if src in ("contours.cpp", "png_decode.cpp"):  # pure host code
+        if src in ("contours.cpp", "png_decode.cpp", "jpeg_decode.cpp"):  # pure host code
             lang = ["-x", "c++"]
         else:
             lang = ["-x", "hip", f"--offload-arch={ARCH}"]

@@ -1,8 +1,15 @@
 """ctypes binding of libllfe.so (the C ABI declared in include/llfe.h).
 
-This is the same binding a non-Python caller would write; nothing
-here depends on torch.  Importing it never falls back to a CPU implementation: if the
-shared library is missing or cannot be loaded, ``lib()`` raises.
+This is the same binding a non-Python caller would write.  Importing
+it never falls back to a CPU implementation: if the shared library is missing or cannot
+be loaded, ``lib()`` raises.
+
+One HIP runtime per process.  PyTorch-ROCm ships its own ``libamdhip64.so`` (SONAME
+``libamdhip64.so.7``, the name libllfe's DT_NEEDED asks for).  When torch is importable
+it is imported *before* libllfe is loaded, so the dynamic linker binds libllfe to the
+runtime torch already mapped: torch's device pointers and ``cuda_stream`` handles are
+then objects of libllfe's own runtime.  ``lib()`` verifies that exactly one
+libamdhip64 is mapped and raises otherwise.
 """
 from __future__ import annotations
 
@@ -12,8 +19,6 @@ import threading
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_PKG, "libllfe.so")
-# experiments only: load a variant build (e.g. libllfe_<tag>.so built with LLFE_EXTRA_FLAGS)
-_VARIANT = os.environ.get("LLFE_LIB_VARIANT")
 
 LLFE_OK = 0
 LLFE_ERR_INVALID = -1
@@ -88,6 +93,7 @@ SIGNATURES = {
     "llfe_destroy": (C.c_int, [_vp]),
     "llfe_last_error": (C.c_char_p, [_vp]),
     "llfe_abi_version": (C.c_int, []),
+    "llfe_hip_runtime": (C.c_char_p, []),
     "llfe_set_profiling": (C.c_int, [_vp, C.c_int]),
     "llfe_set_concurrency": (C.c_int, [_vp, C.c_int]),
     "llfe_set_contour_mode": (C.c_int, [_vp, C.c_int]),
@@ -120,6 +126,8 @@ SIGNATURES = {
                                              C.POINTER(C.c_int64)]),
     "llfe_png_info": (C.c_int, [_vp, C.c_uint64, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "llfe_decode_png_batch": (C.c_int, [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _i32]),
+    "llfe_image_info": (C.c_int, [_vp, C.c_uint64, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "llfe_decode_batch": (C.c_int, [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _i32]),
 }
 
 _lib = None
@@ -132,27 +140,48 @@ class LlfeError(RuntimeError):
         self.code = code
 
 
+def hip_runtimes_mapped() -> list:
+    """Distinct libamdhip64 files mapped into this process (from /proc/self/maps)."""
+    paths = set()
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                p = line.split()[-1] if line.strip() else ""
+                if "libamdhip64" in os.path.basename(p):
+                    paths.add(os.path.realpath(p))
+    except OSError:  # pragma: no cover - non-Linux
+        pass
+    return sorted(paths)
+
+
 def lib():
-    """Load libllfe.so (building it from source if it is absent or stale)."""
+    """Load libllfe.so (building it from source if it is absent or stale), bound to the
+    same HIP runtime as PyTorch when torch is importable."""
     global _lib
     with _lock:
         if _lib is None:
             from . import _build
 
-            if _VARIANT:
-                L = C.CDLL(os.path.join(_PKG, f"libllfe_{_VARIANT}.so"))
-            elif _build._stale():
+            try:  # torch first: its libamdhip64 becomes the one libllfe binds to
+                import torch  # noqa: F401
+            except ImportError:  # pragma: no cover - C-only deployments
+                pass
+            if _build._stale():
                 try:
                     _build.build()
                 except Exception as e:  # pragma: no cover - surfaced to caller
                     if not os.path.exists(LIB_PATH):
                         raise RuntimeError(f"libllfe.so is missing and could not be built: {e}") from e
-            if not _VARIANT:
-                L = C.CDLL(LIB_PATH)
+            L = C.CDLL(LIB_PATH)
             for name, (res, args) in SIGNATURES.items():
                 f = getattr(L, name)
                 f.restype = res
                 f.argtypes = args
+            rts = hip_runtimes_mapped()
+            if len(rts) > 1:
+                raise RuntimeError("two HIP runtimes are mapped into this process (%s); libllfe is bound to %s. "
+                                   "Import torch before loading libllfe so both share one runtime."
+                                   % (", ".join(rts), L.llfe_hip_runtime().decode()))
             _lib = L
     return _lib
 

@@ -113,7 +113,18 @@ class MicroBatcher:
                 res = self._run_batch([im for im, _ in live])
                 for (_, f), r in zip(live, res):
                     f.set_result(r)
-            except BaseException as e:  # every request of the batch sees the error
+            except Exception as e:
+                if len(live) == 1:
+                    live[0][1].set_exception(e)
+                    continue
+                # one bad image must not fail the requests it was batched with (the
+                # reference isolates every request): rerun them one by one
+                for im, f in live:
+                    try:
+                        f.set_result(self._run_batch([im])[0])
+                    except Exception as e1:
+                        f.set_exception(e1)
+            except BaseException as e:  # interpreter shutdown etc.: fail the batch
                 for _, f in live:
                     f.set_exception(e)
         # fail whatever is still queued after close()

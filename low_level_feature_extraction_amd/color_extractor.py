@@ -226,11 +226,11 @@ class ColorExtractor:
 
     @staticmethod
     def extract_colors_batch(images: List[np.ndarray], n_colors: int = 5, seed: Optional[int] = None,
-                             noise=None) -> List[ColorFeatures]:
+                             noise=None, index_base: Optional[int] = None) -> List[ColorFeatures]:
         """Batched extract_colors for same-size BGR uint8 images (N x H x W x 3 array or a
         list).  Mixed sizes are grouped; ``noise`` (parity mode) is the per-image
         np.random.normal(0, 0.5, (H*W, 3)).astype(np.int8) stream."""
         from .pipeline import run_batch
 
-        res = run_batch(images, ("colors",), seed=seed, noise=noise, n_colors=n_colors)
+        res = run_batch(images, ("colors",), seed=seed, noise=noise, n_colors=n_colors, index_base=index_base)
         return [r["colors"] for r in res]

@@ -1438,13 +1438,17 @@ __global__ void k_kmeans_finalize(const uint32_t *__restrict__ keys, long long k
     memset(&r, 0, sizeof r);
     r.n_unique = N;
     if (K <= 1) {
-        r.k = (int)N;
-        if (N == 1) {
-            uint32_t k = keys[(size_t)img * key_stride];
-            r.centers_rgb[0][0] = (uint8_t)(k >> 16);
-            r.centers_rgb[0][1] = (uint8_t)(k >> 8);
-            r.centers_rgb[0][2] = (uint8_t)k;
-            r.counts[0] = 1;
+        // _get_dominant_colors (color_extractor.py:185-186) skips k-means and returns
+        // every unique colour with labels [0] * U, so bincount gives [U, 0, ...] (U > 1)
+        // or no bincount at all (U == 1, count 1): keep the first min(U, kMaxK)
+        // colours in np.unique order
+        r.k = (int)min(N, (long long)kMaxK);
+        for (int k = 0; k < r.k; k++) {
+            const uint32_t key = keys[(size_t)img * key_stride + k];
+            r.centers_rgb[k][0] = (uint8_t)(key >> 16);
+            r.centers_rgb[k][1] = (uint8_t)(key >> 8);
+            r.centers_rgb[k][2] = (uint8_t)key;
+            r.counts[k] = k == 0 ? (int)N : 0;
         }
         r.compactness = 0.0;
     } else {

@@ -8,6 +8,7 @@
 //   -> D2H (1 bit / pixel)
 //   colour bitmap -> compaction -> k-means (10 attempts / image) -> D2H 64 B / image
 //   host thread pool: external contours + shape geometry from the packed masks
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -406,6 +407,8 @@ struct llfe_ctx {
     std::vector<ShapeScratch> shs;
     std::vector<std::vector<llfe_shape>> img_shapes;
     std::vector<int32_t> img_ncont;
+    int64_t host_fallbacks = 0;  // GPU-contour chunks traced on the host instead
+    bool force_ct_fallback = false;  // LLFE_CT_FORCE_HOST_FALLBACK=1 (tests: exercise that path)
 
     int fail(int code, const char *fmt, ...) {
         char buf[512];
@@ -707,34 +710,82 @@ int enqueue_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_
     return LLFE_OK;
 }
 
+// Shape records of n images from their bit-packed dilated masks (hb, host) on the
+// context's thread pool: external contours + the analyze_shapes loop (contours.cpp).
+void host_shapes_from_bits(llfe_ctx *ctx, const uint64_t *hb, int n, int h, int w, int i0,
+                           llfe_image_result *results, llfe_shape *shapes, int64_t shape_capacity,
+                           int64_t &total_shapes) {
+    const int wpr = words_per_row(w);
+    ctx->img_shapes.resize(n);
+    ctx->img_ncont.assign(n, 0);
+    ctx->pool->parallel_for(n, [&](int i, int wid) {
+        external_contours_bits(hb + (size_t)i * h * wpr, h, w, wpr, ctx->work[wid], ctx->cont[wid]);
+        ctx->img_ncont[i] = shapes_from_contours(ctx->cont[wid], ctx->shs[wid], ctx->img_shapes[i]);
+    });
+    for (int i = 0; i < n; i++) {
+        llfe_image_result &r = results[i0 + i];
+        r.shape_offset = total_shapes;
+        r.n_shapes = (int32_t)ctx->img_shapes[i].size();
+        r.n_contours = ctx->img_ncont[i];
+        for (size_t k = 0; k < ctx->img_shapes[i].size(); k++) {
+            if (shapes && total_shapes + (int64_t)k < shape_capacity) shapes[total_shapes + k] = ctx->img_shapes[i][k];
+        }
+        total_shapes += r.n_shapes;
+    }
+}
+
+// Recompute the dilated masks of a chunk synchronously on workspace 0 (the device is
+// idle after the hipDeviceSynchronize) -- the input is still the caller's.
+int redo_masks(llfe_ctx *ctx, const llfe_batch *b, int i0, int n, hipStream_t s) {
+    HIPCHK(ctx, hipDeviceSynchronize());
+    Work &W = ctx->ws[0];
+    const int h = b->height, w = b->width;
+    const uint8_t *img;
+    const int8_t *noise;
+    llfe_batch nb = *b;
+    nb.noise = nullptr;
+    int rc = stage_input(ctx, W, &nb, i0, n, &img, &noise, s);
+    if (rc) return rc;
+    HIPCHK(ctx, W.d_cls.ensure((size_t)n * h * w));
+    HIPCHK(ctx, W.d_bits.ensure((size_t)n * h * words_per_row(w)));
+    HIPCHK(ctx, launch_stencil(img, n, h, w, W.d_cls.p, nullptr, nullptr, nullptr, nullptr, ctx->sp, s));
+    return run_hysteresis_dilate(ctx, W, n, h, w, W.d_bits.p, nullptr, s);
+}
+
 // Shape records of a chunk whose contours ran on the GPU (slot's host copies).  A pass
 // that overflowed a capacity is redone for this chunk alone, synchronously, with the
-// capacities grown from what its counters asked for.
+// capacities grown from what its counters asked for.  A mask the GPU tracer does not
+// handle (a border-following anomaly, a contour wider than its LDS window, a deeper
+// Douglas-Peucker stack than it holds) is traced on the host pool instead: the chunk's
+// masks are recomputed, copied back and run through the bit-identical host path, so
+// one unusual image never fails its batch.
 int gpu_shapes_of_chunk(llfe_ctx *ctx, const llfe_batch *b, int i0, int n, int slot, llfe_image_result *results,
                         llfe_shape *shapes, int64_t shape_capacity, int64_t &total_shapes) {
     const int h = b->height, w = b->width;
     for (int attempt = 0;; attempt++) {
         const CtCounters ct = *ctx->h_ct_ctr_s[slot].p;
-        if (ct.flags & (kCtBadTrace | kCtTooWide | kCtDpOverflow))
-            return ctx->fail(LLFE_ERR_UNSUPPORTED, "GPU contours: unsupported mask (flags 0x%x)", ct.flags);
+        if ((ct.flags & (kCtBadTrace | kCtTooWide | kCtDpOverflow)) || ctx->force_ct_fallback) {
+            hipStream_t s = ctx->streams[0];
+            int rc = redo_masks(ctx, b, i0, n, s);
+            if (rc) return rc;
+            const size_t words = (size_t)n * h * words_per_row(w);
+            HIPCHK(ctx, ctx->h_bits_s[slot].ensure(words));
+            HIPCHK(ctx, hipMemcpyAsync(ctx->h_bits_s[slot].p, ctx->ws[0].d_bits.p, sizeof(uint64_t) * words,
+                                       hipMemcpyDeviceToHost, s));
+            HIPCHK(ctx, hipStreamSynchronize(s));
+            host_shapes_from_bits(ctx, ctx->h_bits_s[slot].p, n, h, w, i0, results, shapes, shape_capacity,
+                                  total_shapes);
+            ctx->host_fallbacks++;
+            return LLFE_OK;
+        }
         if (!(ct.flags & kCtOverflowMask)) break;
         if (attempt >= 8) return ctx->fail(LLFE_ERR_CAPACITY, "GPU contours: capacities still overflow (0x%x)", ct.flags);
         // redo the shapes path of this chunk on workspace 0 once the device is idle
-        HIPCHK(ctx, hipDeviceSynchronize());
+        hipStream_t s = ctx->streams[0];
+        int rc = redo_masks(ctx, b, i0, n, s);
+        if (rc) return rc;
         Work &W = ctx->ws[0];
         grow_contour_caps(W, n, h, w, ct);
-        hipStream_t s = ctx->streams[0];
-        const uint8_t *img;
-        const int8_t *noise;
-        llfe_batch nb = *b;
-        nb.noise = nullptr;
-        int rc = stage_input(ctx, W, &nb, i0, n, &img, &noise, s);
-        if (rc) return rc;
-        HIPCHK(ctx, W.d_cls.ensure((size_t)n * h * w));
-        HIPCHK(ctx, W.d_bits.ensure((size_t)n * h * words_per_row(w)));
-        HIPCHK(ctx, launch_stencil(img, n, h, w, W.d_cls.p, nullptr, nullptr, nullptr, nullptr, ctx->sp, s));
-        rc = run_hysteresis_dilate(ctx, W, n, h, w, W.d_bits.p, nullptr, s);
-        if (rc) return rc;
         rc = run_contours(ctx, W, n, h, w, W.d_bits.p, s);
         if (rc) return rc;
         rc = copy_contours(ctx, W, n, slot, s);
@@ -783,23 +834,7 @@ int finish_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, int i0, 
         int rc = gpu_shapes_of_chunk(ctx, b, i0, n, slot, results, shapes, shape_capacity, total_shapes);
         if (rc) return rc;
     } else if (want_shp) {
-        ctx->img_shapes.resize(n);
-        ctx->img_ncont.assign(n, 0);
-        const uint64_t *hb = ctx->h_bits_s[slot].p;
-        ctx->pool->parallel_for(n, [&](int i, int wid) {
-            external_contours_bits(hb + (size_t)i * h * wpr, h, w, wpr, ctx->work[wid], ctx->cont[wid]);
-            ctx->img_ncont[i] = shapes_from_contours(ctx->cont[wid], ctx->shs[wid], ctx->img_shapes[i]);
-        });
-        for (int i = 0; i < n; i++) {
-            llfe_image_result &r = results[i0 + i];
-            r.shape_offset = total_shapes;
-            r.n_shapes = (int32_t)ctx->img_shapes[i].size();
-            r.n_contours = ctx->img_ncont[i];
-            for (size_t k = 0; k < ctx->img_shapes[i].size(); k++) {
-                if (shapes && total_shapes + (int64_t)k < shape_capacity) shapes[total_shapes + k] = ctx->img_shapes[i][k];
-            }
-            total_shapes += r.n_shapes;
-        }
+        host_shapes_from_bits(ctx, ctx->h_bits_s[slot].p, n, h, w, i0, results, shapes, shape_capacity, total_shapes);
     }
     HIPCHK(ctx, hipEventSynchronize(ctx->chunk_done[slot]));
     if (want_col) {
@@ -826,6 +861,20 @@ int finish_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, int i0, 
 extern "C" {
 
 int llfe_abi_version(void) { return LLFE_ABI_VERSION; }
+
+// path of the HIP runtime this library's HIP calls resolved to (dladdr of hipMalloc):
+// a process must hold exactly one, shared with whatever produced its device pointers
+// and stream handles (e.g. PyTorch-ROCm's torch/lib/libamdhip64.so)
+const char *llfe_hip_runtime(void) {
+    static std::string path;
+    if (path.empty()) {
+        Dl_info info{};
+        hipError_t (*fn)(void **, size_t) = &hipMalloc;
+        if (dladdr((void *)fn, &info) && info.dli_fname) path = info.dli_fname;
+        else path = "?";
+    }
+    return path.c_str();
+}
 
 int llfe_init(int device, llfe_ctx **out) {
     if (!out) return LLFE_ERR_INVALID;
@@ -868,6 +917,7 @@ int llfe_init(int device, llfe_ctx **out) {
         if (!strcmp(cm, "host")) c->gpu_contours = false;
     }
     if (const char *cc = getenv("LLFE_CONCURRENT"); cc && atoi(cc) == 0) c->concurrent = false;
+    if (const char *ff = getenv("LLFE_CT_FORCE_HOST_FALLBACK"); ff && atoi(ff) == 1) c->force_ct_fallback = true;
     gauss_kernel_f32(11, c->sp.k11);
     c->pool = new Pool(default_threads() - 1);
     int nt = c->pool->size() + 1;

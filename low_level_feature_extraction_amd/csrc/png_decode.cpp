@@ -17,6 +17,8 @@
 #include <emmintrin.h>
 #include <zlib.h>
 
+#include <cstdlib>
+
 #include <algorithm>
 #include <atomic>
 #include <cstdint>
@@ -307,22 +309,46 @@ void row_to_bgr(const Png &png, const uint8_t *s, uint8_t *o) {
     }
 }
 
+// cv2.imdecode refuses images above CV_IO_MAX_IMAGE_PIXELS (default 2^30 pixels,
+// OPENCV_IO_MAX_IMAGE_PIXELS overrides): here LLFE_MAX_PIXELS, checked from the header
+// before anything is allocated
+uint64_t max_pixels() {
+    static const uint64_t m = [] {
+        const char *e = getenv("LLFE_MAX_PIXELS");
+        const long long v = e ? atoll(e) : 0;
+        return v > 0 ? (uint64_t)v : (uint64_t)1 << 30;
+    }();
+    return m;
+}
+
+// thread-local scratch above this size is released after each image, so one huge
+// decode does not pin its peak allocation in every decode thread
+constexpr size_t kKeepScratch = (size_t)64 << 20;
+
 int decode_one(const uint8_t *data, size_t size, int32_t h, int32_t w, uint8_t *out) {
     Png png;
     int rc = parse(data, size, png, false);
     if (rc) return rc;
     if ((int64_t)png.h != h || (int64_t)png.w != w) return LLFE_ERR_CAPACITY;
+    if ((uint64_t)png.w * png.h > max_pixels()) return LLFE_ERR_INVALID;
     const int bpp = png.channels() * png.depth / 8;
     const size_t rowb = (size_t)png.w * bpp, stride = rowb + 1, raw_n = stride * png.h;
+    // a zlib stream inflates at most ~1032:1: a declared size the IDAT payload cannot
+    // reach is corrupt -- rejected before the raw buffer is committed
+    size_t idat_n = 0;
+    for (auto &c : png.idat) idat_n += c.second;
+    if (raw_n / 1032 > idat_n + 64) return LLFE_ERR_INVALID;
     thread_local std::vector<uint8_t> raw, cat;
     raw.resize(raw_n);
-    if (!inflate_idat(png, raw.data(), raw_n, cat)) return LLFE_ERR_INVALID;
-    for (uint32_t y = 0; y < png.h; y++) {
+    rc = inflate_idat(png, raw.data(), raw_n, cat) ? LLFE_OK : LLFE_ERR_INVALID;
+    for (uint32_t y = 0; rc == LLFE_OK && y < png.h; y++) {
         uint8_t *r = raw.data() + y * stride;
-        if (!unfilter(r[0], r + 1, y ? r + 1 - stride : nullptr, rowb, bpp)) return LLFE_ERR_INVALID;
-        row_to_bgr(png, r + 1, out + (size_t)y * png.w * 3);
+        if (!unfilter(r[0], r + 1, y ? r + 1 - stride : nullptr, rowb, bpp)) rc = LLFE_ERR_INVALID;
+        else row_to_bgr(png, r + 1, out + (size_t)y * png.w * 3);
     }
-    return LLFE_OK;
+    if (raw.capacity() > kKeepScratch) std::vector<uint8_t>().swap(raw);
+    if (cat.capacity() > kKeepScratch) std::vector<uint8_t>().swap(cat);
+    return rc;
 }
 
 }  // namespace
@@ -335,11 +361,44 @@ extern "C" int llfe_png_info(const uint8_t *data, uint64_t size, int32_t *width,
     if (png.w > 0x7FFFFFFFu || png.h > 0x7FFFFFFFu) return LLFE_ERR_UNSUPPORTED;
     *width = (int32_t)png.w;
     *height = (int32_t)png.h;
+    if ((uint64_t)png.w * png.h > max_pixels()) return LLFE_ERR_CAPACITY;
     return LLFE_OK;
 }
 
-extern "C" int llfe_decode_png_batch(const uint8_t *const *data, const uint64_t *sizes, int32_t n, int32_t height,
-                                     int32_t width, uint8_t *out_bgr, int32_t *status, int32_t threads) {
+// ---------------------------------------------------------------- format dispatch
+int llfe_jpeg_info_one(const uint8_t *data, size_t size, int32_t *w, int32_t *h, int *ncomp);
+int llfe_jpeg_decode_one(const uint8_t *data, size_t size, int32_t h, int32_t w, uint8_t *out);
+
+namespace {
+constexpr uint8_t kPngSig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
+bool is_png(const uint8_t *d, size_t n) { return n >= 8 && !memcmp(d, kPngSig, 8); }
+bool is_jpeg(const uint8_t *d, size_t n) { return n >= 3 && d[0] == 0xFF && d[1] == 0xD8 && d[2] == 0xFF; }
+
+int decode_any(const uint8_t *d, size_t n, int32_t h, int32_t w, uint8_t *out) {
+    if (is_png(d, n)) return decode_one(d, n, h, w, out);
+    if (is_jpeg(d, n)) {
+        if ((uint64_t)(uint32_t)w * (uint32_t)h > max_pixels()) return LLFE_ERR_INVALID;
+        return llfe_jpeg_decode_one(d, n, h, w, out);
+    }
+    return LLFE_ERR_UNSUPPORTED;
+}
+}  // namespace
+
+extern "C" int llfe_image_info(const uint8_t *data, uint64_t size, int32_t *width, int32_t *height) {
+    if (!data || !width || !height) return LLFE_ERR_INVALID;
+    if (is_png(data, (size_t)size)) return llfe_png_info(data, size, width, height);
+    if (!is_jpeg(data, (size_t)size)) return LLFE_ERR_UNSUPPORTED;
+    int nc = 0;
+    const int rc = llfe_jpeg_info_one(data, (size_t)size, width, height, &nc);
+    if (rc) return rc;
+    if ((uint64_t)(uint32_t)*width * (uint32_t)*height > max_pixels()) return LLFE_ERR_CAPACITY;
+    return LLFE_OK;
+}
+
+namespace {
+template <typename F>
+int decode_fanout(const uint8_t *const *data, const uint64_t *sizes, int32_t n, int32_t height, int32_t width,
+                  uint8_t *out_bgr, int32_t *status, int32_t threads, F one) {
     if (n < 0 || (n && (!data || !sizes || !out_bgr || !status)) || height <= 0 || width <= 0) return LLFE_ERR_INVALID;
     const size_t img_bytes = (size_t)height * width * 3;
     const int nt = std::max(1, std::min<int>(threads > 0 ? threads : 1, n));
@@ -348,7 +407,7 @@ extern "C" int llfe_decode_png_batch(const uint8_t *const *data, const uint64_t 
         for (int i; (i = next.fetch_add(1)) < n;) {
             int rc;
             try {
-                rc = data[i] ? decode_one(data[i], (size_t)sizes[i], height, width, out_bgr + (size_t)i * img_bytes)
+                rc = data[i] ? one(data[i], (size_t)sizes[i], height, width, out_bgr + (size_t)i * img_bytes)
                              : LLFE_ERR_INVALID;
             } catch (const std::bad_alloc &) {
                 rc = LLFE_ERR_OOM;
@@ -363,4 +422,15 @@ extern "C" int llfe_decode_png_batch(const uint8_t *const *data, const uint64_t 
     for (int i = 0; i < n; i++)
         if (status[i]) return status[i];
     return LLFE_OK;
+}
+}  // namespace
+
+extern "C" int llfe_decode_png_batch(const uint8_t *const *data, const uint64_t *sizes, int32_t n, int32_t height,
+                                     int32_t width, uint8_t *out_bgr, int32_t *status, int32_t threads) {
+    return decode_fanout(data, sizes, n, height, width, out_bgr, status, threads, decode_one);
+}
+
+extern "C" int llfe_decode_batch(const uint8_t *const *data, const uint64_t *sizes, int32_t n, int32_t height,
+                                 int32_t width, uint8_t *out_bgr, int32_t *status, int32_t threads) {
+    return decode_fanout(data, sizes, n, height, width, out_bgr, status, threads, decode_any);
 }

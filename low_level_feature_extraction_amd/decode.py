@@ -4,7 +4,12 @@ Decoding stays on the host (north star); the reference decodes with OpenCV at
 image_processor.py:208-211 and utils.py:108-109.  IMREAD_COLOR yields an 8-bit,
 3-channel BGR array: alpha is dropped (not composited), grey and palette images are
 expanded, 16-bit samples are scaled by >> 8, and JPEG EXIF orientation is applied.
-Pillow (the reference's other imaging dependency) does the byte-level decoding here.
+
+PNG and JPEG go through libllfe's native host decoders (``llfe_decode_batch``:
+csrc/png_decode.cpp, and csrc/jpeg_decode.cpp over the system libjpeg-turbo with
+OpenCV's settings), fanned out over native threads; what they hand back (interlaced
+PNG, CMYK JPEG, EXIF-rotated JPEG, other formats) is decoded with Pillow.  Images
+above ``MAX_PIXELS`` (cv2's CV_IO_MAX_IMAGE_PIXELS, 2^30) fail like cv2.imdecode does.
 """
 from __future__ import annotations
 
@@ -18,37 +23,49 @@ class DecodeError(ValueError):
 
 
 _PNG_SIG = b"\x89PNG\r\n\x1a\n"
+MAX_PIXELS = 1 << 30  # cv2 CV_IO_MAX_IMAGE_PIXELS (libllfe: LLFE_MAX_PIXELS)
+_ERR_CAPACITY = -3
 
 
-def _png_native(blobs, h, w, out, threads) -> list:
-    """libllfe's host PNG decoder (csrc/png_decode.cpp) over all blobs into out[i];
-    non-PNG blobs get LLFE_ERR_INVALID.  Returns the per-image status list."""
+def _is_native(b) -> bool:
+    return b[:8] == _PNG_SIG or b[:3] == b"\xff\xd8\xff"
+
+
+def _native(blobs, h, w, out, threads) -> list:
+    """libllfe's host decoders (PNG / JPEG, llfe_decode_batch) over all blobs into
+    out[i]; other formats get LLFE_ERR_UNSUPPORTED.  Returns the per-image status list."""
     import ctypes as C
 
     from . import _lib
 
     L = _lib.lib()
     n = len(blobs)
-    keep = [C.c_char_p(b) if b[:8] == _PNG_SIG else None for b in blobs]
+    keep = [C.c_char_p(b) if _is_native(b) else None for b in blobs]
     ptrs = (C.c_void_p * n)(*[C.cast(k, C.c_void_p) if k is not None else None for k in keep])
     sizes = (C.c_uint64 * n)(*[len(b) for b in blobs])
     status = (C.c_int32 * n)()
-    L.llfe_decode_png_batch(ptrs, sizes, n, h, w, out.ctypes.data, status, int(threads))
+    L.llfe_decode_batch(ptrs, sizes, n, h, w, out.ctypes.data, status, int(threads))
     del keep
     return list(status)
 
 
-def _png_size(b):
+def _image_size(b):
+    """(h, w) of a PNG / JPEG from its header, None for other formats or unreadable
+    headers; DecodeError above MAX_PIXELS (cv2.imdecode returns None there)."""
     import ctypes as C
 
     from . import _lib
 
-    if b[:8] != _PNG_SIG:
+    if not _is_native(b):
         return None
     w, h = C.c_int32(), C.c_int32()
-    if _lib.lib().llfe_png_info(b, len(b), C.byref(w), C.byref(h)) != 0:
+    rc = _lib.lib().llfe_image_info(b, len(b), C.byref(w), C.byref(h))
+    if rc == _ERR_CAPACITY:
+        raise DecodeError(f"Failed to decode image: {w.value}x{h.value} exceeds {MAX_PIXELS} pixels")
+    if rc != 0:
         return None
     return h.value, w.value
+
 
 
 def decode_bgr(image_bytes: bytes) -> np.ndarray:
@@ -57,15 +74,19 @@ def decode_bgr(image_bytes: bytes) -> np.ndarray:
 
     if not image_bytes:
         raise DecodeError("Failed to decode image")
-    hw = _png_size(image_bytes)
-    if hw is not None:  # native PNG path; anything it does not take goes through Pillow
+    hw = _image_size(image_bytes)
+    if hw is not None:  # native PNG / JPEG path; anything it does not take goes through Pillow
         out = np.empty((1, hw[0], hw[1], 3), np.uint8)
-        if _png_native([image_bytes], hw[0], hw[1], out, 1)[0] == 0:
+        if _native([image_bytes], hw[0], hw[1], out, 1)[0] == 0:
             return out[0]
     try:
         im = Image.open(io.BytesIO(image_bytes))
+        if im.width * im.height > MAX_PIXELS:
+            raise DecodeError(f"Failed to decode image: {im.width}x{im.height} exceeds {MAX_PIXELS} pixels")
         im.load()
-    except (UnidentifiedImageError, OSError, ValueError, SyntaxError) as e:
+    except (UnidentifiedImageError, OSError, ValueError, SyntaxError, Image.DecompressionBombError) as e:
+        if isinstance(e, DecodeError):
+            raise
         raise DecodeError("Failed to decode image") from e
     if im.format == "JPEG":
         im = ImageOps.exif_transpose(im)
@@ -99,17 +120,34 @@ _POOL = None
 _POOL_LOCK = None
 
 
+def usable_cores() -> int:
+    """CPUs this process may run on (affinity mask, capped by a cgroup v2 cpu.max quota)."""
+    import os
+
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        n = os.cpu_count() or 1
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
 def default_decode_threads() -> int:
+    """The rank's share of the host cores: usable cores / LOCAL_WORLD_SIZE (one process
+    per GPU shares the node's cores), LLFE_DECODE_THREADS overrides."""
     import os
 
     env = os.environ.get("LLFE_DECODE_THREADS")
     if env and int(env) > 0:
         return int(env)
-    try:
-        n = len(os.sched_getaffinity(0))
-    except AttributeError:  # pragma: no cover
-        n = os.cpu_count() or 1
-    return max(1, min(n, 16))
+    local = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1))
+    return max(1, min(usable_cores() // local, 64))
 
 
 def _pool(workers=None):
@@ -147,7 +185,7 @@ def decode_batch(blobs, out=None, workers=None) -> np.ndarray:
     blobs = [bytes(b) for b in blobs]
     if not blobs:
         raise DecodeError("empty batch")
-    hw = _png_size(blobs[0])
+    hw = _image_size(blobs[0])
     first = None if hw is not None else decode_bgr(blobs[0])
     h, w = hw if hw is not None else first.shape[:2]
     if out is None:
@@ -155,8 +193,8 @@ def decode_batch(blobs, out=None, workers=None) -> np.ndarray:
     if out.shape != (len(blobs), h, w, 3) or out.dtype != np.uint8 or not out.flags.c_contiguous:
         raise ValueError(f"out must be a C-contiguous {(len(blobs), h, w, 3)} uint8 array, got {out.shape} {out.dtype}")
     todo = list(range(len(blobs)))
-    if hw is not None:  # PNG batch: native decoder, Pillow for whatever it leaves
-        st = _png_native(blobs, h, w, out, workers or default_decode_threads())
+    if hw is not None:  # PNG / JPEG batch: native decoders, Pillow for whatever they leave
+        st = _native(blobs, h, w, out, workers or default_decode_threads())
         todo = [i for i, s_ in enumerate(st) if s_ != 0]
     else:
         out[0] = first

@@ -52,9 +52,12 @@ def assemble(r, features: Iterable[str]) -> dict:
 
 
 def run_batch(images, features: Sequence[str] = ("colors", "shapes", "shadows"), seed: Optional[int] = None,
-              noise=None, backend: Optional[Backend] = None, raw: bool = False, n_colors: int = 5) -> List[dict]:
+              noise=None, backend: Optional[Backend] = None, raw: bool = False, n_colors: int = 5,
+              index_base: Optional[int] = None) -> List[dict]:
     """images: N x H x W x 3 BGR uint8 array / torch tensor, or a list of H x W x 3
-    arrays of any sizes.  Returns one dict per image, in input order."""
+    arrays of any sizes.  Returns one dict per image, in input order.  ``index_base``
+    fixes the global index of image 0 (the per-image noise / k-means seeds); by default
+    the process counter hands out fresh indices."""
     from . import color_extractor as ce
 
     be = backend or Backend.get()
@@ -64,14 +67,14 @@ def run_batch(images, features: Sequence[str] = ("colors", "shapes", "shadows"),
         seed = ce._SEED
     if isinstance(images, np.ndarray) and images.ndim == 4 or hasattr(images, "data_ptr"):
         n = int(images.shape[0])
-        base = ce._next_index(n)
+        base = ce._next_index(n) if index_base is None else int(index_base)
         res = be.process(images, feats, seed=seed, noise=noise, index_base=base, n_colors=n_colors)
         return res if raw else [assemble(r, feats) for r in res]
     imgs = [np.ascontiguousarray(np.asarray(im, np.uint8)) for im in images]
     for im in imgs:
         if im.ndim != 3 or im.shape[2] != 3:
             raise ValueError(f"expected H x W x 3 BGR uint8 images, got {im.shape}")
-    base = ce._next_index(len(imgs))
+    base = ce._next_index(len(imgs)) if index_base is None else int(index_base)
     groups = defaultdict(list)
     for i, im in enumerate(imgs):
         groups[im.shape[:2]].append(i)

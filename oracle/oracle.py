@@ -316,7 +316,7 @@ def dominant_colors(bgr, noise=None, n_colors=5, rng_state=0xFFFFFFFF):
     counts (K,), n_unique, compactness); counts = np.bincount(labels)."""
     bgr = _chk_bgr(bgr)
     h, w = bgr.shape[:2]
-    cap = max(n_colors, 1)
+    cap = max(n_colors, 5)
     centers = np.zeros((cap, 3), np.uint8)
     counts = np.zeros(cap, np.int32)
     nu = C.c_int64()

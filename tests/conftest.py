@@ -44,3 +44,19 @@ def orc():
 
     oracle.lib()
     return oracle
+
+
+def pytest_sessionfinish(session, exitstatus):
+    """Write the observed k-means parity statistics (tests/kmeans_bar.py) of a GPU run."""
+    try:
+        from tests import kmeans_bar
+    except ImportError:  # pragma: no cover
+        return
+    summ = kmeans_bar.summary()
+    if summ:
+        import json
+
+        out = os.path.join(ROOT, "gpurun_out")
+        os.makedirs(out, exist_ok=True)
+        with open(os.path.join(out, "kmeans_parity_observed.json"), "w") as f:
+            json.dump(summ, f, indent=1)

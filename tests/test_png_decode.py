@@ -80,10 +80,10 @@ def _pillow_ref(b):
 
 
 def _native(b):
-    hw = decode._png_size(b)
+    hw = decode._image_size(b)
     assert hw is not None
     out = np.zeros((1, hw[0], hw[1], 3), np.uint8)
-    st = decode._png_native([b], hw[0], hw[1], out, 1)
+    st = decode._native([b], hw[0], hw[1], out, 1)
     return st[0], out[0]
 
 
