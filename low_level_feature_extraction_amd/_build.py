@@ -14,7 +14,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libllfe.so")
-SOURCES = ["llfe_api.cpp", "contours.cpp", "png_decode.cpp", "jpeg_decode.cpp", "stencil.hip", "hysteresis.hip", "unique.hip", "kmeans.hip", "resize.hip", "contours_gpu.hip",
+SOURCES = ["llfe_api.cpp", "contours.cpp", "png_decode.cpp", "jpeg_decode.cpp", "stencil.hip", "stencil_stream.hip", "hysteresis.hip", "unique.hip", "kmeans.hip", "resize.hip", "contours_gpu.hip",
            "cvresize.hip"]
 HEADERS = ["llfe_internal.h", "contours.h"]
 ARCH = os.environ.get("LLFE_OFFLOAD_ARCH", "gfx950")
@@ -53,7 +53,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
             lang = ["-x", "c++"]
         else:
             lang = ["-x", "hip", f"--offload-arch={ARCH}"]
-        cmd = [hipcc, *common, *lang, "-c", os.path.join(CSRC, src), "-o", obj]
+        extra = ["-fno-slp-vectorize"] if src == "stencil_stream.hip" else []  # keep the scalar fma chains scalar
+        cmd = [hipcc, *common, *lang, *extra, "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))

@@ -311,7 +311,7 @@ struct Profiler {
     }
 };
 
-size_t shadow_tiles(int n, int h, int w) { return (size_t)n * tiles_x(w) * tiles_y(h); }
+size_t shadow_tiles(int n, int h, int w) { return stencil_parts(n, h, w); }
 
 // Images per device pass.  One pass per call when the workspace allows it: a bigger
 // pass amortises the k-means launch's tail (its longest attempts run 100 Lloyd

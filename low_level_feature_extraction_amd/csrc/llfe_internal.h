@@ -23,10 +23,19 @@ struct StencilParams {
 //   cls (may be null): n x h x w u8, 0 weak / 1 suppressed / 2 strong
 //   blurred (may be null): n x h x w u8 (parity of GaussianBlur 5x5)
 //   shadow_sum/shadow_cnt (may be null): per image u64 accumulators (zeroed by caller)
-// shadow_sum / shadow_cnt (when non-null) need tile_part scratch of n * tiles_x(w) * tiles_y(h)
+// shadow_sum / shadow_cnt (when non-null) need tile_part scratch of stencil_parts(n, h, w)
+// entries.  Without `blurred` the row-streaming kernel runs (launch_stencil_stream).
 hipError_t launch_stencil(const uint8_t *bgr, int n, int h, int w, uint8_t *cls, uint8_t *blurred,
                           unsigned long long *shadow_sum, unsigned long long *shadow_cnt, uint2 *tile_part,
                           const StencilParams &p, hipStream_t s);
+
+// The row-streaming form of launch_stencil's cls / shadow outputs (stencil_stream.hip;
+// one wave per 240-column strip and row segment, DPP neighbours, register rings).
+// wave_part: stencil_stream_parts(n, h, w) entries of scratch when shadows are wanted.
+size_t stencil_stream_parts(int n, int h, int w);
+hipError_t launch_stencil_stream(const uint8_t *bgr, int n, int h, int w, uint8_t *cls,
+                                 unsigned long long *shadow_sum, unsigned long long *shadow_cnt, uint2 *wave_part,
+                                 const StencilParams &p, hipStream_t s);
 
 // FontDetector.preprocess_image (font_detector.py:17-37): gray -> adaptiveThreshold(
 // GAUSSIAN_C, THRESH_BINARY_INV, 11, 2) -> n x h x w u8 255 / 0 (the stencil kernel
@@ -102,6 +111,10 @@ hipError_t launch_contours(const uint64_t *bits, int n, int h, int w, const CtWo
 inline int words_per_row(int w) { return (w + 63) / 64; }
 inline int tiles_x(int w) { return (w + kTileW - 1) / kTileW; }
 inline int tiles_y(int h) { return (h + kTileH - 1) / kTileH; }
+inline size_t stencil_parts(int n, int h, int w) {
+    const size_t a = (size_t)n * tiles_x(w) * tiles_y(h), b = stencil_stream_parts(n, h, w);
+    return a > b ? a : b;
+}
 
 // ---------------------------------------------------------------- colours
 constexpr int kMaxK = 5;

@@ -11,6 +11,8 @@
 //            sum/count of blur under the mask -> one u64 atomic pair per tile.
 // Only the class map (1 B/px) leaves the tile; hysteresis + dilate follow in
 // separate launches (global connectivity).
+#include <cstdlib>
+
 #include "llfe_internal.h"
 
 namespace llfe {
@@ -408,6 +410,8 @@ __global__ __launch_bounds__(NT) void k_stencil(const uint8_t *__restrict__ bgr,
 hipError_t launch_stencil(const uint8_t *bgr, int n, int h, int w, uint8_t *cls, uint8_t *blurred,
                           unsigned long long *shadow_sum, unsigned long long *shadow_cnt, uint2 *tile_part,
                           const StencilParams &p, hipStream_t s) {
+    if (!blurred && !getenv("LLFE_TILED_STENCIL"))
+        return launch_stencil_stream(bgr, n, h, w, cls, shadow_sum, shadow_cnt, tile_part, p, s);
     int ntx = tiles_x(w), nty = tiles_y(h);
     dim3 grid(ntx * nty, n);
     hipLaunchKernelGGL(k_stencil, grid, dim3(NT), 0, s, bgr, h, w, ntx, nty, cls, blurred,

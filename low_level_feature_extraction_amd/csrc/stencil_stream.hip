@@ -1,0 +1,480 @@
+// Row-streaming stencil front-end of the shapes + shadows path on gfx950.
+//
+// Replaces, per pixel, the native work of
+//   gray   = cvtColor(BGR2GRAY)                        shape pyc @L18, shadow pyc @L8
+//   blur   = GaussianBlur(gray, (5,5), 0) 8U bit-exact shape pyc @L21, shadow pyc @L9
+//   Canny  : Sobel3 (REPLICATE) -> |dx|+|dy| -> NMS    shape pyc @L24 (classes 0/1/2)
+//   shadow : adaptiveThreshold GAUSSIAN_C 11, C=2, INV  shadow pyc @L17-24
+//            mean = rint(CV_32F Gauss11(blur)), mask = blur - mean <= -2,
+//            sum / count of blur under the mask
+// with the same arithmetic as the tiled kernel (stencil.hip) and the oracle.
+//
+// Layout.  One wave owns a vertical strip of 256 columns (64 lanes x 4 pixels, one
+// packed dword of gray / blur per lane) and marches down a segment of rows.  Of the 64
+// lanes, 2 on each side are halo (8 columns): every horizontal neighbour a pixel
+// needs -- blur5 +-2, Sobel / NMS +-1, Gauss11 +-5 on the blurred row -- comes from lanes
+// L-2 .. L+2 through DPP wave shifts, so 240 columns per wave are exact (1920 = 8 x
+// 240).  Vertical neighbours live in registers: the gray rows of the blur5 in a
+// 5-row ring, and the blurred rows, the Canny magnitude rows and the CV_32F row-pass
+// results of Gauss11 in 11-slot rings indexed by the row modulo 11 -- the row loop is
+// unrolled 11 times, so every ring slot is a fixed register.  One BGR row is loaded
+// per step (3 dwords per lane, coalesced, two steps ahead), each pixel is read from
+// HBM once plus a 16/256 column and 10/rows row halo, and nothing goes through LDS:
+// no barriers, no halo recomputation beyond those margins.
+//
+// Per step (blur row c = clamp(t, 0, H-1) enters; REPLICATE of the blurred image):
+//   gray row reflect101(c + 2) -> vertical then horizontal blur5 (exact integer, any
+//   order: (sum w_i w_j g + 128) >> 8 in packed u16) -> blur ring
+//   CV_32F row pass of the blurred row (fma chain left -> right) -> Gauss ring
+//   Sobel on blurred rows t-2..t (packed i16) -> |dx|+|dy| | dir << 12 -> magnitude ring
+//   NMS of row t-2 from magnitude rows t-3..t-1 -> class map row t-2
+//   column pass (centre, then symmetric pairs inner -> outer) of row t-5, rint,
+//   mask, masked sum / count
+#include "llfe_internal.h"
+
+namespace llfe {
+namespace {
+
+constexpr int kLanesOut = 60;               // lanes 2 .. 61 produce output
+constexpr int kStripW = 4 * kLanesOut;      // 240 output columns per wave
+constexpr int kHalo = 8;                    // columns left of the strip's first output
+constexpr int kRing = 11;
+constexpr int kWavesPerBlock = 4;
+
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+typedef int16_t i16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ u16x2 U(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+__device__ __forceinline__ i16x2 I(uint32_t v) { return __builtin_bit_cast(i16x2, v); }
+__device__ __forceinline__ uint32_t W32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ uint32_t W32(i16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ uint32_t byte_of(uint32_t w, int i) { return (w >> (8 * i)) & 255u; }
+
+// DPP wave shifts: from_left(v) in lane L is v of lane L-1; from_right(v) of lane L+1
+// (bound_ctrl: the lanes shifted in at the wave's ends read 0 -- they are halo lanes)
+__device__ __forceinline__ uint32_t from_left(uint32_t v) { return __builtin_amdgcn_mov_dpp(v, 0x138, 0xf, 0xf, true); }
+__device__ __forceinline__ uint32_t from_right(uint32_t v) { return __builtin_amdgcn_mov_dpp(v, 0x130, 0xf, 0xf, true); }
+// (hi16 of a, lo16 of b) -> the u16 pair straddling two adjacent dwords a, b
+__device__ __forceinline__ uint32_t mid16(uint32_t a, uint32_t b) { return __builtin_amdgcn_alignbit(b, a, 16); }
+
+__device__ __forceinline__ int reflect101(int p, int len) {
+    if ((unsigned)p < (unsigned)len) return p;
+    if (len == 1) return 0;
+    do {
+        p = p < 0 ? -p : 2 * len - 2 - p;
+    } while ((unsigned)p >= (unsigned)len);
+    return p;
+}
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+struct Raw {
+    uint32_t a, b, c;
+};
+
+// 4 BGR pixels of row y at the lane's columns: one aligned 12-byte load when the whole
+// wave is inside the image (wave-uniform `fast`), else 12 byte loads from the
+// REFLECT_101 columns precomputed in coff (byte offsets within a row)
+__device__ __forceinline__ Raw load_px(const uint8_t *__restrict__ img, int y, int W, int x, bool fast,
+                                       const uint32_t coff[4]) {
+    const uint8_t *row = img + (uint32_t)(y * W * 3);  // an image is < 4 GiB
+    Raw r;
+    if (fast) {
+        const uint32_t *p = (const uint32_t *)(row + (uint32_t)(x * 3));
+        r.a = __builtin_nontemporal_load(p);
+        r.b = __builtin_nontemporal_load(p + 1);
+        r.c = __builtin_nontemporal_load(p + 2);
+    } else {
+        uint32_t v[3] = {0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint8_t *q = row + coff[j];
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                const int k = 3 * j + c;
+                v[k >> 2] |= (uint32_t)q[c] << (8 * (k & 3));
+            }
+        }
+        r.a = v[0];
+        r.b = v[1];
+        r.c = v[2];
+    }
+    return r;
+}
+
+// Y = (B*1868 + G*9617 + R*4899 + 2^13) >> 14 for the 4 pixels -> packed u8x4
+__device__ __forceinline__ uint32_t gray4(Raw r) {
+    const u16x2 bg0 = U(__builtin_amdgcn_perm(0u, r.a, 0x0c010c00u));
+    const u16x2 bg1 = U(__builtin_amdgcn_perm(r.b, r.a, 0x0c040c03u));
+    const u16x2 bg2 = U(__builtin_amdgcn_perm(0u, r.b, 0x0c030c02u));
+    const u16x2 bg3 = U(__builtin_amdgcn_perm(0u, r.c, 0x0c020c01u));
+    const u16x2 wbg = {1868, 9617};
+    const uint32_t y0 = __builtin_amdgcn_udot2(bg0, wbg, byte_of(r.a, 2) * 4899u + 8192u, false) >> 14;
+    const uint32_t y1 = __builtin_amdgcn_udot2(bg1, wbg, byte_of(r.b, 1) * 4899u + 8192u, false) >> 14;
+    const uint32_t y2 = __builtin_amdgcn_udot2(bg2, wbg, byte_of(r.c, 0) * 4899u + 8192u, false) >> 14;
+    const uint32_t y3 = __builtin_amdgcn_udot2(bg3, wbg, byte_of(r.c, 3) * 4899u + 8192u, false) >> 14;
+    return y0 | (y1 << 8) | (y2 << 16) | (y3 << 24);
+}
+
+__device__ __forceinline__ uint32_t lo2(uint32_t g) { return __builtin_amdgcn_perm(0u, g, 0x0c010c00u); }  // bytes 0,1 -> u16x2
+__device__ __forceinline__ uint32_t hi2(uint32_t g) { return __builtin_amdgcn_perm(0u, g, 0x0c030c02u); }  // bytes 2,3 -> u16x2
+
+// blur5 of the lane's 4 columns from the 5 gray rows (vertical taps unscaled, then the
+// horizontal taps with the neighbours' vertical sums; (sum + 128) >> 8 -- exact)
+__device__ __forceinline__ uint32_t blur4(uint32_t g0, uint32_t g1, uint32_t g2, uint32_t g3, uint32_t g4) {
+    const u16x2 four = {4, 4}, six = {6, 6};
+    const u16x2 vlo = (U(lo2(g1)) + U(lo2(g3))) * four + (U(lo2(g0)) + U(lo2(g4))) + U(lo2(g2)) * six;
+    const u16x2 vhi = (U(hi2(g1)) + U(hi2(g3))) * four + (U(hi2(g0)) + U(hi2(g4))) + U(hi2(g2)) * six;
+    const uint32_t A = from_left(W32(vhi));   // cols c-2, c-1
+    const uint32_t B = W32(vlo), C = W32(vhi);
+    const uint32_t D = from_right(W32(vlo));  // cols c+4, c+5
+    const u16x2 pm1 = U(mid16(A, B)), p1 = U(mid16(B, C)), p3 = U(mid16(C, D));
+    const u16x2 r128 = {128, 128}, e8 = {8, 8};
+    const u16x2 hlo = ((pm1 + p1) * four + (U(A) + U(C)) + U(B) * six + r128) >> e8;
+    const u16x2 hhi = ((p1 + p3) * four + (U(B) + U(D)) + U(C) * six + r128) >> e8;
+    return __builtin_amdgcn_perm(W32(hhi), W32(hlo), 0x06040200u);
+}
+
+// Sobel (3x3, on REPLICATE'd blurred rows b0 above, b1, b2 below) -> |dx|+|dy| and the
+// Canny NMS direction class (0 horizontal, 1 vertical, 2 / 3 diagonals) as
+// m | dir << 12 in two u16x2 dwords (cols c0 c1 | c2 c3)
+__device__ __forceinline__ void sobel4(uint32_t b0, uint32_t b1, uint32_t b2, uint32_t &mlo, uint32_t &mhi) {
+    const u16x2 two = {2, 2};
+    const u16x2 vs_lo = U(lo2(b0)) + U(lo2(b2)) + U(lo2(b1)) * two;  // [1 2 1] vertical
+    const u16x2 vs_hi = U(hi2(b0)) + U(hi2(b2)) + U(hi2(b1)) * two;
+    const u16x2 vd_lo = U(lo2(b2)) - U(lo2(b0));                       // [-1 0 1] vertical
+    const u16x2 vd_hi = U(hi2(b2)) - U(hi2(b0));
+    const uint32_t sL = from_left(W32(vs_hi)), sR = from_right(W32(vs_lo));
+    const uint32_t dL = from_left(W32(vd_hi)), dR = from_right(W32(vd_lo));
+    // gx(c) = vs(c+1) - vs(c-1); gy(c) = vd(c-1) + 2 vd(c) + vd(c+1)
+    const i16x2 gx_lo = I(mid16(W32(vs_lo), W32(vs_hi))) - I(mid16(sL, W32(vs_lo)));
+    const i16x2 gx_hi = I(mid16(W32(vs_hi), sR)) - I(mid16(W32(vs_lo), W32(vs_hi)));
+    const i16x2 t2 = {2, 2};
+    const i16x2 gy_lo = I(mid16(dL, W32(vd_lo))) + I(mid16(W32(vd_lo), W32(vd_hi))) + I(W32(vd_lo)) * t2;
+    const i16x2 gy_hi = I(mid16(W32(vd_lo), W32(vd_hi))) + I(mid16(W32(vd_hi), dR)) + I(W32(vd_hi)) * t2;
+    const i16x2 z = {0, 0};
+    const i16x2 ax_lo = __builtin_elementwise_max(gx_lo, z - gx_lo), ax_hi = __builtin_elementwise_max(gx_hi, z - gx_hi);
+    const i16x2 ay_lo = __builtin_elementwise_max(gy_lo, z - gy_lo), ay_hi = __builtin_elementwise_max(gy_hi, z - gy_hi);
+    const i16x2 m_lo = ax_lo + ay_lo, m_hi = ax_hi + ay_hi;
+    uint32_t lo = W32(m_lo), hi = W32(m_hi);
+    // the direction class matters only where m > LOW (the NMS below): computed, without
+    // branches, only when some lane of the wave has such a pixel
+    constexpr int LOW = 50, TG22 = 13573;
+    const bool need = (int)m_lo.x > LOW || (int)m_lo.y > LOW || (int)m_hi.x > LOW || (int)m_hi.y > LOW;
+    if (__ballot(need)) {
+        const int gxs[4] = {gx_lo.x, gx_lo.y, gx_hi.x, gx_hi.y};
+        const int gys[4] = {gy_lo.x, gy_lo.y, gy_hi.x, gy_hi.y};
+        const int axs[4] = {ax_lo.x, ax_lo.y, ax_hi.x, ax_hi.y};
+        const int ays[4] = {ay_lo.x, ay_lo.y, ay_hi.x, ay_hi.y};
+        uint32_t d[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int ax = axs[j], ay = ays[j] << 15, tg22x = ax * TG22;
+            // 0 if ay < tg22x, else 1 if ay > tg22x + ax * 2^16, else 2 / 3 by the signs --
+            // as arithmetic on 0/1 flags, so the compiler emits no branches
+            const uint32_t diag = 3u - (uint32_t)((gxs[j] ^ gys[j]) < 0);
+            const uint32_t ge = (uint32_t)(ay >= tg22x), steep = (uint32_t)(ay > tg22x + (ax << 16));
+            d[j] = ge * (diag - steep * (diag - 1u));
+        }
+        lo |= (d[0] << 12) | (d[1] << 28);
+        hi |= (d[2] << 12) | (d[3] << 28);
+    }
+    mlo = lo;
+    mhi = hi;
+}
+
+// Canny NMS + double threshold of the lane's 4 pixels of the middle magnitude row;
+// a = above, m = middle, b = below (lo = cols c0 c1, hi = c2 c3, m | dir << 12).  Called
+// by the whole wave (DPP), branch-free per pixel.
+__device__ __forceinline__ uint32_t nms4(uint32_t alo, uint32_t ahi, uint32_t mlo, uint32_t mhi, uint32_t blo,
+                                         uint32_t bhi) {
+    constexpr int LOW = 50, HIGH = 150;
+    const uint32_t aL = from_left(ahi), aR = from_right(alo);
+    const uint32_t mL = from_left(mhi), mR = from_right(mlo);
+    const uint32_t bL = from_left(bhi), bR = from_right(blo);
+    // magnitudes of columns -1 .. 4 (index c + 1)
+    auto cols = [](uint32_t L, uint32_t lo, uint32_t hi, uint32_t R, int *v) {
+        v[0] = (int)((L >> 16) & 4095u);
+        v[1] = (int)(lo & 4095u);
+        v[2] = (int)((lo >> 16) & 4095u);
+        v[3] = (int)(hi & 4095u);
+        v[4] = (int)((hi >> 16) & 4095u);
+        v[5] = (int)(R & 4095u);
+    };
+    int A[6], M[6], Bv[6];
+    cols(aL, alo, ahi, aR, A);
+    cols(mL, mlo, mhi, mR, M);
+    cols(bL, blo, bhi, bR, Bv);
+    const uint32_t dirs[4] = {(mlo >> 12) & 15u, mlo >> 28, (mhi >> 12) & 15u, mhi >> 28};
+    uint32_t o = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int m = M[j + 1];
+        // neighbours by direction: 0 left / right, 1 up / down, 2 up-right / down-left,
+        // 3 up-left / down-right -- selected on the two bits of dir (equality chains on
+        // dir become switch tables in scratch memory)
+        const bool b0 = dirs[j] & 1u, b1 = dirs[j] & 2u;
+        const int n1 = b1 ? (b0 ? A[j] : A[j + 2]) : (b0 ? A[j + 1] : M[j]);
+        const int n2 = b1 ? (b0 ? Bv[j + 2] : Bv[j]) : (b0 ? Bv[j + 1] : M[j + 2]);
+        // the second neighbour takes >= for 0 / 1 and > for the diagonals
+        const bool keep = m > LOW && m > n1 && m + (b1 ? 0 : 1) > n2;
+        const uint32_t c = keep ? (m > HIGH ? 2u : 0u) : 1u;
+        o |= c << (8 * j);
+    }
+    return o;
+}
+
+// CV_32F Gauss11 row pass (s = 0; s = fma(x[k-5], k[k], s) left -> right) of the lane's
+// 4 columns of one blurred row B; taps reach lanes L-2 .. L+2
+__device__ __forceinline__ void rowpass4(uint32_t B, const float *__restrict__ k11, f32x2 &o01, f32x2 &o23) {
+    const uint32_t l1 = from_left(B), l2 = from_left(l1), r1 = from_right(B), r2 = from_right(r1);
+    // taps for column c0 + j: bytes (c0 - 5 + j) .. (c0 + 5 + j); index 0 = c0 - 5
+    float x[14];
+    x[0] = (float)byte_of(l2, 3);
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        x[1 + i] = (float)byte_of(l1, i);
+        x[5 + i] = (float)byte_of(B, i);
+        x[9 + i] = (float)byte_of(r1, i);
+    }
+    x[13] = (float)byte_of(r2, 0);
+    float o[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int k = 0; k < 11; k++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) o[j] = __builtin_fmaf(x[k + j], k11[k], o[j]);
+    o01 = f32x2{o[0], o[1]};
+    o23 = f32x2{o[2], o[3]};
+}
+
+template <bool CLS, bool SHD>
+__global__ __launch_bounds__(64 * kWavesPerBlock) void k_stencil_stream(
+    const uint8_t *__restrict__ bgr, int H, int W, int strips, int segs, int seg_rows, int total_waves, int vec,
+    uint8_t *__restrict__ cls, uint2 *__restrict__ wave_part, StencilParams prm) {
+    const int lane = threadIdx.x & 63;
+    // wave-uniform (SGPR) wave index: every per-wave quantity below -- strip, segment,
+    // row bounds, border flags -- then stays scalar and its branches cost no exec masking
+    const int wid = blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    if (wid >= total_waves) return;  // whole wave leaves
+    const int strip = wid % strips;
+    const int rest = wid / strips;
+    const int seg = rest % segs;
+    const int img_i = rest / segs;
+    const uint8_t *img = bgr + (size_t)img_i * H * W * 3;
+    uint8_t *cimg = CLS ? cls + (size_t)img_i * H * W : nullptr;
+    const int ya = seg * seg_rows, yb = min(H, ya + seg_rows);
+    const int x = strip * kStripW - kHalo + 4 * lane;  // the lane's first column
+    const bool out_lane = lane >= 2 && lane < 2 + kLanesOut && x < W;
+    const bool out_fast = out_lane && vec && x + 4 <= W;
+    // wave covers the left / right image border: gray columns outside are REFLECT_101'd
+    // (byte loads), blurred columns outside REPLICATE'd; interior waves load 12 aligned
+    // bytes per lane
+    const int xw0 = strip * kStripW - kHalo, xw1 = xw0 + 256;
+    const bool edge_l = xw0 < 0, edge_r = xw1 > W;
+    const bool edge = edge_l || edge_r;
+    const bool fast = vec && !edge;  // wave-uniform
+    uint32_t coff[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) coff[j] = (uint32_t)(reflect101(x + j, W) * 3);
+    // blurred bytes of column 0 / W-1 (REPLICATE) come from these lanes
+    const int lane0 = (0 - xw0) >> 2, laneW = (W - 1 - xw0) >> 2;
+    uint32_t rep_l = 0, rep_r = 0;  // bytes of the lane left of column 0 / right of W-1
+    // per-column "inside the image" masks for the magnitude (Canny: no magnitude outside)
+    uint32_t in_lo = 0xffffffffu, in_hi = 0xffffffffu;
+    if (edge) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if (x + j < 0) rep_l |= 255u << (8 * j);
+            if (x + j >= W) rep_r |= 255u << (8 * j);
+        }
+        in_lo = ((unsigned)x < (unsigned)W ? 0xffffu : 0u) | ((unsigned)(x + 1) < (unsigned)W ? 0xffff0000u : 0u);
+        in_hi = ((unsigned)(x + 2) < (unsigned)W ? 0xffffu : 0u) | ((unsigned)(x + 3) < (unsigned)W ? 0xffff0000u : 0u);
+    }
+    float k11[11];
+#pragma unroll
+    for (int k = 0; k < 11; k++) k11[k] = prm.k11[k];
+
+    const int t0 = ya - 5, t_end = yb + 5;
+    auto crow = [&](int t) { return clampi(t, 0, H - 1); };
+    auto loadrow = [&](int t) { return reflect101(crow(t) + 2, H); };
+    // gray ring: rows reflect101(c - 2 .. c + 1) of the blur row c = crow(t) entering next
+    const int c0 = crow(t0);
+    uint32_t g0 = gray4(load_px(img, reflect101(c0 - 2, H), W, x, fast, coff));
+    uint32_t g1 = gray4(load_px(img, reflect101(c0 - 1, H), W, x, fast, coff));
+    uint32_t g2 = gray4(load_px(img, reflect101(c0, H), W, x, fast, coff));
+    uint32_t g3 = gray4(load_px(img, reflect101(c0 + 1, H), W, x, fast, coff));
+    Raw q0 = load_px(img, loadrow(t0), W, x, fast, coff);
+    Raw q1 = load_px(img, loadrow(t0 + 1), W, x, fast, coff);
+
+    uint32_t bring[kRing];
+    uint32_t mlo[kRing], mhi[kRing];
+    f32x2 ra[kRing], rb[kRing];
+#pragma unroll
+    for (int k = 0; k < kRing; k++) {
+        bring[k] = 0;
+        mlo[k] = mhi[k] = 0;
+        ra[k] = rb[k] = f32x2{0.0f, 0.0f};
+    }
+    uint32_t lsum = 0, lcnt = 0;
+
+    for (int tb = t0; tb < t_end; tb += kRing) {
+#pragma unroll
+        for (int k = 0; k < kRing; k++) {
+            const int t = tb + k;
+            if (t < t_end) {  // (no break: the loop must unroll so ring slots are registers)
+            // ---- blur row crow(t) enters
+            const Raw raw = q0;
+            q0 = q1;
+            q1 = load_px(img, loadrow(t + 2), W, x, fast, coff);
+            const uint32_t g4 = gray4(raw);
+            uint32_t B = blur4(g0, g1, g2, g3, g4);
+            if (crow(t + 1) != crow(t)) {
+                g0 = g1;
+                g1 = g2;
+                g2 = g3;
+                g3 = g4;
+            }
+            if (edge) {  // REPLICATE the blurred image beyond columns 0 / W-1
+                const uint32_t bl = byte_of(__builtin_amdgcn_readlane(B, max(lane0, 0) & 63), 0) * 0x01010101u;
+                const uint32_t br = byte_of(__builtin_amdgcn_readlane(B, min(laneW, 63) & 63), (W - 1 - xw0) & 3) * 0x01010101u;
+                B = (B & ~(rep_l | rep_r)) | (bl & rep_l) | (br & rep_r);
+            }
+            bring[k] = B;
+            if (SHD) rowpass4(B, k11, ra[k], rb[k]);
+            if (CLS) {
+                // ---- magnitude row t-1 from blurred rows t-2, t-1, t
+                uint32_t lo, hi;
+                sobel4(bring[(k + kRing - 2) % kRing], bring[(k + kRing - 1) % kRing], B, lo, hi);
+                const bool row_in = (unsigned)(t - 1) < (unsigned)H;
+                mlo[k] = row_in ? (lo & in_lo) : 0u;
+                mhi[k] = row_in ? (hi & in_hi) : 0u;
+                // ---- NMS of row t-2 from magnitude rows t-3, t-2, t-1
+                const int yn = t - 2;
+                if (yn >= ya && yn < yb) {
+                    const int km = (k + kRing - 1) % kRing, kb = k, ka = (k + kRing - 2) % kRing;
+                    // a Canny candidate (m > LOW) anywhere in the wave's row, else class 1
+                    const uint32_t ml = mlo[km], mh = mhi[km];
+                    const bool cand = (ml & 4095u) > 50u || ((ml >> 16) & 4095u) > 50u || (mh & 4095u) > 50u ||
+                                      ((mh >> 16) & 4095u) > 50u;
+                    uint32_t o = 0x01010101u;
+                    if (__ballot(cand)) o = nms4(mlo[ka], mhi[ka], ml, mh, mlo[kb], mhi[kb]);
+                    uint8_t *dst = cimg + (uint32_t)(yn * W + x);
+                    if (out_fast) {
+                        __builtin_nontemporal_store(o, (uint32_t *)dst);
+                    } else if (out_lane) {
+#pragma unroll
+                        for (int j = 0; j < 4; j++)
+                            if (x + j < W) dst[j] = (uint8_t)(o >> (8 * j));
+                    }
+                }
+            }
+            if (SHD) {
+                // ---- Gauss11 column pass of row t-5, mean, mask, masked sum / count
+                const int yg = t - 5;
+                if (yg >= ya && yg < yb) {
+                    const int kc = (k + kRing - 5) % kRing;
+                    const f32x2 w5 = {k11[5], k11[5]};
+                    f32x2 s01 = ra[kc] * w5, s23 = rb[kc] * w5;
+#pragma unroll
+                    for (int d = 1; d <= 5; d++) {
+                        const int kp = (kc + d) % kRing, kq = (kc + kRing - d) % kRing;
+                        const f32x2 wd = {k11[5 + d], k11[5 + d]};
+                        s01 = __builtin_elementwise_fma(ra[kp] + ra[kq], wd, s01);
+                        s23 = __builtin_elementwise_fma(rb[kp] + rb[kq], wd, s23);
+                    }
+                    const float sj[4] = {s01.x, s01.y, s23.x, s23.y};
+                    const uint32_t bw = bring[kc];
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        // mean = saturate(rint(s)) (s <= 255 + rounding, so rint(s) <= 255)
+                        const float mean = __builtin_rintf(sj[j]);
+                        const uint32_t b = byte_of(bw, j);
+                        const bool m = out_lane && x + j < W && (float)b + 2.0f <= mean;
+                        lsum += m ? b : 0u;
+                        lcnt += m ? 1u : 0u;
+                    }
+                }
+            }
+            }
+        }
+    }
+    if (SHD) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {  // <= 240 x 4096 x 255 < 2^32 per wave
+            lsum += __shfl_xor(lsum, off);
+            lcnt += __shfl_xor(lcnt, off);
+        }
+        if (lane == 0) wave_part[wid] = make_uint2(lsum, lcnt);
+    }
+}
+
+// per image: sum of its waves' (sum, count)
+__global__ __launch_bounds__(256) void k_stream_shadow_reduce(const uint2 *__restrict__ part, int per_img,
+                                                              unsigned long long *__restrict__ shadow_sum,
+                                                              unsigned long long *__restrict__ shadow_cnt) {
+    __shared__ unsigned long long rs[4], rc[4];
+    const int img = blockIdx.x, tid = threadIdx.x;
+    unsigned long long a = 0, b = 0;
+    for (int t = tid; t < per_img; t += 256) {
+        const uint2 v = part[(size_t)img * per_img + t];
+        a += v.x;
+        b += v.y;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        a += __shfl_xor(a, off);
+        b += __shfl_xor(b, off);
+    }
+    if ((tid & 63) == 0) {
+        rs[tid >> 6] = a;
+        rc[tid >> 6] = b;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        shadow_sum[img] = rs[0] + rs[1] + rs[2] + rs[3];
+        shadow_cnt[img] = rc[0] + rc[1] + rc[2] + rc[3];
+    }
+}
+
+void stream_geometry(int h, int w, int &strips, int &segs, int &seg_rows) {
+    strips = (w + kStripW - 1) / kStripW;
+    // ~180-row segments: 10 extra rows per segment (5 %), 48 waves per 1080p image
+    segs = std::max(1, (h + 179) / 180);
+    seg_rows = (h + segs - 1) / segs;
+    segs = (h + seg_rows - 1) / seg_rows;
+}
+
+}  // namespace
+
+size_t stencil_stream_parts(int n, int h, int w) {
+    int strips, segs, seg_rows;
+    stream_geometry(h, w, strips, segs, seg_rows);
+    return (size_t)n * strips * segs;
+}
+
+hipError_t launch_stencil_stream(const uint8_t *bgr, int n, int h, int w, uint8_t *cls,
+                                 unsigned long long *shadow_sum, unsigned long long *shadow_cnt, uint2 *wave_part,
+                                 const StencilParams &p, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    int strips, segs, seg_rows;
+    stream_geometry(h, w, strips, segs, seg_rows);
+    const long long waves = (long long)n * strips * segs;
+    const int blocks = (int)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
+    const int vec = ((((uintptr_t)bgr | (uintptr_t)cls) & 3) == 0 && (w & 3) == 0) ? 1 : 0;
+    const bool shd = shadow_sum != nullptr;
+    if (cls && shd)
+        hipLaunchKernelGGL((k_stencil_stream<true, true>), dim3(blocks), dim3(64 * kWavesPerBlock), 0, s, bgr, h, w,
+                           strips, segs, seg_rows, (int)waves, vec, cls, wave_part, p);
+    else if (cls)
+        hipLaunchKernelGGL((k_stencil_stream<true, false>), dim3(blocks), dim3(64 * kWavesPerBlock), 0, s, bgr, h, w,
+                           strips, segs, seg_rows, (int)waves, vec, cls, wave_part, p);
+    else if (shd)
+        hipLaunchKernelGGL((k_stencil_stream<false, true>), dim3(blocks), dim3(64 * kWavesPerBlock), 0, s, bgr, h, w,
+                           strips, segs, seg_rows, (int)waves, vec, cls, wave_part, p);
+    if (shd)
+        hipLaunchKernelGGL(k_stream_shadow_reduce, dim3(n), dim3(256), 0, s, wave_part, strips * segs, shadow_sum,
+                           shadow_cnt);
+    return hipGetLastError();
+}
+
+}  // namespace llfe

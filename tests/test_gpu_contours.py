@@ -172,3 +172,23 @@ def test_batch_gpu_contour_mode_capacity_regrowth(backend, orc):
         backend.set_contour_mode(prev)
     assert r.shapes == orc.analyze_shapes(x[0])["shapes"]
     assert len(r.shapes) > 320
+
+
+def test_unsupported_gpu_contour_chunk_falls_back_to_host(orc, monkeypatch):
+    """A chunk the GPU tracer flags as unsupported (kCtBadTrace / kCtTooWide /
+    kCtDpOverflow) is traced on the host pool instead of failing the batch
+    (llfe_api.cpp gpu_shapes_of_chunk); LLFE_CT_FORCE_HOST_FALLBACK=1 takes that path."""
+    from low_level_feature_extraction_amd import synth
+    from low_level_feature_extraction_amd.backend import Backend
+
+    monkeypatch.setenv("LLFE_CT_FORCE_HOST_FALLBACK", "1")
+    be = Backend(0)
+    try:
+        be.set_contour_mode("gpu")
+        x = np.stack([synth.synth_numpy(i, 200, 300, seed=71) for i in range(3)])
+        res = be.process(x, ("shapes", "shadows"), seed=1)
+        for i in range(3):
+            assert res[i].shapes == orc.analyze_shapes(x[i])["shapes"]
+            assert (res[i].shadow_sum, res[i].shadow_count) == orc.shadow_stats(x[i])
+    finally:
+        be.close()
