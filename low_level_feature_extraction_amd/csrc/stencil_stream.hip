@@ -138,7 +138,7 @@ __device__ __forceinline__ uint32_t blur4(uint32_t g0, uint32_t g1, uint32_t g2,
 // Sobel (3x3, on REPLICATE'd blurred rows b0 above, b1, b2 below) -> |dx|+|dy| and the
 // Canny NMS direction class (0 horizontal, 1 vertical, 2 / 3 diagonals) as
 // m | dir << 12 in two u16x2 dwords (cols c0 c1 | c2 c3)
-__device__ __forceinline__ void sobel4(uint32_t b0, uint32_t b1, uint32_t b2, uint32_t &mlo, uint32_t &mhi) {
+__device__ __forceinline__ bool sobel4(uint32_t b0, uint32_t b1, uint32_t b2, uint32_t &mlo, uint32_t &mhi) {
     const u16x2 two = {2, 2};
     const u16x2 vs_lo = U(lo2(b0)) + U(lo2(b2)) + U(lo2(b1)) * two;  // [1 2 1] vertical
     const u16x2 vs_hi = U(hi2(b0)) + U(hi2(b2)) + U(hi2(b1)) * two;
@@ -161,7 +161,8 @@ __device__ __forceinline__ void sobel4(uint32_t b0, uint32_t b1, uint32_t b2, ui
     // branches, only when some lane of the wave has such a pixel
     constexpr int LOW = 50, TG22 = 13573;
     const bool need = (int)m_lo.x > LOW || (int)m_lo.y > LOW || (int)m_hi.x > LOW || (int)m_hi.y > LOW;
-    if (__ballot(need)) {
+    const bool wave_need = __ballot(need) != 0;
+    if (wave_need) {
         const int gxs[4] = {gx_lo.x, gx_lo.y, gx_hi.x, gx_hi.y};
         const int gys[4] = {gy_lo.x, gy_lo.y, gy_hi.x, gy_hi.y};
         const int axs[4] = {ax_lo.x, ax_lo.y, ax_hi.x, ax_hi.y};
@@ -181,6 +182,7 @@ __device__ __forceinline__ void sobel4(uint32_t b0, uint32_t b1, uint32_t b2, ui
     }
     mlo = lo;
     mhi = hi;
+    return wave_need;  // some pixel of the wave's row has m > LOW (a Canny candidate)
 }
 
 // Canny NMS + double threshold of the lane's 4 pixels of the middle magnitude row;
@@ -248,7 +250,7 @@ __device__ __forceinline__ void rowpass4(uint32_t B, const float *__restrict__ k
 }
 
 template <bool CLS, bool SHD>
-__global__ __launch_bounds__(64 * kWavesPerBlock) void k_stencil_stream(
+__global__ __launch_bounds__(64 * kWavesPerBlock, 4) void k_stencil_stream(
     const uint8_t *__restrict__ bgr, int H, int W, int strips, int segs, int seg_rows, int total_waves, int vec,
     uint8_t *__restrict__ cls, uint2 *__restrict__ wave_part, StencilParams prm) {
     const int lane = threadIdx.x & 63;
@@ -307,12 +309,13 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void k_stencil_stream(
     Raw q1 = load_px(img, loadrow(t0 + 1), W, x, fast, coff);
 
     uint32_t bring[kRing];
-    uint32_t mlo[kRing], mhi[kRing];
+    // magnitude rows t-3 (a), t-2 (m) and whether row m has a candidate in this wave
+    uint32_t a_lo = 0, a_hi = 0, m_lo = 0, m_hi = 0;
+    bool m_cand = false;
     f32x2 ra[kRing], rb[kRing];
 #pragma unroll
     for (int k = 0; k < kRing; k++) {
         bring[k] = 0;
-        mlo[k] = mhi[k] = 0;
         ra[k] = rb[k] = f32x2{0.0f, 0.0f};
     }
     uint32_t lsum = 0, lcnt = 0;
@@ -344,20 +347,15 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void k_stencil_stream(
             if (CLS) {
                 // ---- magnitude row t-1 from blurred rows t-2, t-1, t
                 uint32_t lo, hi;
-                sobel4(bring[(k + kRing - 2) % kRing], bring[(k + kRing - 1) % kRing], B, lo, hi);
+                const bool cand = sobel4(bring[(k + kRing - 2) % kRing], bring[(k + kRing - 1) % kRing], B, lo, hi);
                 const bool row_in = (unsigned)(t - 1) < (unsigned)H;
-                mlo[k] = row_in ? (lo & in_lo) : 0u;
-                mhi[k] = row_in ? (hi & in_hi) : 0u;
-                // ---- NMS of row t-2 from magnitude rows t-3, t-2, t-1
+                const uint32_t b_lo = row_in ? (lo & in_lo) : 0u, b_hi = row_in ? (hi & in_hi) : 0u;
+                // ---- NMS of row t-2 from magnitude rows t-3, t-2, t-1 (class 1 for the
+                // whole row when no pixel of the wave's row is a candidate)
                 const int yn = t - 2;
                 if (yn >= ya && yn < yb) {
-                    const int km = (k + kRing - 1) % kRing, kb = k, ka = (k + kRing - 2) % kRing;
-                    // a Canny candidate (m > LOW) anywhere in the wave's row, else class 1
-                    const uint32_t ml = mlo[km], mh = mhi[km];
-                    const bool cand = (ml & 4095u) > 50u || ((ml >> 16) & 4095u) > 50u || (mh & 4095u) > 50u ||
-                                      ((mh >> 16) & 4095u) > 50u;
                     uint32_t o = 0x01010101u;
-                    if (__ballot(cand)) o = nms4(mlo[ka], mhi[ka], ml, mh, mlo[kb], mhi[kb]);
+                    if (m_cand) o = nms4(a_lo, a_hi, m_lo, m_hi, b_lo, b_hi);
                     uint8_t *dst = cimg + (uint32_t)(yn * W + x);
                     if (out_fast) {
                         __builtin_nontemporal_store(o, (uint32_t *)dst);
@@ -367,6 +365,11 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void k_stencil_stream(
                             if (x + j < W) dst[j] = (uint8_t)(o >> (8 * j));
                     }
                 }
+                a_lo = m_lo;
+                a_hi = m_hi;
+                m_lo = b_lo;
+                m_hi = b_hi;
+                m_cand = cand && row_in;
             }
             if (SHD) {
                 // ---- Gauss11 column pass of row t-5, mean, mask, masked sum / count
@@ -438,8 +441,8 @@ __global__ __launch_bounds__(256) void k_stream_shadow_reduce(const uint2 *__res
 
 void stream_geometry(int h, int w, int &strips, int &segs, int &seg_rows) {
     strips = (w + kStripW - 1) / kStripW;
-    // ~180-row segments: 10 extra rows per segment (5 %), 48 waves per 1080p image
-    segs = std::max(1, (h + 179) / 180);
+    // ~270-row segments: 10 extra rows per segment (3.7 %), 32 waves per 1080p image
+    segs = std::max(1, (h + 269) / 270);
     seg_rows = (h + segs - 1) / segs;
     segs = (h + seg_rows - 1) / seg_rows;
 }
