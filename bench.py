@@ -43,8 +43,9 @@ def _load_traffic():
         return {}, {}
 
 
-# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 4 cycles each
-VALU_SLOTS_PER_S = 256 * 4 / 4 * 2.4e9
+# VALU issue peak: 256 CUs x 4 SIMD-32 units, one wave64 VALU instruction per 2 cycles
+# each at 2.4 GHz (MI355X_MICROARCH.md "Wave scheduling"; 4 cycles is one wave alone)
+VALU_SLOTS_PER_S = 256 * 4 / 2 * 2.4e9
 TRAFFIC, VALU_INSTS = _load_traffic()
 
 
@@ -65,7 +66,23 @@ def _cpu_worker(args):
     return time.perf_counter() - t, int(nu)
 
 
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+
+    return platform.processor() or "unknown"
+
+
 def cpu_baseline(n_images, h, w, workers):
+    """a process pool of single-threaded workers, one image per task,
+    N = the cores this process may use (affinity / cgroup quota: on the GPU box
+    os.cpu_count() reports the whole machine, of which one GPU's share is a slice)."""
     import multiprocessing as mp
 
     from oracle import oracle as O
@@ -77,13 +94,16 @@ def cpu_baseline(n_images, h, w, workers):
         res = pool.map(_cpu_worker, [(i, h, w) for i in range(n_images)], chunksize=1)
     wall = time.perf_counter() - t0
     return {
-        "value": n_images / wall,
+        "value": round(n_images / wall, 3),
         "unit": "images/s",
         "cores": workers,
         "kind": "port",
+        "cpu_model": cpu_model(),
+        "os_cpu_count": os.cpu_count(),
         "sample": f"{n_images} synthetic {w}x{h} images ({(n_images + 1) // 2} ui / {n_images // 2} photo), full "
                   f"colors+shapes+shadows via the C oracle (oracle/llfe_oracle.c), {workers} single-threaded worker "
-                  f"processes, {wall:.1f}s wall; mean per-image CPU time {sum(r[0] for r in res) / len(res):.2f}s",
+                  f"processes (one per usable core), {wall:.1f}s wall; mean per-image CPU time "
+                  f"{sum(r[0] for r in res) / len(res):.2f}s",
     }
 
 
@@ -98,6 +118,35 @@ def _encode_png(args):
     b = io.BytesIO()
     Image.fromarray(synth.synth_numpy(i, h, w, seed=seed)[:, :, ::-1]).save(b, "PNG")
     return b.getvalue()
+
+
+def e2e_host(be, imgs_dev, feats, steps, seed, index_base):
+    """End-to-end from decoded host arrays: the batch sits in pinned host
+    memory and every step pays its H2D inside libllfe (llfe_submit_batch copies host
+    inputs into the workspace on its own stream); two batches in flight, so batch k+1's
+    H2D overlaps batch k's kernels.  Reported beside `value`, never as it."""
+    import torch
+
+    host = [torch.empty(imgs_dev.shape, dtype=torch.uint8).pin_memory() for _ in range(2)]
+    for hb in host:
+        hb.copy_(imgs_dev.cpu())
+    arrs = [hb.numpy() for hb in host]
+    be.process(arrs[0][:2], feats, seed=seed)  # warm the host-input path
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    pending = []
+    for k in range(steps):
+        pending.append(be.submit(arrs[k % 2], feats, seed=seed + k, index_base=index_base))
+        if len(pending) == 2:
+            be.collect(pending.pop(0))
+    while pending:
+        be.collect(pending.pop(0))
+    dt = time.perf_counter() - t0
+    n, h, w = imgs_dev.shape[0], imgs_dev.shape[1], imgs_dev.shape[2]
+    gb = n * h * w * 3 * steps / 1e9
+    return {"value": round(n * steps / dt, 2), "unit": "images/s", "h2d_gbs": round(gb / dt, 2),
+            "sample": f"{steps} x {n} decoded {w}x{h} BGR arrays in pinned host memory (two alternating buffers), "
+                      f"H2D + full GPU path per batch, two batches in flight (llfe_submit_batch / llfe_collect_batch)"}
 
 
 def e2e_png(be, B, H, W, feats, steps, distinct, seed):
@@ -133,6 +182,19 @@ def e2e_png(be, B, H, W, feats, steps, distinct, seed):
                       f"then the full GPU path incl. H2D"}
 
 
+def _config_name(B, H, W, feats, pre):
+    full = set(feats) == {"colors", "shapes", "shadows"}
+    if (H, W) == (1080, 1920) and full and pre == "auto":
+        return "BASELINE configs[3]: 4096 x 1080p over 8 GPUs = 512 per GPU"
+    if (H, W) == (2160, 3840) and full and pre == "high_quality":
+        return "BASELINE configs[4]: 1024 x 4K high_quality over 8 GPUs = 128 per GPU"
+    if (H, W) == (1080, 1920) and set(feats) == {"colors"}:
+        return "BASELINE configs[1]: 256 x 1080p colours"
+    if (H, W) == (1080, 1920) and set(feats) == {"colors", "shapes"}:
+        return "BASELINE configs[2]: 256 x 1080p colours + shapes"
+    return "custom"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -143,8 +205,12 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--features", default="colors,shapes,shadows")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
-    ap.add_argument("--cpu-images", type=int, default=16)
-    ap.add_argument("--cpu-workers", type=int, default=16)
+    ap.add_argument("--cpu-images", type=int, default=0, help="0: two images per worker")
+    ap.add_argument("--cpu-workers", type=int, default=0, help="0: the usable cores (affinity / cgroup)")
+    ap.add_argument("--preprocessing", default="auto", choices=["none", "auto", "high_quality", "performance"],
+                    help="validate_and_preprocess_image mode the workload is quoted under (the bench checks that "
+                         "it does not resize this size: BASELINE configs [3] auto at 1080p, [4] high_quality at 4K)")
+    ap.add_argument("--e2e-host-steps", type=int, default=3, help="0 disables the decoded-host-array line")
     ap.add_argument("--seed", type=int, default=2025)
     ap.add_argument("--e2e-png-steps", type=int, default=2, help="0 disables the PNG end-to-end line")
     ap.add_argument("--contours", choices=["auto", "host", "gpu"], default="auto",
@@ -177,6 +243,10 @@ def main():
         be.set_contour_mode(args.contours)
     feats = tuple(f for f in args.features.split(",") if f)
     B, H, W = args.batch, args.height, args.width
+    from low_level_feature_extraction_amd.backend import preprocess_size
+
+    if preprocess_size(W, H, args.preprocessing) is not None:
+        raise SystemExit(f"preprocessing={args.preprocessing!r} would resize {W}x{H}; bench the resized size instead")
     base, _ = shard.shard_bounds(B * world, rank, world)  # weak scaling: B images per rank
     imgs = synth.synth_batch(B, H, W, seed=args.seed, device=f"cuda:{local}", index_base=base)
     torch.cuda.synchronize()
@@ -236,10 +306,8 @@ def main():
     be.set_concurrency(True)
     be.set_profiling(False)
 
-    if rank != 0:
-        if dist is not None:
-            dist.destroy_process_group()
-        return
+    # (the e2e lines run on every rank before rank 0 reports: each rank pays its own
+    # host-side work, as a serving node would)
 
     total_images = B * world * args.steps
     def roof(name, src=None):
@@ -279,12 +347,35 @@ def main():
 
     cpu = None
     if args.cpu_baseline == "auto" and world == 1:
-        workers = max(1, min(args.cpu_workers, os.cpu_count() or 1, args.cpu_images))
-        cpu = cpu_baseline(args.cpu_images, H, W, workers)
+        from low_level_feature_extraction_amd.decode import usable_cores
 
+        workers = args.cpu_workers or usable_cores()
+        cpu = cpu_baseline(args.cpu_images or 2 * workers, H, W, workers)
+
+    def all_ranks(line):
+        """Whole-job rate of an e2e line every rank ran at once: images of all ranks over
+        the slowest rank's time."""
+        if line is None or world == 1:
+            return line
+        t = B * (args.e2e_host_steps if "h2d_gbs" in line else args.e2e_png_steps) / line["value"]
+        line = dict(line)
+        line["value"] = round(B * world * (args.e2e_host_steps if "h2d_gbs" in line else args.e2e_png_steps) /
+                              shard.max_over_ranks(t, device=f"cuda:{local}"), 2)
+        line["per_rank"] = True
+        return line
+
+    barrier()
+    e2e_h = None
+    if args.e2e_host_steps > 0:
+        e2e_h = all_ranks(e2e_host(be, imgs, feats, args.e2e_host_steps, args.seed, base))
+    barrier()
     e2e = None
-    if args.e2e_png_steps > 0 and world == 1:
-        e2e = e2e_png(be, B, H, W, feats, args.e2e_png_steps, 8, args.seed)
+    if args.e2e_png_steps > 0:  # every rank decodes its own shard with its core share
+        e2e = all_ranks(e2e_png(be, B, H, W, feats, args.e2e_png_steps, 8, args.seed))
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
 
     out = {
         "metric": METRIC,
@@ -302,8 +393,10 @@ def main():
         "dtype": "u8",
         "data": "synthetic",
         "config": {
-            "workload": f"{B} x {W}x{H} BGR images per GPU per step, features={list(feats)}, preprocessing='auto' "
-                        f"(no resize below 2000 px), 50% ui / 50% photo synthetic mix (BASELINE configs[3])",
+            "workload": f"{B} x {W}x{H} BGR images per GPU per step, features={list(feats)}, "
+                        f"preprocessing={args.preprocessing!r} (no resize at this size), 50% ui / 50% photo "
+                        f"synthetic mix ({_config_name(B, H, W, feats, args.preprocessing)})",
+            "preprocessing": args.preprocessing,
             "global_batch": B * world,
             "batch_per_gpu": B,
             "height": H,
@@ -318,6 +411,7 @@ def main():
         "kernels": kernels,
         "shapes_per_image": round(n_shapes / (B * args.steps), 2),
         "cpu_baseline": cpu,
+        "e2e_host": e2e_h,
         "e2e_png": e2e,
     }
     print(json.dumps(out))

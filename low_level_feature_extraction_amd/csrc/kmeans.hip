@@ -1132,11 +1132,7 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
                 // cubes straddling a boundary: their colours (enumerated from the
                 // occupancy mask, no key loads) packed densely into the lanes and
                 // labelled 64 at a time
-#ifdef LLFE_EXP_NO_BOUNDARY
-                unsigned long long fm = 0;
-#else
                 unsigned long long fm = __ballot(valid && !pass);
-#endif
                 // per lane: the origin key of its cube (read back per failing cube with one
                 // readlane instead of rebuilding it in scalar code)
                 const uint32_t okey = cube_origin_key(e.id);

@@ -9,6 +9,7 @@
 //   colour bitmap -> compaction -> k-means (10 attempts / image) -> D2H 64 B / image
 //   host thread pool: external contours + shape geometry from the packed masks
 #include <dlfcn.h>
+#include <sched.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -327,13 +328,31 @@ int chunk_for(int explicit_chunk, int h, int w) {
     return (int)std::max(1.0, std::min(n, (double)kMaxKmeansBatch));
 }
 
-// host cores per GPU process: the node's cores shared by the LOCAL_WORLD_SIZE ranks
-// torchrun starts on it
+// CPUs this process may run on: the affinity mask (sched_getaffinity), capped by a
+// cgroup v2 cpu.max quota -- std::thread::hardware_concurrency() counts the whole node
+int usable_cpus() {
+    int n = 0;
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof set, &set) == 0) n = CPU_COUNT(&set);
+    if (n <= 0) n = (int)std::max(1u, std::thread::hardware_concurrency());
+    if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char quota[64] = {0};
+        long long period = 0;
+        if (fscanf(f, "%63s %lld", quota, &period) == 2 && strcmp(quota, "max") != 0 && period > 0) {
+            const long long q = atoll(quota) / period;
+            if (q >= 1 && q < n) n = (int)q;
+        }
+        fclose(f);
+    }
+    return std::max(1, n);
+}
+
+// host cores per GPU process: the usable cores shared by the LOCAL_WORLD_SIZE ranks
+// torchrun starts on the node
 int cores_per_process() {
-    unsigned hc = std::thread::hardware_concurrency();
     int local = 1;
     if (const char *lw = getenv("LOCAL_WORLD_SIZE"); lw && atoi(lw) > 0) local = atoi(lw);
-    return std::max(1, (int)(hc ? hc : 4u) / local);
+    return std::max(1, usable_cpus() / local);
 }
 
 int default_threads() {
