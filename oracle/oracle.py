@@ -70,6 +70,12 @@ def _chk_bgr(bgr: np.ndarray) -> np.ndarray:
 
 
 # --------------------------------------------------------------------------- stencils
+def set_fma(on: bool):
+    """Oracle arithmetic mode (parity-risk probe only): True = FMA (AVX2 OpenCV build,
+    the default and what the device reproduces), False = separate mul + add (SSE2 build)."""
+    lib().orc_set_fma(1 if on else 0)
+
+
 def bgr2gray(bgr):
     bgr = _chk_bgr(bgr)
     h, w = bgr.shape[:2]
