@@ -121,6 +121,10 @@ int llfe_abi_version(void);
  * and `stream` handles passed in must come from this same runtime: a process that
  * also uses PyTorch-ROCm loads libllfe after torch, so both share torch's runtime. */
 const char *llfe_hip_runtime(void);
+/* host threads a new ctx gives its contour pool: the process's share of the usable CPUs
+ * (affinity mask and cgroup quota) / LOCAL_WORLD_SIZE, at most 16; LLFE_HOST_THREADS
+ * overrides.  Host only. */
+int llfe_default_host_threads(void);
 /* enable (1) / disable (0) event timing; enabling resets the statistics */
 int llfe_set_profiling(llfe_ctx *ctx, int enable);
 /* llfe_process_batch runs the colour path on a second stream beside shapes / shadows

@@ -94,6 +94,7 @@ SIGNATURES = {
     "llfe_last_error": (C.c_char_p, [_vp]),
     "llfe_abi_version": (C.c_int, []),
     "llfe_hip_runtime": (C.c_char_p, []),
+    "llfe_default_host_threads": (C.c_int, []),
     "llfe_set_profiling": (C.c_int, [_vp, C.c_int]),
     "llfe_set_concurrency": (C.c_int, [_vp, C.c_int]),
     "llfe_set_contour_mode": (C.c_int, [_vp, C.c_int]),

@@ -881,6 +881,8 @@ extern "C" {
 
 int llfe_abi_version(void) { return LLFE_ABI_VERSION; }
 
+int llfe_default_host_threads(void) { return default_threads(); }
+
 // path of the HIP runtime this library's HIP calls resolved to (dladdr of hipMalloc):
 // a process must hold exactly one, shared with whatever produced its device pointers
 // and stream handles (e.g. PyTorch-ROCm's torch/lib/libamdhip64.so)

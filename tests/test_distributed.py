@@ -1,6 +1,8 @@
 """N>1 path on CPU: world_size-2 gloo process groups exercising the sharding,
 timing reduction and result gather that bench.py and run_sharded use on RCCL."""
 import os
+
+import numpy as np
 import socket
 
 import pytest
@@ -79,3 +81,66 @@ def test_single_process_fallthrough():
 
     assert shard.run_sharded(5, lambda a, b: list(range(a, b))) == [0, 1, 2, 3, 4]
     assert shard.max_over_ranks(3.0) == 3.0
+
+
+def _cpu_records(a, b):
+    """Per-image ImageFeatures records of the images [a, b) computed on the host only:
+    shapes through libllfe's host contour path (llfe_shapes_from_mask, the code the
+    batch runs on the host pool) over the oracle's dilated Canny mask, shadows from the
+    oracle's statistics -- what a rank contributes, minus the GPU stages."""
+    from low_level_feature_extraction_amd import backend, synth
+    from low_level_feature_extraction_amd.backend import ImageFeatures
+    from oracle import oracle as O
+
+    out = []
+    for i in range(a, b):
+        img = synth.synth_numpy(i, 96, 160, seed=31)
+        s, c = O.shadow_stats(img)
+        shapes = backend.shapes_from_mask(O.shape_mask(img))
+        out.append(ImageFeatures(np.zeros((0, 3), np.uint8), np.zeros(0, np.int64), 0, 0.0, s, c, shapes, 0, 160, 96))
+    return out
+
+
+def _worker_records(rank, world, port, n_total, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LOCAL_WORLD_SIZE=str(world))
+    import torch.distributed as dist
+
+    from low_level_feature_extraction_amd import _lib, decode, shard
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        got = shard.run_sharded(n_total, _cpu_records, gather_to=0)
+        # per-rank host thread budgets: the rank's share of the usable cores
+        threads = (_lib.lib().llfe_default_host_threads(), decode.default_decode_threads(), decode.usable_cores())
+        q.put((rank, got, threads))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_gathers_real_records():
+    import numpy as np  # noqa: F401
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    n_total = 6
+    procs = [ctx.Process(target=_worker_records, args=(r, 2, port, n_total, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(2):
+        rank, got, threads = q.get(timeout=240)
+        out[rank] = (got, threads)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    got = out[0][0]
+    assert out[1][0] is None and len(got) == n_total
+    want = _cpu_records(0, n_total)
+    assert [r.shapes for r in got] == [r.shapes for r in want]
+    assert [(r.shadow_sum, r.shadow_count) for r in got] == [(r.shadow_sum, r.shadow_count) for r in want]
+    assert any(r.shapes for r in got)
+    for rank in (0, 1):
+        host, dec, usable = out[rank][1]
+        assert host == max(1, min(usable // 2, 16))
+        assert dec == max(1, min(usable // 2, 64))
