@@ -171,6 +171,7 @@ struct KmSmem {
     unsigned long long found_excl[3];
     int ci[3];
     int flag;
+    int next_chunk;                      // Lloyd: next 64-cube chunk to hand out
     unsigned long long fail_pts;  // keys read point by point in this Lloyd sweep
     // cube-based k-means++ (pp_cubes)
     unsigned long long psum[3][kParts];  // per trial and red-quarter partition: sum of T_j
@@ -506,6 +507,7 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
         }
         // ---- trial sums T_j = sum min(D, d(., t_j)) per partition (kk == 0: sum d(., c0))
         if (tid < 3 * kParts) (&sm.psum[0][0])[tid] = 0;
+        if (tid == 0) sm.next_chunk = 0;
         __syncthreads();
         unsigned long long acc0 = 0, acc1 = 0, acc2 = 0, fails = 0;
         int Pcur = -1;
@@ -562,12 +564,25 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
         }
         __syncthreads();
         const int *Mkk = sm.marg, *NA = sm.marg + kMaxK * kMaxK, *NB = sm.marg + kMaxK * kMaxK + 3 * kMaxK;
-        CubeRing ring;
-        ring.init(ctab, cb, cend, lane);
-        for (int base = cb; base < cend; base += 64) {
+        // waves take 64-cube chunks from a shared counter (ascending per wave, so the
+        // partition bookkeeping below still sees its partitions in order)
+        auto grab = [&]() {
+            int b = 0;
+            if (lane == 0) b = atomicAdd(&sm.next_chunk, 64);
+            return __builtin_amdgcn_readfirstlane(b);
+        };
+        int base = grab();
+        CubeEnt en;
+        en.mask = 0;
+        en.id = 0;
+        en.sums = 0;
+        if (base + lane < C) en = ctab[base + lane];
+        while (base < C) {
             const int cidx = base + lane;
-            const bool valid = cidx < cend;
-            const CubeEnt e = ring.next(ctab, cidx, cend);
+            const bool valid = cidx < C;
+            const CubeEnt e = en;
+            const int nb = grab();
+            if (nb + lane < C) en = ctab[nb + lane];
             const CubeGeo g = cube_geo(e);
             const int P = valid ? (int)((e.id >> 12) & 63u) : kParts;
             uint32_t v0 = 0, v1 = 0, v2 = 0;
@@ -685,6 +700,7 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
                 if (!rest) break;
                 Pseg = __shfl(P, (int)__builtin_ctzll(rest));
             }
+            base = nb;
         }
         if (Pcur >= 0) {
             flush_pk();
@@ -743,6 +759,10 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
 #ifndef LLFE_KM_MINW
 #define LLFE_KM_MINW 1
 #endif
+// kCubes: the cube-table path (the batch pipeline); !kCubes: plain sweeps over
+// caller-supplied keys (llfe_kmeans).  Separate instantiations keep the plain path's
+// register-heavy prefetch out of the hot kernel.
+template <bool kCubes>
 __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__restrict__ keys, long long key_stride,
                                                const long long *__restrict__ n_unique, int n_colors,
                                                unsigned long long seed, long long index_base,
@@ -775,6 +795,7 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
             o->t_sel = 0;
             o->ll_pts = 0;
             o->t_sw = 0;
+            o->drift_hist = 0;
             o->t_end = wall_clock64();
         }
         return;
@@ -789,7 +810,7 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
     uint32_t *ss = scratch + ((size_t)img * kAttempts + att) * (size_t)scratch_stride;
     // cube-pruned Lloyd sweeps (when the cube table was built): waves own contiguous
     // ranges of cubes
-    const bool use_cubes = cubes.cubes != nullptr;
+    constexpr bool use_cubes = kCubes;
     const int C = use_cubes ? cubes.n_cubes[img] : 0;
     const CubeEnt *ctab = use_cubes ? cubes.cubes + (size_t)img * cubes.cube_stride : nullptr;
     const int Cw = (C + KW - 1) / KW;
@@ -1030,9 +1051,12 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
     }
     __syncthreads();
 
+    if (tid == 0) sm.next_chunk = 0;
+    __syncthreads();
     int iter = 1;
     const double eps2 = 0.2 * 0.2;
     uint64_t t_sw = 0;  // (trace) time in the labelling sweeps
+    uint64_t drift_hist = 0;  // (trace)
     for (;;) {
         const uint64_t tsw0 = wall_clock64();
         const CentP c = pack_centres(load_centres(sm.c));
@@ -1082,12 +1106,27 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
                 }
                 tail += count;
             };
-            CubeRing ring;
-            ring.init(ctab, cb, cend, lane);
-            for (int base = cb; base < cend; base += 64) {
+            // Waves take 64-cube chunks from a shared counter (not fixed ranges): the
+            // boundary cubes cluster, and with fixed ranges the other waves idled at the
+            // iteration barrier behind the wave that drew the boundary.  The next chunk's
+            // index and entries are fetched one chunk ahead.
+            auto grab = [&]() {
+                int b = 0;
+                if (lane == 0) b = atomicAdd(&sm.next_chunk, 64);
+                return __builtin_amdgcn_readfirstlane(b);
+            };
+            int base = grab();
+            CubeEnt en;
+            en.mask = 0;
+            en.id = 0;
+            en.sums = 0;
+            if (base + lane < C) en = ctab[base + lane];
+            while (base < C) {
                 const int ci = base + lane;
-                const bool valid = ci < cend;
-                const CubeEnt e = ring.next(ctab, ci, cend);
+                const bool valid = ci < C;
+                const CubeEnt e = en;
+                const int nb = grab();
+                if (nb + lane < C) en = ctab[nb + lane];
                 bool pass = false;
                 int k = 0;
                 if (valid) {
@@ -1159,6 +1198,7 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
                     }
                     while (head - tail >= 64) label_stage(64);
                 }
+                base = nb;
             }
             if (head > tail) label_stage(head - tail);
             fails = (unsigned long long)head;
@@ -1324,6 +1364,14 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
                 max_shift = fmax(max_shift, dist);
             }
             sm.flag = (iter + 1 == 100 || max_shift <= eps2) ? 1 : 0;
+            sm.next_chunk = 0;
+            // (trace) iterations by their largest centre move, 8 u8 bins
+            // [0,.25) [.25,.5) [.5,1) [1,2) [2,4) [4,8) [8,16) [16,inf)
+            const double mv = sqrt(max_shift);
+            int bin = 0;
+            for (double t = 0.25; bin < 7 && mv >= t; t *= 2.0) bin++;
+            const unsigned long long sh = 8ull * (unsigned)bin;
+            if (((drift_hist >> sh) & 255ull) < 255ull) drift_hist += 1ull << sh;
         }
         iter++;
         __syncthreads();
@@ -1393,6 +1441,7 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
             o->ll_pts = ll_pts;
             o->t_sw = t_sw;
             o->n_cubes = (uint32_t)C;
+            o->drift_hist = drift_hist;
             o->t_end = wall_clock64();
             for (int k = 0; k < kMaxK; k++) {
                 for (int j = 0; j < 3; j++) o->centers[k][j] = k < K ? sm.c[k][j] : 0.f;
@@ -1458,7 +1507,11 @@ __global__ void k_kmeans_finalize(const uint32_t *__restrict__ keys, long long k
             }
         }
         const KmeansAttemptOut &b = att[(size_t)img * kAttempts + best];
-        for (int a = 0; a < kAttempts; a++) r.bytes += att[(size_t)img * kAttempts + a].bytes;
+        // algorithmic bytes: 4 U per fused multi-attempt pass over the
+        // keys x passes (K k-means++ passes + the Lloyd sweeps of the longest attempt)
+        int sweeps = 0;
+        for (int a = 0; a < kAttempts; a++) sweeps = max(sweeps, att[(size_t)img * kAttempts + a].iters - 1);
+        r.bytes = 4ull * (unsigned long long)N * (unsigned long long)(K + sweeps);
         r.k = K;
         r.compactness = bc;
         for (int k = 0; k < K; k++) {
@@ -1480,12 +1533,14 @@ hipError_t launch_kmeans(const uint32_t *keys, int64_t key_stride, const int64_t
     static bool attr_set = false;
     const size_t smem = sizeof(KmSmem);
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void *)k_kmeans, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        hipError_t e = hipFuncSetAttribute((const void *)k_kmeans<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        if (e != hipSuccess) return e;
+        e = hipFuncSetAttribute((const void *)k_kmeans<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
     hipLaunchKernelGGL(k_kmeans_order, dim3(1), dim3(OT), 0, s, (const long long *)n_unique, n, order);
-    hipLaunchKernelGGL(k_kmeans, dim3(n * kAttempts), dim3(KT), smem, s, keys, (long long)key_stride,
+    hipLaunchKernelGGL(cubes.cubes ? k_kmeans<true> : k_kmeans<false>, dim3(n * kAttempts), dim3(KT), smem, s, keys, (long long)key_stride,
                        (const long long *)n_unique, n_colors, (unsigned long long)seed, (long long)index_base, order,
                        scratch, (long long)scratch_stride, attempts, cubes);
     hipLaunchKernelGGL(k_kmeans_finalize, dim3((n + 255) / 256), dim3(256), 0, s, keys, (long long)key_stride,

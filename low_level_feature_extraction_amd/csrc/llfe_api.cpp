@@ -606,10 +606,10 @@ int kmeans_stage(llfe_ctx *ctx, Work &W, const uint32_t *keys, int64_t key_strid
             for (int i = 0; i < n; i++)
                 for (int a = 0; a < kAttempts; a++) {
                     const KmeansAttemptOut &o = att[(size_t)i * kAttempts + a];
-                    fprintf(f, "%d %d %lld %d %llu %llu %u %u %llu %llu %llu %u %u %d %llu %llu %llu\n", i, a, (long long)nu[i], o.iters,
+                    fprintf(f, "%d %d %lld %d %llu %llu %u %u %llu %llu %llu %u %u %d %llu %llu %llu 0 0 %llu\n", i, a, (long long)nu[i], o.iters,
                             (unsigned long long)o.t_start, (unsigned long long)o.t_end, o.hw_id, o.xcc_id,
                             (unsigned long long)o.t_pp, (unsigned long long)o.t_lloyd, (unsigned long long)o.bytes, o.pp_pts, o.n_cubes, o.pad, (unsigned long long)o.t_sel,
-                            (unsigned long long)o.ll_pts, (unsigned long long)o.t_sw);
+                            (unsigned long long)o.ll_pts, (unsigned long long)o.t_sw, (unsigned long long)o.drift_hist);
                 }
             fclose(f);
         }

@@ -136,6 +136,7 @@ struct KmeansAttemptOut {
     uint64_t t_sel;            // k-means++ time in the selection scans (ticks)
     uint64_t ll_pts;           // colours Lloyd labelled one by one (all sweeps)
     uint64_t t_sw;             // Lloyd time in the labelling sweeps (ticks)
+    uint64_t drift_hist;       // Lloyd iterations by largest centre move (8 x u8 bins)
 };
 
 struct KmeansImageOut {

@@ -25,6 +25,7 @@ def main():
     t_sel = a.T[14] / 100.0 if a.shape[1] >= 15 else z
     ll_pts = a.T[15] if a.shape[1] >= 16 else z
     t_sw = a.T[16] / 100.0 if a.shape[1] >= 17 else z
+    dh = a.T[19].astype(np.uint64) if a.shape[1] >= 20 else z.astype(np.uint64)
     ok = it > 1
     pp = (tpp - t0) / 100.0
     ll = (tll - tpp) / 100.0
@@ -40,6 +41,10 @@ def main():
             print(f"      cubes/U {np.mean(ncub[m] / U[m]):.3f}  k-means++ colours read one by one / U"
                   f" {np.mean(pp_pts[m] / U[m]):.3f} (undecided cubes) + {np.mean(pp_sel[m] / U[m]):.3f} (selection);"
                   f" selection time {t_sel[m].mean() / 1e3:.3f} ms; Lloyd sweeps {t_sw[m].mean() / 1e3:.3f} ms")
+        if dh[m].any():
+            bins = np.stack([((dh[m] >> np.uint64(8 * b)) & np.uint64(255)).astype(np.int64) for b in range(8)], 1)
+            print("      iterations by largest centre move [<.25 <.5 <1 <2 <4 <8 <16 >=16]:",
+                  np.round(bins.mean(0), 2).tolist(), f"; iters max {it[m].max()}")
     dur = (t1 - t0) / 100.0
     cu = xcc * 1000 + ((hw >> 13) & 7) * 100 + ((hw >> 12) & 1) * 16 + ((hw >> 8) & 15)
     busy = {}
