@@ -171,7 +171,7 @@ struct KmSmem {
     unsigned long long found_excl[3];
     int ci[3];
     int flag;
-    int next_chunk;                      // Lloyd: next 64-cube chunk to hand out
+    int next_chunk;                      // next 64-cube chunk to hand out (cube sweeps)
     unsigned long long fail_pts;  // keys read point by point in this Lloyd sweep
     // cube-based k-means++ (pp_cubes)
     unsigned long long psum[3][kParts];  // per trial and red-quarter partition: sum of T_j
@@ -564,14 +564,16 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
         }
         __syncthreads();
         const int *Mkk = sm.marg, *NA = sm.marg + kMaxK * kMaxK, *NB = sm.marg + kMaxK * kMaxK + 3 * kMaxK;
-        // waves take 64-cube chunks from a shared counter (ascending per wave, so the
-        // partition bookkeeping below still sees its partitions in order)
+        // waves take 64-cube chunks from a shared LDS counter, read two chunks ahead
+        // (ascending per wave, so the partition bookkeeping below still sees its
+        // partitions in order)
         auto grab = [&]() {
             int b = 0;
             if (lane == 0) b = atomicAdd(&sm.next_chunk, 64);
-            return __builtin_amdgcn_readfirstlane(b);
+            return b;
         };
-        int base = grab();
+        int base = __builtin_amdgcn_readfirstlane(grab());
+        int ahead = grab();
         CubeEnt en;
         en.mask = 0;
         en.id = 0;
@@ -581,8 +583,9 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
             const int cidx = base + lane;
             const bool valid = cidx < C;
             const CubeEnt e = en;
-            const int nb = grab();
+            const int nb = __builtin_amdgcn_readfirstlane(ahead);
             if (nb + lane < C) en = ctab[nb + lane];
+            if (nb < C) ahead = grab();
             const CubeGeo g = cube_geo(e);
             const int P = valid ? (int)((e.id >> 12) & 63u) : kParts;
             uint32_t v0 = 0, v1 = 0, v2 = 0;
@@ -624,7 +627,7 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
 #pragma unroll
                     for (int m = 0; m < kMaxK; m++) {
                         if (m >= kk) break;
-                        if (m != k) owned = owned && (Dc[m] - Dk - selk(Mkk + m * kMaxK) >= 0);
+                        if (m != k) owned = owned & (Dc[m] - Dk - selk(Mkk + m * kMaxK) >= 0);
                     }
                     // cube sums: P + n D_c(o) - 2 c.S_u, P = n |o|^2 + 2 o.S_u + S_u2
                     const int Pc = __mul24(g.n, __mul24(g.ox, g.ox) + __mul24(g.oy, g.oy) + __mul24(g.oz, g.oz)) +
@@ -639,7 +642,7 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
                         const int f = Dt - Dk;
                         const bool A = f - selk(NA + j * kMaxK) >= 0;  // t_j never strictly closer than c_k
                         const bool B = f + selk(NB + j * kMaxK) <= 0;  // t_j always at least as close
-                        dec = dec && (A || B);
+                        dec = dec & (A | B);
                         vv[j] = A ? ds
                                   : (uint32_t)(Pc + __mul24(g.n, Dt) -
                                                2 * (__mul24(tx[j], g.sx) + __mul24(ty[j], g.sy) + __mul24(tz[j], g.sz)));
@@ -1106,16 +1109,18 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
                 }
                 tail += count;
             };
-            // Waves take 64-cube chunks from a shared counter (not fixed ranges): the
+            // Waves take 64-cube chunks from a shared LDS counter, not fixed ranges: the
             // boundary cubes cluster, and with fixed ranges the other waves idled at the
-            // iteration barrier behind the wave that drew the boundary.  The next chunk's
-            // index and entries are fetched one chunk ahead.
+            // iteration barrier behind the wave that drew the boundary (measured: 94 ->
+            // 74 us per photo iteration; round-robin chunks 79).  The counter is read two
+            // chunks ahead and the entries one chunk ahead.
             auto grab = [&]() {
                 int b = 0;
                 if (lane == 0) b = atomicAdd(&sm.next_chunk, 64);
-                return __builtin_amdgcn_readfirstlane(b);
+                return b;  // (lane 0's; read with readfirstlane one chunk later)
             };
-            int base = grab();
+            int base = __builtin_amdgcn_readfirstlane(grab());
+            int ahead = grab();
             CubeEnt en;
             en.mask = 0;
             en.id = 0;
@@ -1125,8 +1130,9 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
                 const int ci = base + lane;
                 const bool valid = ci < C;
                 const CubeEnt e = en;
-                const int nb = grab();
+                const int nb = __builtin_amdgcn_readfirstlane(ahead);
                 if (nb + lane < C) en = ctab[nb + lane];
+                if (nb < C) ahead = grab();
                 bool pass = false;
                 int k = 0;
                 if (valid) {
@@ -1148,17 +1154,18 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
                     // T[k][j] at q.  T is symmetric and dv[k] = m1, so the test per pair
                     // (a, b) is |dv[a] - dv[b]| > T[a][b]: ten compares into lane masks,
                     // combined per k with scalar mask logic
+                    // (bitwise & | on the lane masks: no short-circuit branches)
                     const bool e0 = dv[0] == m1, e1 = dv[1] == m1, e2 = dv[2] == m1, e3 = dv[3] == m1;
-                    const bool is0 = e0, is1 = !e0 && e1, is2 = !e0 && !e1 && e2, is3 = !e0 && !e1 && !e2 && e3,
-                               is4 = !(e0 || e1 || e2 || e3);
+                    const bool is0 = e0, is1 = !e0 & e1, is2 = !e0 & !e1 & e2, is3 = !e0 & !e1 & !e2 & e3,
+                               is4 = !(e0 | e1 | e2 | e3);
                     const bool o01 = fabsf(dv[0] - dv[1]) > thr[0][1], o02 = fabsf(dv[0] - dv[2]) > thr[0][2],
                                o03 = fabsf(dv[0] - dv[3]) > thr[0][3], o04 = fabsf(dv[0] - dv[4]) > thr[0][4],
                                o12 = fabsf(dv[1] - dv[2]) > thr[1][2], o13 = fabsf(dv[1] - dv[3]) > thr[1][3],
                                o14 = fabsf(dv[1] - dv[4]) > thr[1][4], o23 = fabsf(dv[2] - dv[3]) > thr[2][3],
                                o24 = fabsf(dv[2] - dv[4]) > thr[2][4], o34 = fabsf(dv[3] - dv[4]) > thr[3][4];
-                    pass = (is0 && o01 && o02 && o03 && o04) || (is1 && o01 && o12 && o13 && o14) ||
-                           (is2 && o02 && o12 && o23 && o24) || (is3 && o03 && o13 && o23 && o34) ||
-                           (is4 && o04 && o14 && o24 && o34);
+                    pass = (is0 & o01 & o02 & o03 & o04) | (is1 & o01 & o12 & o13 & o14) |
+                           (is2 & o02 & o12 & o23 & o24) | (is3 & o03 & o13 & o23 & o34) |
+                           (is4 & o04 & o14 & o24 & o34);
                     k = is0 ? 0 : (is1 ? 1 : (is2 ? 2 : (is3 ? 3 : 4)));
                 }
                 if (pass) {
