@@ -131,6 +131,10 @@ __device__ __forceinline__ int label5p(uint32_t key, const CentP &c) {
 }
 
 constexpr int PF = 4;  // steps of 16-B key loads kept in flight per wave
+// k-means++ selection: 256-key steps per wave chunk of a partition (<= 4 x 256 x 256 keys,
+// + alignment) and steps whose loads are issued together
+constexpr int kSelSteps = ((4 * 256 * 256 + 3 + STEP - 1) / STEP + KW - 1) / KW + 1;
+constexpr int SEL_U = 4;
 #ifndef LLFE_KM_UNROLL
 #define LLFE_KM_UNROLL 4
 #endif
@@ -414,60 +418,122 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
                 }
             }
             __syncthreads();
-            // ---- the partition's sorted keys in KW wave chunks: chunk sums of D ...
+            // ---- the partition's sorted keys in KW wave chunks of whole 256-key steps
+            // (aligned to the key list, so every lane reads its 4 keys with one 16-byte
+            // load; keys outside the partition are masked): step sums of D into LDS and
+            // chunk sums.  The three trials' chunks are walked together, SEL_U steps per
+            // trip with their loads issued first -- these scans were chains of dependent
+            // scalar loads (~75 us per k-means++ round on a photo).
+            // Step sums alias the Lloyd accumulators (unused until Lloyd).
+            uint32_t(*stp)[KW][kSelSteps] = reinterpret_cast<uint32_t(*)[KW][kSelSteps]>(&sm.accA[0][0]);
+            uint32_t ca[3], cb2[3], cw0[3], cw1[3];  // partition [a, b), this wave's steps [w0, w1)
 #pragma unroll
             for (int j = 0; j < 3; j++) {
                 const int P = sm.pj[j];
-                if (P < 0) continue;
-                const uint32_t a = sm.pbase[P], b = sm.pbase[P + 1];
-                const uint32_t len = (b - a + KW - 1) / KW;
-                const uint32_t wa = min(b, a + (uint32_t)wid * len), wb = min(b, wa + len);
-                uint32_t ls = 0;
-                for (uint32_t s0 = wa; s0 < wb; s0 += STEP) {
-                    const uint32_t i0 = s0 + (uint32_t)lane * 4;
+                ca[j] = P >= 0 ? sm.pbase[P] : 0u;
+                cb2[j] = P >= 0 ? sm.pbase[P + 1] : 0u;
+                const uint32_t A = ca[j] & ~3u;
+                const uint32_t nst = (cb2[j] - A + STEP - 1) / STEP;   // steps over [A, b)
+                const uint32_t per = (nst + KW - 1) / KW;               // steps per wave (<= kSelSteps)
+                cw0[j] = A + min(nst, (uint32_t)wid * per) * STEP;
+                cw1[j] = A + min(nst, (uint32_t)(wid + 1) * per) * STEP;
+            }
+            {
+                uint32_t csum_lo[3] = {0u, 0u, 0u};  // per-lane partial chunk sums
+                unsigned long long cnt = 0;
 #pragma unroll
-                    for (int jj = 0; jj < 4; jj++)
-                        if (i0 + jj < wb) {
-                            const uint32_t k = pts[i0 + jj];
-                            ls += (uint32_t)dmin_chosen(unpack_r(k), unpack_g(k), unpack_b(k), ch, kk);
+                for (int j = 0; j < 3; j++) {
+                    uint32_t ls = 0;
+                    for (uint32_t s0 = cw0[j]; s0 < cw1[j]; s0 += SEL_U * STEP) {
+                        uint4 kv[SEL_U];
+#pragma unroll
+                        for (int u = 0; u < SEL_U; u++) {
+                            const uint32_t i0 = s0 + (uint32_t)u * STEP + (uint32_t)lane * 4;
+                            kv[u] = make_uint4(0u, 0u, 0u, 0u);
+                            if (i0 < cw1[j] && i0 < cb2[j] && i0 + 4 > ca[j]) kv[u] = *(const uint4 *)(pts + i0);
                         }
+#pragma unroll
+                        for (int u = 0; u < SEL_U; u++) {
+                            const uint32_t st = s0 + (uint32_t)u * STEP;
+                            if (st >= cw1[j]) break;  // (uniform)
+                            const uint32_t i0 = st + (uint32_t)lane * 4;
+                            const uint32_t kq[4] = {kv[u].x, kv[u].y, kv[u].z, kv[u].w};
+                            uint32_t sd = 0;
+#pragma unroll
+                            for (int jj = 0; jj < 4; jj++) {
+                                const uint32_t i = i0 + (uint32_t)jj;
+                                const bool in = i >= ca[j] && i < cb2[j];
+                                const int d = dmin_chosen(unpack_r(kq[jj]), unpack_g(kq[jj]), unpack_b(kq[jj]), ch, kk);
+                                sd += in ? (uint32_t)d : 0u;
+                            }
+                            ls += sd;
+                            const uint32_t ssum = wave_sum(sd);  // <= 256 x 195075 < 2^32
+                            if (lane == 0) stp[j][wid][(st - cw0[j]) / STEP] = ssum;
+                        }
+                    }
+                    csum_lo[j] = ls;
+                    cnt += cw1[j] - cw0[j];
                 }
-                const unsigned long long ws = wave_sum((unsigned long long)ls);
-                if (lane == 0) {
-                    sm.wchunk[j][wid] = ws;
-                    atomicAdd(&sm.sel_pts, (unsigned long long)(wb - wa));
+#pragma unroll
+                for (int j = 0; j < 3; j++) {
+                    const unsigned long long ws = wave_sum((unsigned long long)csum_lo[j]);
+                    if (lane == 0) sm.wchunk[j][wid] = ws;
                 }
+                if (lane == 0) atomicAdd(&sm.sel_pts, cnt);
             }
             __syncthreads();
-            // ... then waves 0..2 find the chunk holding p_j and the first crossing in it
+            // ... then wave j < 3 finds the chunk, the step (from the step sums) and the
+            // first crossing in that one step
             if (wid < 3) {
                 const int j = wid;
                 const double pj = j == 0 ? p[0] : (j == 1 ? p[1] : p[2]);
                 const int P = sm.pj[j];
                 int ci = P == -2 ? 0 : N - 1;
                 if (P >= 0) {
-                    const uint32_t a = sm.pbase[P], b = sm.pbase[P + 1];
-                    const uint32_t len = (b - a + KW - 1) / KW;
+                    const uint32_t a = sm.pbase[P], b = sm.pbase[P + 1];  // (not ca[j]: no dynamic private indexing)
+                    const uint32_t A = a & ~3u;
+                    const uint32_t nst = (b - A + STEP - 1) / STEP, per = (nst + KW - 1) / KW;
                     unsigned long long e = sm.pex[j];
                     int w = 0;
                     for (; w < KW - 1; w++) {
                         if ((double)(e + sm.wchunk[j][w]) >= pj) break;
                         e += sm.wchunk[j][w];
                     }
-                    const uint32_t wa = min(b, a + (uint32_t)w * len), wb = min(b, wa + len);
+                    const uint32_t w0 = A + min(nst, (uint32_t)w * per) * STEP, w1 = A + min(nst, (uint32_t)(w + 1) * per) * STEP;
+                    const int ns = (int)((w1 - w0) / STEP);
+                    // the step: inclusive prefix of the chunk's step sums, 64 at a time
+                    int sidx = ns - 1;
+                    for (int s_base = 0; s_base < ns; s_base += 64) {
+                        const int si = s_base + lane;
+                        const unsigned long long v = si < ns ? (unsigned long long)stp[j][w][si] : 0ull;
+                        unsigned long long x = v;
+#pragma unroll
+                        for (int off = 1; off < 64; off <<= 1) {
+                            const unsigned long long y = __shfl_up(x, off);
+                            if (lane >= off) x += y;
+                        }
+                        const unsigned long long bal = __ballot(si < ns && (double)(e + x) >= pj);
+                        if (bal) {
+                            const int f = (int)__builtin_ctzll(bal);
+                            sidx = s_base + f;
+                            e += __shfl(x - v, f);
+                            break;
+                        }
+                        e += __shfl(x, 63);
+                    }
                     int found = -1;
-                    unsigned long long scanned = 0;
-                    for (uint32_t s0 = wa; s0 < wb && found < 0; s0 += STEP) {
-                        scanned += min((uint32_t)STEP, wb - s0);
+                    if (ns > 0) {
+                        const uint32_t s0 = w0 + (uint32_t)sidx * STEP;
                         const uint32_t i0 = s0 + (uint32_t)lane * 4;
+                        uint4 kv = make_uint4(0u, 0u, 0u, 0u);
+                        if (i0 < b && i0 + 4 > a) kv = *(const uint4 *)(pts + i0);
+                        const uint32_t kq[4] = {kv.x, kv.y, kv.z, kv.w};
                         uint32_t dv[4], ls = 0;
 #pragma unroll
                         for (int jj = 0; jj < 4; jj++) {
-                            dv[jj] = 0;
-                            if (i0 + jj < wb) {
-                                const uint32_t k = pts[i0 + jj];
-                                dv[jj] = (uint32_t)dmin_chosen(unpack_r(k), unpack_g(k), unpack_b(k), ch, kk);
-                            }
+                            const uint32_t i = i0 + (uint32_t)jj;
+                            const bool in = i >= a && i < b;
+                            dv[jj] = in ? (uint32_t)dmin_chosen(unpack_r(kq[jj]), unpack_g(kq[jj]), unpack_b(kq[jj]), ch, kk) : 0u;
                             ls += dv[jj];
                         }
                         unsigned long long x = ls;
@@ -480,18 +546,18 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
                         int hit = -1;
 #pragma unroll
                         for (int jj = 0; jj < 4; jj++) {
+                            const uint32_t i = i0 + (uint32_t)jj;
                             ee += dv[jj];
-                            if (hit < 0 && (double)ee >= pj) hit = jj;
+                            if (hit < 0 && i >= a && i < b && (double)ee >= pj) hit = jj;
                         }
                         const unsigned long long bal = __ballot(hit >= 0);
                         if (bal) {
                             const int first = (int)__builtin_ctzll(bal);
                             found = (int)(s0 + (uint32_t)first * 4) + __shfl(hit, first);
                         }
-                        e += __shfl(x, 63);
+                        if (lane == 0) atomicAdd(&sm.sel_pts, (unsigned long long)STEP);
                     }
                     if (found >= 0) ci = min(found, N - 1);
-                    if (lane == 0) atomicAdd(&sm.sel_pts, scanned);
                 }
                 if (lane == 0) sm.pj[j] = ci;
             }
