@@ -31,7 +31,9 @@
 extern "C" {
 #endif
 
-#define LLFE_ABI_VERSION 1
+#define LLFE_ABI_VERSION 2
+/* most k-means centres per image (extract_colors(n_colors=...) accepts 1 .. LLFE_MAX_COLORS) */
+#define LLFE_MAX_COLORS 32
 
 #define LLFE_OK 0
 #define LLFE_ERR_INVALID (-1)
@@ -71,7 +73,7 @@ typedef struct {
      * distribution. */
     const int8_t *noise;
     int32_t noise_on_device;
-    int32_t n_colors;      /* extract_colors(n_colors=...) in [1, 5]; 0 -> 5 (the default) */
+    int32_t n_colors;      /* extract_colors(n_colors=...) in [1, LLFE_MAX_COLORS]; 0 -> 5 (the default) */
     int64_t index_base;    /* global index of image 0 (seeds are per global index) */
 } llfe_batch;
 
@@ -81,9 +83,9 @@ typedef struct {
                                   (n_colors = 1 or U <= 1) the reference returns every unique
                                   colour with labels [0]*U (color_extractor.py:185-186): here
                                   the first min(U, 5) in np.unique order, counts [U, 0, ...] */
-    int32_t counts[5];         /* np.bincount(labels) per centre, k-means order */
-    uint8_t centers_rgb[5][3]; /* centers.astype(np.uint8), k-means order */
-    uint8_t pad_[1];
+    int32_t counts[LLFE_MAX_COLORS];         /* np.bincount(labels) per centre, k-means order */
+    uint8_t centers_rgb[LLFE_MAX_COLORS][3]; /* centers.astype(np.uint8), k-means order */
+    uint8_t pad_[4];
     int64_t n_unique;          /* len(np.unique(pixels, axis=0)) */
     double compactness;        /* best cv2.kmeans compactness */
     /* shadows: processed[thresh == 255] sum / size (shadow pyc @L21-24) */

@@ -14,9 +14,9 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libllfe.so")
-SOURCES = ["llfe_api.cpp", "contours.cpp", "png_decode.cpp", "jpeg_decode.cpp", "stencil.hip", "stencil_stream.hip", "hysteresis.hip", "unique.hip", "kmeans.hip", "resize.hip", "contours_gpu.hip",
+SOURCES = ["llfe_api.cpp", "contours.cpp", "png_decode.cpp", "jpeg_decode.cpp", "stencil.hip", "stencil_stream.hip", "hysteresis.hip", "unique.hip", "kmeans.hip", "kmeans_big.hip", "resize.hip", "contours_gpu.hip",
            "cvresize.hip"]
-HEADERS = ["llfe_internal.h", "contours.h"]
+HEADERS = ["llfe_internal.h", "contours.h", "kmeans_common.h"]
 ARCH = os.environ.get("LLFE_OFFLOAD_ARCH", "gfx950")
 
 

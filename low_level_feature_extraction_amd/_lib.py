@@ -34,6 +34,9 @@ FEATURE_SHADOWS = 4
 SHAPE_TYPES = {0: "unknown", 1: "triangle", 2: "rectangle", 3: "circle", 4: "polygon"}
 
 
+MAX_COLORS = 32  # LLFE_MAX_COLORS (include/llfe.h)
+
+
 class LlfeBatch(C.Structure):
     _fields_ = [
         ("data", C.c_void_p),
@@ -51,9 +54,9 @@ class LlfeBatch(C.Structure):
 class LlfeImageResult(C.Structure):
     _fields_ = [
         ("n_colors", C.c_int32),
-        ("counts", C.c_int32 * 5),
-        ("centers_rgb", (C.c_uint8 * 3) * 5),
-        ("pad_", C.c_uint8),
+        ("counts", C.c_int32 * MAX_COLORS),
+        ("centers_rgb", (C.c_uint8 * 3) * MAX_COLORS),
+        ("pad_", C.c_uint8 * 4),
         ("n_unique", C.c_int64),
         ("compactness", C.c_double),
         ("shadow_sum", C.c_uint64),

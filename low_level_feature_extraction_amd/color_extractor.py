@@ -25,6 +25,7 @@ from typing import List, Optional, Union
 
 import numpy as np
 
+from ._lib import MAX_COLORS
 from .models import ColorFeatures
 
 try:
@@ -157,8 +158,8 @@ class ColorExtractor:
         bgr = np.ascontiguousarray(px[:, ::-1]).reshape(1, -1, 3)
         zero = np.zeros(bgr.size, np.int8)
         idx = _next_index()
-        if not 1 <= int(n_colors) <= 5:
-            raise ValueError("the MI355X backend supports n_colors in [1, 5]")
+        if not 1 <= int(n_colors) <= MAX_COLORS:
+            raise ValueError(f"the MI355X backend supports n_colors in [1, {MAX_COLORS}]")
         r = _backend().process(bgr[None], ("colors",), seed=_SEED if seed is None else seed, noise=zero,
                                index_base=idx, n_colors=int(n_colors))[0]
         centers = r.centers_rgb
@@ -203,8 +204,8 @@ class ColorExtractor:
             k = int(n_colors)
             if k <= 1:
                 return ColorExtractor._unique_palette(bgr)
-            if k > 5:
-                raise ValueError("the MI355X backend supports n_colors <= 5")
+            if k > MAX_COLORS:
+                raise ValueError(f"the MI355X backend supports n_colors <= {MAX_COLORS}")
             r = _backend().process(bgr[None], ("colors",), seed=_SEED, index_base=_next_index(), n_colors=k)[0]
             return ColorExtractor._palette(r.centers_rgb, r.counts)
         except Exception as e:  # the reference never raises from extract_colors

@@ -20,7 +20,7 @@
 //  * compactness = sum of double(normL2Sqr) to the final centres with the labels of
 //    the last assignment.  Cluster sums are exact int64 (OpenCV accumulates float32
 //    sequentially; the difference is far below the uint8 truncation of the output).
-#include "llfe_internal.h"
+#include "kmeans_common.h"
 
 namespace llfe {
 namespace {
@@ -33,23 +33,9 @@ constexpr int KW = KT / 64;       // waves
 constexpr int STEP = 256;         // points per wave step (64 lanes x 4)
 constexpr float kFar = 1e30f;     // coordinate of an unused centre: its distance is +inf
 
-__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
-    x += 0x9E3779B97F4A7C15ull;
-    uint64_t z = x;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-}
-
-__device__ __forceinline__ uint32_t cvrng_next(uint64_t &s) {
-    s = (uint64_t)(uint32_t)s * 4164903690ull + (uint32_t)(s >> 32);
-    return (uint32_t)s;
-}
-__device__ __forceinline__ double cvrng_double(uint64_t &s) {
-    uint32_t t = cvrng_next(s);
-    uint64_t v = ((uint64_t)t << 32) | cvrng_next(s);
-    return (double)v * 5.4210108624275221700372640043497e-20;
-}
+using km::cvrng_double;
+using km::cvrng_next;
+using km::splitmix64;
 
 __device__ __forceinline__ float uni(float v) {
     return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
@@ -1613,9 +1599,15 @@ hipError_t launch_kmeans(const uint32_t *keys, int64_t key_stride, const int64_t
         attr_set = true;
     }
     hipLaunchKernelGGL(k_kmeans_order, dim3(1), dim3(OT), 0, s, (const long long *)n_unique, n, order);
-    hipLaunchKernelGGL(cubes.cubes ? k_kmeans<true> : k_kmeans<false>, dim3(n * kAttempts), dim3(KT), smem, s, keys, (long long)key_stride,
-                       (const long long *)n_unique, n_colors, (unsigned long long)seed, (long long)index_base, order,
-                       scratch, (long long)scratch_stride, attempts, cubes);
+    if (n_colors > kMaxK) {  // general K: plain sweeps over the keys (kmeans_big.hip)
+        const hipError_t e = launch_kmeans_big(keys, key_stride, n_unique, n, n_colors, seed, index_base, order,
+                                               scratch, scratch_stride, attempts, s);
+        if (e != hipSuccess) return e;
+    } else {
+        hipLaunchKernelGGL(cubes.cubes ? k_kmeans<true> : k_kmeans<false>, dim3(n * kAttempts), dim3(KT), smem, s, keys,
+                           (long long)key_stride, (const long long *)n_unique, n_colors, (unsigned long long)seed,
+                           (long long)index_base, order, scratch, (long long)scratch_stride, attempts, cubes);
+    }
     hipLaunchKernelGGL(k_kmeans_finalize, dim3((n + 255) / 256), dim3(256), 0, s, keys, (long long)key_stride,
                        (const long long *)n_unique, n, n_colors, attempts, out);
     return hipGetLastError();

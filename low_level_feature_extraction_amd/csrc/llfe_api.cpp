@@ -585,7 +585,8 @@ int color_stage(llfe_ctx *ctx, Work &W, const uint8_t *img, const int8_t *noise,
 
 int kmeans_stage(llfe_ctx *ctx, Work &W, const uint32_t *keys, int64_t key_stride, const int64_t *d_nuniq, int n,
                  int n_colors, uint64_t seed, int64_t index_base, const KmeansCubes &cubes, hipStream_t s) {
-    if (n_colors < 1 || n_colors > kMaxK) return ctx->fail(LLFE_ERR_UNSUPPORTED, "n_colors must be in [1, 5]");
+    if (n_colors < 1 || n_colors > kMaxColors)
+        return ctx->fail(LLFE_ERR_UNSUPPORTED, "n_colors must be in [1, LLFE_MAX_COLORS]");
     const int64_t sstride = kmeans_scratch_stride(key_stride);
     HIPCHK(ctx, W.d_order.ensure(n));
     HIPCHK(ctx, W.d_kscratch.ensure((size_t)n * kAttempts * sstride));
@@ -619,7 +620,7 @@ int kmeans_stage(llfe_ctx *ctx, Work &W, const uint32_t *keys, int64_t key_strid
 
 void fill_color_result(const KmeansImageOut &k, llfe_image_result &r) {
     r.n_colors = k.k;
-    for (int c = 0; c < 5; c++) {
+    for (int c = 0; c < kMaxColors; c++) {
         r.counts[c] = k.counts[c];
         for (int j = 0; j < 3; j++) r.centers_rgb[c][j] = k.centers_rgb[c][j];
     }
@@ -1013,8 +1014,8 @@ int llfe_process_batch(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, ui
     if (!ctx || !b || !results) return LLFE_ERR_INVALID;
     if (!valid_dims(b->n, b->height, b->width) || (b->n > 0 && !b->data))
         return ctx->fail(LLFE_ERR_INVALID, "invalid batch n=%d h=%d w=%d", b->n, b->height, b->width);
-    if (b->n_colors < 0 || b->n_colors > kMaxK)
-        return ctx->fail(LLFE_ERR_UNSUPPORTED, "n_colors=%d outside [1, %d]", b->n_colors, kMaxK);
+    if (b->n_colors < 0 || b->n_colors > kMaxColors)
+        return ctx->fail(LLFE_ERR_UNSUPPORTED, "n_colors=%d outside [1, %d]", b->n_colors, kMaxColors);
     if (ctx->inflight[0].busy || ctx->inflight[1].busy)
         return ctx->fail(LLFE_ERR_INVALID, "llfe_process_batch with submitted batches not yet collected");
     HIPCHK(ctx, hipSetDevice(ctx->device));
@@ -1066,8 +1067,8 @@ int llfe_submit_batch(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uin
     if (!ctx || !b || !ticket) return LLFE_ERR_INVALID;
     if (!valid_dims(b->n, b->height, b->width) || (b->n > 0 && !b->data))
         return ctx->fail(LLFE_ERR_INVALID, "invalid batch n=%d h=%d w=%d", b->n, b->height, b->width);
-    if (b->n_colors < 0 || b->n_colors > kMaxK)
-        return ctx->fail(LLFE_ERR_UNSUPPORTED, "n_colors=%d outside [1, %d]", b->n_colors, kMaxK);
+    if (b->n_colors < 0 || b->n_colors > kMaxColors)
+        return ctx->fail(LLFE_ERR_UNSUPPORTED, "n_colors=%d outside [1, %d]", b->n_colors, kMaxColors);
     if (b->n > chunk_for(ctx->chunk, b->height, b->width))
         return ctx->fail(LLFE_ERR_UNSUPPORTED, "llfe_submit_batch: n=%d exceeds one device pass (%d)", b->n,
                          chunk_for(ctx->chunk, b->height, b->width));

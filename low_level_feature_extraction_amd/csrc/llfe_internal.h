@@ -117,15 +117,16 @@ inline size_t stencil_parts(int n, int h, int w) {
 }
 
 // ---------------------------------------------------------------- colours
-constexpr int kMaxK = 5;
+constexpr int kMaxK = 5;                     // the cube-table k-means (n_colors <= 5)
+constexpr int kMaxColors = LLFE_MAX_COLORS;  // the generic k-means (k_kmeans_big) up to this
 constexpr int kAttempts = 10;
 constexpr int kParts = 64;         // key partitions by red quarter r >> 2
 constexpr int kCubesPerPart = 4096;  // 64 x 64 cubes of 4x4x4 per partition
 
 struct KmeansAttemptOut {
     double compactness;
-    float centers[kMaxK][3];
-    int32_t counts[kMaxK];
+    float centers[kMaxColors][3];
+    int32_t counts[kMaxColors];
     int32_t iters;
     int32_t pad;
     uint64_t bytes;  // algorithmic bytes this attempt read (keys, cube table)
@@ -141,9 +142,9 @@ struct KmeansAttemptOut {
 
 struct KmeansImageOut {
     int32_t k;
-    int32_t counts[kMaxK];
-    uint8_t centers_rgb[kMaxK][3];
-    uint8_t pad[1];
+    int32_t counts[kMaxColors];
+    uint8_t centers_rgb[kMaxColors][3];
+    uint8_t pad[4];
     int64_t n_unique;
     double compactness;
     uint64_t bytes;  // algorithmic bytes read, summed over the attempts (roofline)
@@ -192,6 +193,11 @@ hipError_t launch_kmeans(const uint32_t *keys, int64_t key_stride, const int64_t
                          uint64_t seed, int64_t index_base, int32_t *order, uint32_t *scratch, int64_t scratch_stride,
                          KmeansAttemptOut *attempts, KmeansImageOut *out, const KmeansCubes &cubes,
                          hipStream_t s);
+// K in (kMaxK, kMaxColors]: the general-K attempts (kmeans_big.hip) in the order of
+// k_kmeans_order, into the same attempt records (launch_kmeans calls it)
+hipError_t launch_kmeans_big(const uint32_t *keys, int64_t key_stride, const int64_t *n_unique, int n, int n_colors,
+                             uint64_t seed, int64_t index_base, const int32_t *order, uint32_t *scratch,
+                             int64_t scratch_stride, KmeansAttemptOut *attempts, hipStream_t s);
 // u32 scratch per (image, attempt) for k-means++ step sums
 int64_t kmeans_scratch_stride(int64_t key_stride);
 constexpr int kMaxKmeansBatch = 4096;

@@ -39,9 +39,9 @@ def test_library_exports_every_header_symbol():
 
 
 def test_abi_version_and_struct_sizes():
-    assert L.lib().llfe_abi_version() == 1
+    assert L.lib().llfe_abi_version() == 2
     assert C.sizeof(L.LlfeBatch) == 48
-    assert C.sizeof(L.LlfeImageResult) == 88
+    assert C.sizeof(L.LlfeImageResult) == 280
     assert C.sizeof(L.LlfeShape) == 40
     assert C.sizeof(L.LlfeKernelStat) == 56
 

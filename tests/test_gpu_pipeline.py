@@ -141,6 +141,47 @@ def test_n_colors_parameter(backend, orc):
             assert delta_e_matched(r.centers_rgb, centers) <= 2.5
 
 
+@pytest.mark.parametrize("k", [6, 8, 12, 32])
+def test_n_colors_above_five_vs_oracle(backend, orc, k):
+    """K = min(n_colors, U) > 5 runs the general-K kernel (kmeans_big.hip): same attempts
+    and the same bar as K <= 5, through the batch path and the fine-grained llfe_kmeans."""
+    import torch
+
+    x = np.stack([synth.synth_numpy(i, 120, 200, seed=31) for i in range(2)])
+    noise = np.stack([orc.numpy_noise(120 * 200, 40 + i) for i in range(2)])
+    res = backend.process(x, ("colors",), seed=6, noise=noise, n_colors=k)
+    for i, r in enumerate(res):
+        centers, counts, nu, comp = orc.dominant_colors(x[i], noise[i], k, orc.image_rng_state(6, i))
+        assert len(r.centers_rgb) == len(centers) == min(k, nu)
+        assert int(np.sum(r.counts)) == nu
+        kmeans_bar.check(r.centers_rgb, r.counts, r.compactness, centers, counts, comp, nu, tag=f"batch-K{k}")
+    keys_list = [orc.color_unique(x[i], noise[i]) for i in range(2)]
+    stride = (max(len(q) for q in keys_list) + 3) // 4 * 4
+    buf = np.zeros((2, stride), np.uint32)
+    for i, q in enumerate(keys_list):
+        buf[i, : len(q)] = q
+    got = backend.kmeans(torch.from_numpy(buf.view(np.int32)).cuda(), np.array([len(q) for q in keys_list]), k, seed=9)
+    for i, q in enumerate(keys_list):
+        data = np.stack([(q >> 16) & 255, (q >> 8) & 255, q & 255], -1).astype(np.float32)
+        comp, labels, centers, counts, _ = orc.kmeans(data, min(k, len(q)), rng_state=orc.image_rng_state(9, i))
+        gc, gcount, gcomp = got[i]
+        kmeans_bar.check(gc, gcount, gcomp, centers.astype(np.uint8), np.bincount(labels, minlength=len(centers)),
+                         comp, len(q), tag=f"abi-K{k}")
+
+
+def test_n_colors_above_five_few_unique(backend, orc):
+    """U < n_colors: K = U (every colour its own cluster)."""
+    x = np.zeros((1, 30, 40, 3), np.uint8)
+    x[0, :, :20] = (10, 200, 30)
+    x[0, :10, 20:] = (90, 20, 240)
+    x[0, 10:, 20:] = (250, 250, 5)
+    noise = np.zeros((1, 30 * 40 * 3), np.int8)
+    r = backend.process(x, ("colors",), seed=2, noise=noise, n_colors=12)[0]
+    centers, counts, nu, comp = orc.dominant_colors(x[0], noise[0], 12, orc.image_rng_state(2, 0))
+    assert nu == 3 and len(r.centers_rgb) == 3
+    kmeans_bar.check(r.centers_rgb, r.counts, r.compactness, centers, counts, comp, nu, tag="K12-U3")
+
+
 # --------------------------------------------------------------------------- drop-ins
 def test_shape_and_shadow_analyzers(orc):
     from low_level_feature_extraction_amd import ShadowAnalyzer, ShapeAnalyzer
@@ -167,7 +208,8 @@ def test_color_extractor_dropin(orc):
     assert res.metadata["success"] is True
     res = ColorExtractor.extract_colors(np.zeros((2, 5, 6, 3), np.uint8))  # 4-D: flattened like the reference
     assert res.metadata["success"] is True
-    assert ColorExtractor.extract_colors(img, n_colors=9).metadata["success"] is False
+    assert ColorExtractor.extract_colors(img, n_colors=9).metadata["success"] is True  # general-K kernel
+    assert ColorExtractor.extract_colors(img, n_colors=33).metadata["success"] is False  # > LLFE_MAX_COLORS
     batch = ColorExtractor.extract_colors_batch([img, img[:50], img], seed=4)
     assert len(batch) == 3 and all(b.metadata["success"] for b in batch)
 
