@@ -75,6 +75,9 @@ typedef struct {
     int32_t noise_on_device;
     int32_t n_colors;      /* extract_colors(n_colors=...) in [1, LLFE_MAX_COLORS]; 0 -> 5 (the default) */
     int64_t index_base;    /* global index of image 0 (seeds are per global index) */
+    const int64_t *indices; /* optional (host): global index of each image, overriding
+                               index_base + i -- results stay those of each image's own index
+                               whatever the batching (a request's image keeps its seeds) */
 } llfe_batch;
 
 typedef struct {
@@ -156,6 +159,32 @@ int llfe_kernel_stats(llfe_ctx *ctx, llfe_kernel_stat *out, int32_t cap);
 int llfe_process_batch(llfe_ctx *ctx, const llfe_batch *batch, uint32_t features, uint64_t seed,
                        llfe_image_result *results, llfe_shape *shapes, int64_t shape_capacity,
                        int64_t *shapes_needed, llfe_stream stream);
+
+/* One image of a ragged batch: H x W BGR u8 pixels, rows of W * 3 bytes row_stride bytes
+ * apart (0: packed), in host or device memory. */
+typedef struct {
+    const uint8_t *data;
+    int32_t height, width;
+    int64_t row_stride;
+    int32_t on_device;
+    int32_t noise_on_device;
+    /* optional parity-mode noise of this image after preprocessing (H' x W' x 3 int8, RGB
+     * order, as llfe_batch.noise); give it for every image of the call or for none */
+    const int8_t *noise;
+} llfe_image_desc;
+
+/* llfe_process_batch for a ragged batch: every image its own size, row
+ * stride and memory, plus validate_and_preprocess_image's resize rule applied on the GPU
+ * first (preprocessing = LLFE_PRE_NONE / AUTO / HIGH_QUALITY / PERFORMANCE, utils.py:
+ * 118-143: INTER_AREA above 2000 px / LANCZOS4 above 4000 / LINEAR above 1000).  Images
+ * of one (preprocessed) size share device passes; image i keeps global index
+ * index_base + i, so its results equal a one-image call's.  results[i] belongs to
+ * images[i]; its shapes are shapes[results[i].shape_offset ...] (LLFE_ERR_CAPACITY and
+ * *shapes_needed as llfe_process_batch).  Synchronous. */
+int llfe_process_images(llfe_ctx *ctx, const llfe_image_desc *images, int32_t n, uint32_t features,
+                        int32_t preprocessing, int32_t n_colors, uint64_t seed, int64_t index_base,
+                        llfe_image_result *results, llfe_shape *shapes, int64_t shape_capacity,
+                        int64_t *shapes_needed, llfe_stream stream);
 
 /* Asynchronous form (serving loops): llfe_submit_batch enqueues the device work of one
  * batch (n <= one device pass) and returns a ticket; llfe_collect_batch (tickets in

@@ -48,6 +48,7 @@ class LlfeBatch(C.Structure):
         ("noise_on_device", C.c_int32),
         ("n_colors", C.c_int32),
         ("index_base", C.c_int64),
+        ("indices", C.c_void_p),
     ]
 
 
@@ -64,6 +65,18 @@ class LlfeImageResult(C.Structure):
         ("shape_offset", C.c_int64),
         ("n_shapes", C.c_int32),
         ("n_contours", C.c_int32),
+    ]
+
+
+class LlfeImageDesc(C.Structure):
+    _fields_ = [
+        ("data", C.c_void_p),
+        ("height", C.c_int32),
+        ("width", C.c_int32),
+        ("row_stride", C.c_int64),
+        ("on_device", C.c_int32),
+        ("noise_on_device", C.c_int32),
+        ("noise", C.c_void_p),
     ]
 
 
@@ -106,6 +119,8 @@ SIGNATURES = {
     "llfe_collect_batch": (C.c_int, [_vp, C.c_int64, _vp, _vp, C.c_int64, C.POINTER(C.c_int64)]),
     "llfe_kernel_stats": (C.c_int, [_vp, C.POINTER(LlfeKernelStat), _i32]),
     "llfe_process_batch": (C.c_int, [_vp, C.POINTER(LlfeBatch), _u32, _u64, _vp, _vp, _i64, C.POINTER(C.c_int64), _vp]),
+    "llfe_process_images": (C.c_int, [_vp, _vp, _i32, _u32, _i32, _i32, _u64, _i64, _vp, _vp, _i64,
+                                      C.POINTER(C.c_int64), _vp]),
     "llfe_gray_blur5": (C.c_int, [_vp, _vp, _vp, _i32, _i32, _i32, _vp]),
     "llfe_shape_mask": (C.c_int, [_vp, _vp, _vp, _i32, _i32, _i32, _vp]),
     "llfe_edge_classes": (C.c_int, [_vp, _vp, _vp, _i32, _i32, _i32, _vp]),

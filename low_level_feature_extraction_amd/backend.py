@@ -202,6 +202,64 @@ class Backend:
         del keep, nkeep
         return out
 
+    def process_images(self, images, features=("colors", "shapes", "shadows"), seed: int = 0, noise=None,
+                       index_base: int = 0, n_colors: int = 5, preprocessing: str = "none") -> list:
+        """Ragged batch through llfe_process_images: ``images`` is a list of H x W x 3 BGR
+        uint8 images of any sizes -- numpy arrays (host) or torch tensors (host or GPU;
+        rows may be strided, pixels must be packed) -- with validate_and_preprocess_image's
+        resize rule (``preprocessing``: none / auto / high_quality / performance; other
+        names do not resize, as in utils.py:116-143) applied on the GPU first.  Image i
+        keeps global index index_base + i.  ``noise``: one parity-noise array per image of
+        its preprocessed size, or None.  Returns ImageFeatures in input order."""
+        n = len(images)
+        mode = PRE_MODES.get(preprocessing, 0)
+        descs = (L.LlfeImageDesc * max(n, 1))()
+        keep, sizes = [], []
+        for i, im in enumerate(images):
+            if _is_torch(im):
+                t = im
+                if t.dtype != _torch().uint8 or t.dim() != 3 or t.shape[2] != 3:
+                    raise ValueError(f"image {i}: expected H x W x 3 uint8, got {tuple(t.shape)} {t.dtype}")
+                if t.stride(2) != 1 or t.stride(1) != 3:
+                    t = t.contiguous()  # pixels not packed: one explicit copy
+                ptr, h, w, stride, dev = t.data_ptr(), t.shape[0], t.shape[1], t.stride(0), int(t.is_cuda)
+            else:
+                t = np.asarray(im)
+                if t.dtype != np.uint8 or t.ndim != 3 or t.shape[2] != 3:
+                    raise ValueError(f"image {i}: expected H x W x 3 uint8, got {t.shape} {t.dtype}")
+                if t.strides[2] != 1 or t.strides[1] != 3 or t.strides[0] < 3 * t.shape[1]:
+                    t = np.ascontiguousarray(t)
+                ptr, h, w, stride, dev = t.ctypes.data, t.shape[0], t.shape[1], t.strides[0], 0
+            keep.append(t)
+            descs[i].data, descs[i].height, descs[i].width = ptr, h, w
+            descs[i].row_stride, descs[i].on_device = stride, dev
+            plan = preprocess_size(w, h, preprocessing)
+            oh, ow = (plan[1], plan[0]) if plan else (h, w)
+            sizes.append((ow, oh))
+            if noise is not None:
+                nptr, n_on_dev, nk = self._noise_view(noise[i], 1, oh, ow)
+                keep.append(nk)
+                descs[i].noise, descs[i].noise_on_device = nptr, n_on_dev
+        mask = feature_mask(features)
+        results = (L.LlfeImageResult * max(n, 1))()
+        cap = max(64 * n, 64)
+        needed = C.c_int64(0)
+        stream = self._stream(next((t for t in keep if _is_torch(t) and t.is_cuda), None))
+        with self._lock:
+            while True:
+                shapes = (L.LlfeShape * cap)()
+                rc = self._lib.llfe_process_images(self.ctx, descs, n, mask, mode, int(n_colors),
+                                                   C.c_uint64(seed & (2**64 - 1)), index_base, results, shapes, cap,
+                                                   C.byref(needed), stream)
+                if rc == L.LLFE_ERR_CAPACITY and needed.value > cap:
+                    cap = int(needed.value)
+                    continue
+                self._chk(rc)
+                break
+        out = self._convert(results, shapes, n, mask, [sz[0] for sz in sizes], [sz[1] for sz in sizes])
+        del keep
+        return out
+
     @staticmethod
     def _convert(results, shapes, n, mask, w, h) -> list:
         # bulk conversion through numpy views of the ctypes arrays (per-field ctypes
@@ -222,8 +280,10 @@ class Backend:
                     for t, x, y, ww, hh, br, ar in zip(S["type"].tolist(), S["x"].tolist(), S["y"].tolist(),
                                                        S["width"].tolist(), S["height"].tolist(),
                                                        S["border_radius"].tolist(), S["area"].tolist())]
+        ws = w if isinstance(w, list) else [w] * n
+        hs = h if isinstance(h, list) else [h] * n
         out = [ImageFeatures(cen[i, :ncol[i]], cnt[i, :ncol[i]], nu[i], comp[i], ssum[i], scnt[i],
-                             recs[off[i]:off[i] + nsh[i]] if recs else [], ncont[i], w, h) for i in range(n)]
+                             recs[off[i]:off[i] + nsh[i]] if recs else [], ncont[i], ws[i], hs[i]) for i in range(n)]
         return out
 
     # ------------------------------------------------------------------ async batches

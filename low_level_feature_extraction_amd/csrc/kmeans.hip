@@ -820,7 +820,7 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
 template <bool kCubes>
 __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__restrict__ keys, long long key_stride,
                                                const long long *__restrict__ n_unique, int n_colors,
-                                               unsigned long long seed, long long index_base,
+                                               unsigned long long seed, ImgIndex index,
                                                const int *__restrict__ order,
                                                uint32_t *__restrict__ scratch, long long scratch_stride,
                                                KmeansAttemptOut *__restrict__ out, const KmeansCubes cubes) {
@@ -877,7 +877,7 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
     if (tid == 0) sm.fail_pts = 0;
 #define SSLOT(slot) (ss + (size_t)(slot) * (size_t)M)
 
-    uint64_t rng = splitmix64(seed + (unsigned long long)(index_base + img));
+    uint64_t rng = splitmix64(seed + (unsigned long long)index.at(img));
     if (rng == 0) rng = 0xFFFFFFFFull;  // cv::RNG(0) takes the default state
     for (int q = 0, skip = att * (1 + 6 * (K - 1)); q < skip; q++) cvrng_next(rng);
 
@@ -1584,7 +1584,7 @@ __global__ void k_kmeans_finalize(const uint32_t *__restrict__ keys, long long k
 }  // namespace
 
 hipError_t launch_kmeans(const uint32_t *keys, int64_t key_stride, const int64_t *n_unique, int n, int n_colors,
-                         uint64_t seed, int64_t index_base, int32_t *order, uint32_t *scratch, int64_t scratch_stride,
+                         uint64_t seed, ImgIndex index, int32_t *order, uint32_t *scratch, int64_t scratch_stride,
                          KmeansAttemptOut *attempts, KmeansImageOut *out, const KmeansCubes &cubes,
                          hipStream_t s) {
     if (n > OMAX) return hipErrorInvalidValue;
@@ -1600,13 +1600,13 @@ hipError_t launch_kmeans(const uint32_t *keys, int64_t key_stride, const int64_t
     }
     hipLaunchKernelGGL(k_kmeans_order, dim3(1), dim3(OT), 0, s, (const long long *)n_unique, n, order);
     if (n_colors > kMaxK) {  // general K: plain sweeps over the keys (kmeans_big.hip)
-        const hipError_t e = launch_kmeans_big(keys, key_stride, n_unique, n, n_colors, seed, index_base, order,
+        const hipError_t e = launch_kmeans_big(keys, key_stride, n_unique, n, n_colors, seed, index, order,
                                                scratch, scratch_stride, attempts, s);
         if (e != hipSuccess) return e;
     } else {
         hipLaunchKernelGGL(cubes.cubes ? k_kmeans<true> : k_kmeans<false>, dim3(n * kAttempts), dim3(KT), smem, s, keys,
                            (long long)key_stride, (const long long *)n_unique, n_colors, (unsigned long long)seed,
-                           (long long)index_base, order, scratch, (long long)scratch_stride, attempts, cubes);
+                           index, order, scratch, (long long)scratch_stride, attempts, cubes);
     }
     hipLaunchKernelGGL(k_kmeans_finalize, dim3((n + 255) / 256), dim3(256), 0, s, keys, (long long)key_stride,
                        (const long long *)n_unique, n, n_colors, attempts, out);

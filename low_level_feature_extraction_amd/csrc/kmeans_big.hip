@@ -90,7 +90,7 @@ __device__ __forceinline__ int moved_label(const BigSmem &sm, int i, int l) {
 
 __global__ __launch_bounds__(BT) void k_kmeans_big(const uint32_t *__restrict__ keys, long long key_stride,
                                                    const long long *__restrict__ n_unique, int n_colors,
-                                                   unsigned long long seed, long long index_base,
+                                                   unsigned long long seed, ImgIndex index,
                                                    const int *__restrict__ order, uint32_t *__restrict__ scratch,
                                                    long long scratch_stride, KmeansAttemptOut *__restrict__ out) {
     __shared__ BigSmem sm;
@@ -130,7 +130,7 @@ __global__ __launch_bounds__(BT) void k_kmeans_big(const uint32_t *__restrict__ 
         }
         return cnt;
     };
-    uint64_t rng = attempt_rng(seed, index_base + img, att, K);
+    uint64_t rng = attempt_rng(seed, index.at(img), att, K);
 
     // ------------------------------------------------ k-means++ (generateCentersPP)
     {
@@ -479,11 +479,11 @@ __global__ __launch_bounds__(BT) void k_kmeans_big(const uint32_t *__restrict__ 
 }  // namespace
 
 hipError_t launch_kmeans_big(const uint32_t *keys, int64_t key_stride, const int64_t *n_unique, int n, int n_colors,
-                             uint64_t seed, int64_t index_base, const int32_t *order, uint32_t *scratch,
+                             uint64_t seed, ImgIndex index, const int32_t *order, uint32_t *scratch,
                              int64_t scratch_stride, KmeansAttemptOut *attempts, hipStream_t s) {
     if (n_colors > kMaxColors) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_kmeans_big, dim3(n * kAttempts), dim3(BT), 0, s, keys, (long long)key_stride,
-                       (const long long *)n_unique, n_colors, (unsigned long long)seed, (long long)index_base, order,
+                       (const long long *)n_unique, n_colors, (unsigned long long)seed, index, order,
                        scratch, (long long)scratch_stride, attempts);
     return hipGetLastError();
 }

@@ -19,6 +19,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <map>
 #include <cstring>
 #include <functional>
 #include <mutex>
@@ -214,6 +215,7 @@ struct Work {
     DevBuf<int64_t> d_nuniq;
     DevBuf<KmeansAttemptOut> d_att;
     DevBuf<KmeansImageOut> d_kout;
+    DevBuf<long long> d_index;  // per-image global indices of the chunk (llfe_batch.indices)
     // GPU contours (contours_gpu.hip); capacities grow when a pass overflows them
     DevBuf<uint64_t> d_ct_planes;
     DevBuf<CtComp> d_ct_comps;
@@ -390,6 +392,8 @@ struct llfe_ctx {
     Pending inflight[2];
     int64_t next_ticket = 0, next_collect = 0;
     DevBuf<uint8_t> d_rsz_tmp, d_rsz_src;
+    DevBuf<uint8_t> d_ragged;       // llfe_process_images: one size group's packed images
+    DevBuf<int8_t> d_ragged_noise;
     DevBuf<int32_t> d_coef;
     // pinned host staging; the per-chunk results are double-buffered so the host can
     // trace chunk c's contours while the GPU runs chunk c + 1
@@ -554,7 +558,7 @@ void grow_contour_caps(Work &W, int n, int h, int w, const CtCounters &ct) {
 }
 
 int color_stage(llfe_ctx *ctx, Work &W, const uint8_t *img, const int8_t *noise, int n, int h, int w, uint64_t seed,
-                int64_t index_base, hipStream_t s) {
+                ImgIndex index, hipStream_t s) {
     // unique colours -> W.d_keys (sorted, key_stride) + cube table for k-means
     const int64_t P = (int64_t)h * w;
     const int64_t key_stride = (std::max<int64_t>(P, 1) + 3) & ~int64_t(3);
@@ -570,7 +574,7 @@ int color_stage(llfe_ctx *ctx, Work &W, const uint8_t *img, const int8_t *noise,
              *cc = uq + (size_t)n * kParts;
     HIPCHK(ctx, hipMemsetAsync(hist, 0, sizeof(uint32_t) * 2 * n * kParts, s));
     TIMED(ctx, s, "k_uq_keys", (double)n * P * (noise ? 10 : 7),
-          launch_uq_keys(img, noise, n, h, w, seed, index_base, key_stride, W.d_raw.p, hist, s));
+          launch_uq_keys(img, noise, n, h, w, seed, index, key_stride, W.d_raw.p, hist, s));
     TIMED(ctx, s, "k_uq_scatter", (double)n * P * 8,
           launch_uq_scatter(W.d_raw.p, n, P, key_stride, hist, cursor, W.d_keys.p, s));
     // the partitions' sorted unique keys overwrite the (dead) raw keys
@@ -584,7 +588,7 @@ int color_stage(llfe_ctx *ctx, Work &W, const uint8_t *img, const int8_t *noise,
 }
 
 int kmeans_stage(llfe_ctx *ctx, Work &W, const uint32_t *keys, int64_t key_stride, const int64_t *d_nuniq, int n,
-                 int n_colors, uint64_t seed, int64_t index_base, const KmeansCubes &cubes, hipStream_t s) {
+                 int n_colors, uint64_t seed, ImgIndex index, const KmeansCubes &cubes, hipStream_t s) {
     if (n_colors < 1 || n_colors > kMaxColors)
         return ctx->fail(LLFE_ERR_UNSUPPORTED, "n_colors must be in [1, LLFE_MAX_COLORS]");
     const int64_t sstride = kmeans_scratch_stride(key_stride);
@@ -594,7 +598,7 @@ int kmeans_stage(llfe_ctx *ctx, Work &W, const uint32_t *keys, int64_t key_strid
     HIPCHK(ctx, W.d_kout.ensure(n));
     // per-image cv::RNG state = splitmix64(seed + global index) is derived on the device
     TIMED(ctx, s, "k_kmeans", 0,
-          launch_kmeans(keys, key_stride, d_nuniq, n, n_colors, seed, index_base, W.d_order.p, W.d_kscratch.p,
+          launch_kmeans(keys, key_stride, d_nuniq, n, n_colors, seed, index, W.d_order.p, W.d_kscratch.p,
                         sstride, W.d_att.p, W.d_kout.p, cubes, s));
     if (const char *path = getenv("LLFE_KM_TRACE")) {  // debug: per-attempt timeline + U
         std::vector<KmeansAttemptOut> att((size_t)n * kAttempts);
@@ -630,6 +634,18 @@ void fill_color_result(const KmeansImageOut &k, llfe_image_result &r) {
 
 bool valid_dims(int n, int h, int w) { return n >= 0 && h > 0 && w > 0 && (int64_t)h * w < (1LL << 31); }
 
+// global indices of images [i0, i0 + n) of a batch: index_base + i, or the caller's list
+// (uploaded on stream s into the workspace)
+int chunk_index(llfe_ctx *ctx, Work &W, const llfe_batch *b, int i0, int n, hipStream_t s, ImgIndex *out) {
+    *out = ImgIndex{b->index_base + i0, nullptr};
+    if (b->indices && n > 0) {
+        HIPCHK(ctx, W.d_index.ensure((size_t)n));
+        HIPCHK(ctx, hipMemcpyAsync(W.d_index.p, b->indices + i0, sizeof(long long) * n, hipMemcpyHostToDevice, s));
+        out->idx = W.d_index.p;
+    }
+    return LLFE_OK;
+}
+
 // Device half of one chunk, on slot `slot`'s stream and workspace: every kernel, then
 // the D2H of the per-image results into host slot `slot`, with events the host half
 // waits on.
@@ -647,6 +663,9 @@ int enqueue_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_
     const int8_t *noise;
     int rc = stage_input(ctx, W, b, i0, n, &img, &noise, s);
     if (rc) return rc;
+    ImgIndex index;
+    rc = chunk_index(ctx, W, b, i0, n, s, &index);
+    if (rc) return rc;
     // single-slot mode: the colour path (unique colours + k-means) runs on the second
     // stream, concurrently with shapes / shadows (both only read the input).  Measured
     // (512 x 1080p): shapes alongside the colour front 13.1k images/s; shapes held back
@@ -661,7 +680,7 @@ int enqueue_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_
     // colour front (unique colours), then shapes / shadows (on the other stream unless
     // held back), then k-means
     if (want_col) {
-        rc = color_stage(ctx, W, img, noise, n, h, w, seed, b->index_base + i0, col_s);
+        rc = color_stage(ctx, W, img, noise, n, h, w, seed, index, col_s);
         if (rc) return rc;
         if (col_s != s && ctx->shapes_after_front) {
             HIPCHK(ctx, hipEventRecord(ctx->front_done, col_s));
@@ -716,7 +735,7 @@ int enqueue_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_
         const KmeansCubes cubes{W.d_cubes.p, std::min<int64_t>(key_stride, kMaxCubes), W.d_ncubes.p,
                                 W.d_pmeta.p + (size_t)2 * n * kParts};
         rc = kmeans_stage(ctx, W, W.d_keys.p, key_stride, W.d_nuniq.p, n, b->n_colors ? b->n_colors : kMaxK, seed,
-                          b->index_base + i0, cubes, col_s);
+                          index, cubes, col_s);
         if (rc) return rc;
         HIPCHK(ctx, ctx->h_kout_s[slot].ensure(n));
         HIPCHK(ctx, hipMemcpyAsync(ctx->h_kout_s[slot].p, W.d_kout.p, sizeof(KmeansImageOut) * n,
@@ -1059,6 +1078,130 @@ int llfe_process_batch(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, ui
     return LLFE_OK;
 }
 
+// Ragged batch: images grouped by (preprocessed) size in input order; each group is
+// packed into a device buffer (2-D copies absorb row strides and host / device sources;
+// images the preprocessing rule resizes go through cv2.resize on the GPU) and runs as
+// ordinary batches that carry every image's own global index.
+int llfe_process_images(llfe_ctx *ctx, const llfe_image_desc *images, int32_t n, uint32_t features,
+                        int32_t preprocessing, int32_t n_colors, uint64_t seed, int64_t index_base,
+                        llfe_image_result *results, llfe_shape *shapes, int64_t shape_capacity,
+                        int64_t *shapes_needed, llfe_stream stream) {
+    if (!ctx || n < 0 || (n > 0 && (!images || !results))) return LLFE_ERR_INVALID;
+    if (preprocessing < LLFE_PRE_NONE || preprocessing > LLFE_PRE_PERFORMANCE)
+        return ctx->fail(LLFE_ERR_INVALID, "preprocessing mode %d", preprocessing);
+    if (n_colors < 0 || n_colors > kMaxColors)
+        return ctx->fail(LLFE_ERR_UNSUPPORTED, "n_colors=%d outside [1, %d]", n_colors, kMaxColors);
+    struct Item {
+        int oh, ow, interp;
+        bool resize;
+    };
+    std::vector<Item> it((size_t)n);
+    const bool with_noise = n > 0 && images[0].noise;
+    for (int i = 0; i < n; i++) {
+        const llfe_image_desc &d = images[i];
+        if (!d.data || !valid_dims(1, d.height, d.width) ||
+            (d.row_stride != 0 && d.row_stride < 3 * (int64_t)d.width))
+            return ctx->fail(LLFE_ERR_INVALID, "image %d: invalid descriptor (%d x %d, stride %lld)", i, d.height,
+                             d.width, (long long)d.row_stride);
+        if ((d.noise != nullptr) != with_noise)
+            return ctx->fail(LLFE_ERR_INVALID, "parity noise must be given for every image or for none");
+        Item &q = it[i];
+        int ow = d.width, oh = d.height, interp = 0;
+        const int r = llfe_preprocess_size(d.width, d.height, preprocessing, &ow, &oh, &interp);
+        if (r < 0) return ctx->fail(LLFE_ERR_INVALID, "image %d: preprocessing size", i);
+        q = Item{r ? oh : d.height, r ? ow : d.width, interp, r == 1};
+    }
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = (hipStream_t)stream;
+    // size groups, in order of first appearance; members in input order
+    std::vector<std::pair<std::pair<int, int>, std::vector<int>>> groups;
+    {
+        std::map<std::pair<int, int>, size_t> gi;
+        for (int i = 0; i < n; i++) {
+            const auto key = std::make_pair(it[i].oh, it[i].ow);
+            auto f = gi.find(key);
+            if (f == gi.end()) {
+                gi[key] = groups.size();
+                groups.push_back({key, {i}});
+            } else {
+                groups[f->second].second.push_back(i);
+            }
+        }
+    }
+    const bool want_shp = features & LLFE_FEATURE_SHAPES;
+    int64_t total_shapes = 0;
+    bool short_cap = false;
+    std::vector<llfe_image_result> res;
+    std::vector<int64_t> gidx;
+    for (const auto &g : groups) {
+        const int oh = g.first.first, ow = g.first.second;
+        const int64_t P3 = (int64_t)oh * ow * 3;
+        // staging passes of at most two device chunks (the batch path pipelines them)
+        const int per = std::max(1, 2 * chunk_for(ctx->chunk, oh, ow));
+        for (size_t a = 0; a < g.second.size(); a += per) {
+            const int nb = (int)std::min<size_t>(per, g.second.size() - a);
+            HIPCHK(ctx, ctx->d_ragged.ensure((size_t)nb * P3));
+            if (with_noise) HIPCHK(ctx, ctx->d_ragged_noise.ensure((size_t)nb * P3));
+            gidx.resize(nb);
+            for (int j = 0; j < nb; j++) {
+                const int i = g.second[a + j];
+                const llfe_image_desc &d = images[i];
+                gidx[j] = index_base + i;
+                const size_t pitch = d.row_stride ? (size_t)d.row_stride : (size_t)d.width * 3;
+                const hipMemcpyKind kind = d.on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+                uint8_t *dst = ctx->d_ragged.p + (size_t)j * P3;
+                if (!it[i].resize) {
+                    HIPCHK(ctx, hipMemcpy2DAsync(dst, (size_t)ow * 3, d.data, pitch, (size_t)d.width * 3, d.height,
+                                                 kind, s));
+                } else {
+                    HIPCHK(ctx, ctx->d_rsz_src.ensure((size_t)d.height * d.width * 3));
+                    HIPCHK(ctx, hipMemcpy2DAsync(ctx->d_rsz_src.p, (size_t)d.width * 3, d.data, pitch,
+                                                 (size_t)d.width * 3, d.height, kind, s));
+                    const int rc = llfe_resize_cv(ctx, ctx->d_rsz_src.p, d.height, d.width, 3, dst, oh, ow,
+                                                  it[i].interp, stream);
+                    if (rc) return rc;
+                }
+                if (with_noise)
+                    HIPCHK(ctx, hipMemcpyAsync(ctx->d_ragged_noise.p + (size_t)j * P3, d.noise, (size_t)P3,
+                                               d.noise_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
+            }
+            llfe_batch bb{};
+            bb.data = ctx->d_ragged.p;
+            bb.n = nb;
+            bb.height = oh;
+            bb.width = ow;
+            bb.on_device = 1;
+            bb.noise = with_noise ? ctx->d_ragged_noise.p : nullptr;
+            bb.noise_on_device = 1;
+            bb.n_colors = n_colors;
+            bb.index_base = index_base;
+            bb.indices = gidx.data();
+            res.assign((size_t)nb, llfe_image_result{});
+            const int64_t left = std::max<int64_t>(0, shape_capacity - total_shapes);
+            int64_t need = 0;
+            const int rc = llfe_process_batch(ctx, &bb, features, seed, res.data(),
+                                              shapes && left > 0 ? shapes + total_shapes : nullptr, left, &need,
+                                              stream);
+            if (rc == LLFE_ERR_CAPACITY) {
+                short_cap = true;  // results are valid; keep counting what is needed
+            } else if (rc) {
+                return rc;
+            }
+            for (int j = 0; j < nb; j++) {
+                llfe_image_result r = res[j];
+                r.shape_offset += total_shapes;
+                results[g.second[a + j]] = r;
+            }
+            total_shapes += need;
+        }
+    }
+    if (shapes_needed) *shapes_needed = total_shapes;
+    if (want_shp && (short_cap || total_shapes > shape_capacity))
+        return ctx->fail(LLFE_ERR_CAPACITY, "shape capacity %lld < %lld", (long long)shape_capacity,
+                         (long long)total_shapes);
+    return LLFE_OK;
+}
+
 // Asynchronous form of llfe_process_batch: up to two batches in flight, each on its own
 // workspace and stream pair, so batch k + 1's unique-colour and stencil kernels start in
 // the tail of batch k's k-means launch (where most CUs are idle) instead of after it.
@@ -1200,7 +1343,10 @@ int llfe_color_unique(llfe_ctx *ctx, const llfe_batch *b, uint64_t seed, uint32_
     const int8_t *noise;
     int rc = stage_input(ctx, W, b, 0, n, &img, &noise, s);
     if (rc) return rc;
-    rc = color_stage(ctx, W, img, noise, n, h, w, seed, b->index_base, s);
+    ImgIndex index;
+    rc = chunk_index(ctx, W, b, 0, n, s, &index);
+    if (rc) return rc;
+    rc = color_stage(ctx, W, img, noise, n, h, w, seed, index, s);
     if (rc) return rc;
     HIPCHK(ctx, hipMemcpy2DAsync(keys, sizeof(uint32_t) * P, W.d_keys.p, sizeof(uint32_t) * key_stride,
                                  sizeof(uint32_t) * P, n, hipMemcpyDeviceToDevice, s));
@@ -1224,7 +1370,7 @@ int llfe_kmeans(llfe_ctx *ctx, const uint32_t *keys, int64_t key_stride, const i
     HIPCHK(ctx, W.d_nuniq.ensure(n));
     HIPCHK(ctx, hipMemcpyAsync(W.d_nuniq.p, n_points, sizeof(int64_t) * n, hipMemcpyHostToDevice, s));
     const KmeansCubes none{nullptr, 0, nullptr, nullptr};  // plain sweeps over caller-supplied keys
-    int rc = kmeans_stage(ctx, W, keys, key_stride, W.d_nuniq.p, n, n_colors, seed, index_base, none, s);
+    int rc = kmeans_stage(ctx, W, keys, key_stride, W.d_nuniq.p, n, n_colors, seed, ImgIndex{index_base, nullptr}, none, s);
     if (rc) return rc;
     HIPCHK(ctx, ctx->h_kout.ensure(n));
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_kout.p, W.d_kout.p, sizeof(KmeansImageOut) * n, hipMemcpyDeviceToHost, s));

@@ -116,6 +116,16 @@ inline size_t stencil_parts(int n, int h, int w) {
     return a > b ? a : b;
 }
 
+// Global index of image i of a launch (per-image noise streams and k-means seeds, so
+// results do not depend on batching): base + i, or idx[i] (device) when a ragged batch
+// or a caller's index list gives images non-consecutive indices.
+struct ImgIndex {
+    long long base;
+    const long long *idx;
+    __host__ __device__ long long at(int i) const { return idx ? idx[i] : base + i; }
+    ImgIndex shifted(int i0) const { return ImgIndex{base + i0, idx ? idx + i0 : nullptr}; }
+};
+
 // ---------------------------------------------------------------- colours
 constexpr int kMaxK = 5;                     // the cube-table k-means (n_colors <= 5)
 constexpr int kMaxColors = LLFE_MAX_COLORS;  // the generic k-means (k_kmeans_big) up to this
@@ -177,7 +187,7 @@ struct KmeansCubes {
 //   gather:  contiguous sorted keys -> `keys` (may alias part), cube table -> `cubes`,
 //            n_unique, n_cubes
 hipError_t launch_uq_keys(const uint8_t *bgr, const int8_t *noise, int n, int h, int w, uint64_t seed,
-                          int64_t index_base, int64_t key_stride, uint32_t *raw, uint32_t *hist, hipStream_t s);
+                          ImgIndex index, int64_t key_stride, uint32_t *raw, uint32_t *hist, hipStream_t s);
 hipError_t launch_uq_scatter(const uint32_t *raw, int n, int64_t P, int64_t key_stride, const uint32_t *hist,
                              uint32_t *cursor, uint32_t *part, hipStream_t s);
 hipError_t launch_uq_part(const uint32_t *part, int n, int64_t key_stride, const uint32_t *hist, uint32_t *skeys,
@@ -188,15 +198,15 @@ hipError_t launch_uq_gather(const uint32_t *skeys, int n, int64_t key_stride, co
 
 // per image: K = min(n_colors, U); attempts run as separate workgroups
 // (ordered largest U first), then a finalize kernel picks the best attempt.
-// cv::RNG state of image i = splitmix64(seed + index_base + i), 0 -> 0xffffffff
+// cv::RNG state of image i = splitmix64(seed + index.at(i)), 0 -> 0xffffffff
 hipError_t launch_kmeans(const uint32_t *keys, int64_t key_stride, const int64_t *n_unique, int n, int n_colors,
-                         uint64_t seed, int64_t index_base, int32_t *order, uint32_t *scratch, int64_t scratch_stride,
+                         uint64_t seed, ImgIndex index, int32_t *order, uint32_t *scratch, int64_t scratch_stride,
                          KmeansAttemptOut *attempts, KmeansImageOut *out, const KmeansCubes &cubes,
                          hipStream_t s);
 // K in (kMaxK, kMaxColors]: the general-K attempts (kmeans_big.hip) in the order of
 // k_kmeans_order, into the same attempt records (launch_kmeans calls it)
 hipError_t launch_kmeans_big(const uint32_t *keys, int64_t key_stride, const int64_t *n_unique, int n, int n_colors,
-                             uint64_t seed, int64_t index_base, const int32_t *order, uint32_t *scratch,
+                             uint64_t seed, ImgIndex index, const int32_t *order, uint32_t *scratch,
                              int64_t scratch_stride, KmeansAttemptOut *attempts, hipStream_t s);
 // u32 scratch per (image, attempt) for k-means++ step sums
 int64_t kmeans_scratch_stride(int64_t key_stride);

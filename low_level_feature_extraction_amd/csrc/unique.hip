@@ -66,14 +66,14 @@ __device__ __forceinline__ uint32_t key_of(int b, int g, int r, int nb, int ng, 
 // (counter-based: two 32-bit hashes of (image stream, pixel) -> three 21-bit uniforms).
 __global__ __launch_bounds__(KB) void k_uq_keys(const uint8_t *__restrict__ bgr, const int8_t *__restrict__ noise,
                                                 long long P, long long key_stride, unsigned long long seed,
-                                                long long index_base, uint32_t *__restrict__ keys,
+                                                ImgIndex index, uint32_t *__restrict__ keys,
                                                 uint32_t *__restrict__ hist) {
     __shared__ uint32_t lh[NPART];
     const int img = blockIdx.y;
     const uint8_t *src = bgr + (size_t)img * P * 3;
     const int8_t *nz = noise ? noise + (size_t)img * P * 3 : nullptr;
     uint32_t *out = keys + (size_t)img * key_stride;
-    const uint64_t stream = mix64(seed ^ mix64((uint64_t)(index_base + img) + 0x4C4C46454C4C4645ull));
+    const uint64_t stream = mix64(seed ^ mix64((uint64_t)index.at(img) + 0x4C4C46454C4C4645ull));
     if (threadIdx.x < NPART) lh[threadIdx.x] = 0;
     __syncthreads();
     const long long nchunks = (P + PPT - 1) / PPT;
@@ -442,13 +442,13 @@ __global__ __launch_bounds__(GT) void k_uq_gather(const uint32_t *__restrict__ s
 }  // namespace
 
 hipError_t launch_uq_keys(const uint8_t *bgr, const int8_t *noise, int n, int h, int w, uint64_t seed,
-                          int64_t index_base, int64_t key_stride, uint32_t *keys, uint32_t *hist, hipStream_t s) {
+                          ImgIndex index, int64_t key_stride, uint32_t *keys, uint32_t *hist, hipStream_t s) {
     const long long P = (long long)h * w;
     const long long per_block = (long long)KB * PPT * 4;
     int bx = (int)std::min((P + per_block - 1) / per_block, 2048LL);
     if (bx < 1) bx = 1;
     hipLaunchKernelGGL(k_uq_keys, dim3(bx, n), dim3(KB), 0, s, bgr, noise, P, (long long)key_stride,
-                       (unsigned long long)seed, (long long)index_base, keys, hist);
+                       (unsigned long long)seed, index, keys, hist);
     return hipGetLastError();
 }
 

@@ -11,7 +11,6 @@ per-image calls return:
 """
 from __future__ import annotations
 
-from collections import defaultdict
 from typing import Iterable, List, Optional, Sequence
 
 import numpy as np
@@ -53,11 +52,12 @@ def assemble(r, features: Iterable[str]) -> dict:
 
 def run_batch(images, features: Sequence[str] = ("colors", "shapes", "shadows"), seed: Optional[int] = None,
               noise=None, backend: Optional[Backend] = None, raw: bool = False, n_colors: int = 5,
-              index_base: Optional[int] = None) -> List[dict]:
+              index_base: Optional[int] = None, preprocessing: str = "none") -> List[dict]:
     """images: N x H x W x 3 BGR uint8 array / torch tensor, or a list of H x W x 3
     arrays of any sizes.  Returns one dict per image, in input order.  ``index_base``
     fixes the global index of image 0 (the per-image noise / k-means seeds); by default
-    the process counter hands out fresh indices."""
+    the process counter hands out fresh indices.  ``preprocessing`` (lists only):
+    validate_and_preprocess_image's resize mode, applied on the GPU before the features."""
     from . import color_extractor as ce
 
     be = backend or Backend.get()
@@ -70,30 +70,17 @@ def run_batch(images, features: Sequence[str] = ("colors", "shapes", "shadows"),
         base = ce._next_index(n) if index_base is None else int(index_base)
         res = be.process(images, feats, seed=seed, noise=noise, index_base=base, n_colors=n_colors)
         return res if raw else [assemble(r, feats) for r in res]
-    imgs = [np.ascontiguousarray(np.asarray(im, np.uint8)) for im in images]
+    # a list of images of any sizes: one ragged llfe_process_images call (size groups
+    # share device passes; every image keeps its own global index)
+    imgs = [im if hasattr(im, "data_ptr") else np.asarray(im, np.uint8) for im in images]
     for im in imgs:
-        if im.ndim != 3 or im.shape[2] != 3:
-            raise ValueError(f"expected H x W x 3 BGR uint8 images, got {im.shape}")
+        if len(im.shape) != 3 or im.shape[2] != 3:
+            raise ValueError(f"expected H x W x 3 BGR uint8 images, got {tuple(im.shape)}")
     base = ce._next_index(len(imgs)) if index_base is None else int(index_base)
-    groups = defaultdict(list)
-    for i, im in enumerate(imgs):
-        groups[im.shape[:2]].append(i)
-    out: List[Optional[dict]] = [None] * len(imgs)
-    for (h, w), idx in groups.items():
-        batch = np.stack([imgs[i] for i in idx])
-        nz = None
-        if noise is not None:
-            nz = np.stack([np.asarray(noise[i], np.int8).reshape(h * w, 3) for i in idx])
-        # every image keeps its own global index, so results do not depend on grouping:
-        # one launch per run of consecutive indices
-        runs, start = [], 0
-        for j in range(1, len(idx) + 1):
-            if j == len(idx) or idx[j] != idx[j - 1] + 1:
-                runs.append((start, j))
-                start = j
-        for a, b in runs:
-            res = be.process(batch[a:b], feats, seed=seed, noise=None if nz is None else nz[a:b],
-                             index_base=base + idx[a], n_colors=n_colors)
-            for j, r in zip(range(a, b), res):
-                out[idx[j]] = r if raw else assemble(r, feats)
+    nz = None
+    if noise is not None:
+        nz = [np.asarray(noise[i], np.int8).reshape(-1, 3) for i in range(len(imgs))]
+    res = be.process_images(imgs, feats, seed=seed, noise=nz, index_base=base, n_colors=n_colors,
+                            preprocessing=preprocessing)
+    out = res if raw else [assemble(r, feats) for r in res]
     return out  # type: ignore[return-value]
