@@ -257,6 +257,11 @@ int llfe_thumbnail_size(int32_t w, int32_t h, int32_t max_w, int32_t max_h, int3
 int llfe_thumbnail_pil(llfe_ctx *ctx, const uint8_t *src, int32_t h, int32_t w, int32_t ch, int32_t max_w,
                        int32_t max_h, uint8_t *dst, int64_t dst_capacity, int32_t *out_h, int32_t *out_w,
                        llfe_stream stream);
+/* the same for n same-size device images packed n x h x w x ch -> n x out_h x out_w x ch
+ * (ImageProcessor.auto_process_image over a batch: one launch sequence per pass) */
+int llfe_thumbnail_pil_batch(llfe_ctx *ctx, const uint8_t *src, int32_t n, int32_t h, int32_t w, int32_t ch,
+                             int32_t max_w, int32_t max_h, uint8_t *dst, int64_t dst_capacity, int32_t *out_h,
+                             int32_t *out_w, llfe_stream stream);
 /* host-side external contours (findContours RETR_EXTERNAL/CHAIN_APPROX_SIMPLE,
  * shape pyc @L140) on a host u8 mask; points x,y pairs; offsets[n_contours+1].
  * Returns the number of contours, or LLFE_ERR_CAPACITY with *needed_points set. */

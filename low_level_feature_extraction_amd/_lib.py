@@ -136,6 +136,8 @@ SIGNATURES = {
                                        C.POINTER(C.c_int32)]),
     "llfe_thumbnail_pil": (C.c_int, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _i64, C.POINTER(C.c_int32),
                                      C.POINTER(C.c_int32), _vp]),
+    "llfe_thumbnail_pil_batch": (C.c_int, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _i64,
+                                           C.POINTER(C.c_int32), C.POINTER(C.c_int32), _vp]),
     "llfe_find_contours":(C.c_int, [_vp, _i32, _i32, _vp, _i64, _vp, _i32, C.POINTER(C.c_int64)]),
     "llfe_border_radius": (C.c_double, [_vp, _i32, C.c_double]),
     "llfe_classify_contour": (C.c_int, [_vp, _i32, C.POINTER(LlfeShape)]),

@@ -509,6 +509,22 @@ class Backend:
         out = out[: oh.value * ow.value * ch].view(oh.value, ow.value, ch)
         return out[:, :, 0] if squeeze else out
 
+    def thumbnail_pil_batch(self, images, max_w=1920, max_h=1080):
+        """PIL thumbnail((max_w, max_h), LANCZOS) of N same-size H x W x 3 uint8 images
+        (N x H x W x 3 array / tensor) in one llfe_thumbnail_pil_batch call."""
+        torch = _torch()
+        x = images if _is_torch(images) else torch.from_numpy(np.ascontiguousarray(images, np.uint8))
+        x = x.to(f"cuda:{self.device}").contiguous()
+        n, h, w, ch = x.shape
+        plan = thumbnail_size(w, h, max_w, max_h)
+        ow, oh = plan if plan else (w, h)
+        out = torch.empty((n, oh, ow, ch), dtype=torch.uint8, device=x.device)
+        ro, co = C.c_int32(0), C.c_int32(0)
+        self._chk(self._lib.llfe_thumbnail_pil_batch(self.ctx, x.data_ptr(), n, h, w, ch, max_w, max_h, out.data_ptr(),
+                                                     out.numel(), C.byref(ro), C.byref(co), self._stream(x)))
+        assert (ro.value, co.value) == (oh, ow)
+        return out
+
 
 CV_INTER = {"linear": 1, "area": 3, "lanczos4": 4}
 PRE_MODES = {"none": 0, "auto": 1, "high_quality": 2, "performance": 3}

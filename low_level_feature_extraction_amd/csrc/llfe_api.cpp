@@ -1382,11 +1382,10 @@ int llfe_kmeans(llfe_ctx *ctx, const uint32_t *keys, int64_t key_stride, const i
     return LLFE_OK;
 }
 
-int llfe_resize_lanczos_pil(llfe_ctx *ctx, const uint8_t *src, int32_t h, int32_t w, int32_t ch, uint8_t *dst,
-                            int32_t out_h, int32_t out_w, const double *box, llfe_stream stream) {
-    if (!ctx || !src || !dst || h <= 0 || w <= 0 || ch <= 0 || out_h <= 0 || out_w <= 0) return LLFE_ERR_INVALID;
-    HIPCHK(ctx, hipSetDevice(ctx->device));
-    hipStream_t s = (hipStream_t)stream;
+namespace {
+// Image.resize(size, LANCZOS, box) of n same-size packed device images
+int resize_lanczos_n(llfe_ctx *ctx, const uint8_t *src, int n, int32_t h, int32_t w, int32_t ch, uint8_t *dst,
+                     int32_t out_h, int32_t out_w, const double *box, hipStream_t s) {
     double bx0 = box ? box[0] : 0, by0 = box ? box[1] : 0, bx1 = box ? box[2] : w, by1 = box ? box[3] : h;
     bool need_h = out_w != w || bx0 != 0 || bx1 != out_w;
     bool need_v = out_h != h || by0 != 0 || by1 != out_h;
@@ -1407,20 +1406,64 @@ int llfe_resize_lanczos_pil(llfe_ctx *ctx, const uint8_t *src, int32_t h, int32_
     all.insert(all.end(), kv.begin(), kv.end());
     HIPCHK(ctx, hipMemcpyAsync(ctx->d_coef.p, all.data(), nb * sizeof(int32_t), hipMemcpyHostToDevice, s));
     const int32_t *dbh = ctx->d_coef.p, *dkh = dbh + bh.size(), *dbv = dkh + kh.size(), *dkv = dbv + bv.size();
+    const long long in_img = (long long)h * w * ch, out_img = (long long)out_h * out_w * ch;
     if (!need_h && !need_v) {
-        HIPCHK(ctx, hipMemcpyAsync(dst, src, (size_t)h * w * ch, hipMemcpyDeviceToDevice, s));
+        HIPCHK(ctx, hipMemcpyAsync(dst, src, (size_t)n * in_img, hipMemcpyDeviceToDevice, s));
     } else if (need_h && !need_v) {
-        HIPCHK(ctx, launch_resize_h(src, h, w, ch, yfirst, ylast - yfirst, dst, out_w, dbh, dkh, ksh, s));
+        HIPCHK(ctx, launch_resize_h(src, h, w, ch, yfirst, ylast - yfirst, dst, out_w, dbh, dkh, ksh, s, n, in_img,
+                                    out_img));
     } else if (!need_h) {
-        HIPCHK(ctx, launch_resize_v(src, w, ch, dst, out_h, dbv, dkv, ksv, s));
+        HIPCHK(ctx, launch_resize_v(src, w, ch, dst, out_h, dbv, dkv, ksv, s, n, in_img, out_img));
     } else {
         const int rows = ylast - yfirst;
-        HIPCHK(ctx, ctx->d_rsz_tmp.ensure((size_t)rows * out_w * ch));
-        HIPCHK(ctx, launch_resize_h(src, h, w, ch, yfirst, rows, ctx->d_rsz_tmp.p, out_w, dbh, dkh, ksh, s));
-        HIPCHK(ctx, launch_resize_v(ctx->d_rsz_tmp.p, out_w, ch, dst, out_h, dbv, dkv, ksv, s));
+        const long long tmp_img = (long long)rows * out_w * ch;
+        HIPCHK(ctx, ctx->d_rsz_tmp.ensure((size_t)n * tmp_img));
+        HIPCHK(ctx, launch_resize_h(src, h, w, ch, yfirst, rows, ctx->d_rsz_tmp.p, out_w, dbh, dkh, ksh, s, n, in_img,
+                                    tmp_img));
+        HIPCHK(ctx, launch_resize_v(ctx->d_rsz_tmp.p, out_w, ch, dst, out_h, dbv, dkv, ksv, s, n, tmp_img, out_img));
     }
     HIPCHK(ctx, hipStreamSynchronize(s));  // host coefficient vectors die here
     return LLFE_OK;
+}
+
+// thumbnail((max_w, max_h), LANCZOS) incl. the reducing_gap=2.0 reduce() pre-pass, n images
+int thumbnail_n(llfe_ctx *ctx, const uint8_t *src, int n, int32_t h, int32_t w, int32_t ch, int32_t max_w,
+                int32_t max_h, uint8_t *dst, int64_t dst_capacity, int32_t *out_h, int32_t *out_w, hipStream_t s) {
+    int32_t ow, oh;
+    int rc = llfe_thumbnail_size(w, h, max_w, max_h, &ow, &oh);
+    if (rc < 0) return ctx->fail(rc, "invalid thumbnail geometry");
+    if ((int64_t)n * ow * oh * ch > dst_capacity) return ctx->fail(LLFE_ERR_CAPACITY, "thumbnail dst too small");
+    *out_w = ow;
+    *out_h = oh;
+    if (rc == 0) {
+        HIPCHK(ctx, hipMemcpyAsync(dst, src, (size_t)n * h * w * ch, hipMemcpyDeviceToDevice, s));
+        HIPCHK(ctx, hipStreamSynchronize(s));
+        return LLFE_OK;
+    }
+    // Image.resize(size, LANCZOS, box=None, reducing_gap=2.0)
+    const double gap = 2.0;
+    int fx = (int)((double)w / ow / gap), fy = (int)((double)h / oh / gap);
+    if (fx < 1) fx = 1;
+    if (fy < 1) fy = 1;
+    if (fx > 1 || fy > 1) {
+        // _get_safe_box of the full image is the full image itself
+        const int rw = (w + fx - 1) / fx, rh = (h + fy - 1) / fy;
+        const long long red_img = (long long)rw * rh * ch;
+        HIPCHK(ctx, ctx->d_rsz_src.ensure((size_t)n * red_img));
+        HIPCHK(ctx, launch_reduce(src, w, ch, 0, 0, w, h, fx, fy, ctx->d_rsz_src.p, rw, rh, s, n,
+                                  (long long)h * w * ch, red_img));
+        const double box[4] = {0.0, 0.0, (double)w / fx, (double)h / fy};
+        return resize_lanczos_n(ctx, ctx->d_rsz_src.p, n, rh, rw, ch, dst, oh, ow, box, s);
+    }
+    return resize_lanczos_n(ctx, src, n, h, w, ch, dst, oh, ow, nullptr, s);
+}
+}  // namespace
+
+int llfe_resize_lanczos_pil(llfe_ctx *ctx, const uint8_t *src, int32_t h, int32_t w, int32_t ch, uint8_t *dst,
+                            int32_t out_h, int32_t out_w, const double *box, llfe_stream stream) {
+    if (!ctx || !src || !dst || h <= 0 || w <= 0 || ch <= 0 || out_h <= 0 || out_w <= 0) return LLFE_ERR_INVALID;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    return resize_lanczos_n(ctx, src, 1, h, w, ch, dst, out_h, out_w, box, (hipStream_t)stream);
 }
 
 // PIL Image.thumbnail's preserve_aspect_ratio (Python float semantics).  Returns 1
@@ -1455,33 +1498,18 @@ int llfe_thumbnail_pil(llfe_ctx *ctx, const uint8_t *src, int32_t h, int32_t w, 
                        int32_t max_h, uint8_t *dst, int64_t dst_capacity, int32_t *out_h, int32_t *out_w,
                        llfe_stream stream) {
     if (!ctx || !src || !dst || !out_h || !out_w || ch <= 0) return LLFE_ERR_INVALID;
-    int32_t ow, oh;
-    int rc = llfe_thumbnail_size(w, h, max_w, max_h, &ow, &oh);
-    if (rc < 0) return ctx->fail(rc, "invalid thumbnail geometry");
-    if ((int64_t)ow * oh * ch > dst_capacity) return ctx->fail(LLFE_ERR_CAPACITY, "thumbnail dst too small");
-    *out_w = ow;
-    *out_h = oh;
     HIPCHK(ctx, hipSetDevice(ctx->device));
-    hipStream_t s = (hipStream_t)stream;
-    if (rc == 0) {
-        HIPCHK(ctx, hipMemcpyAsync(dst, src, (size_t)h * w * ch, hipMemcpyDeviceToDevice, s));
-        HIPCHK(ctx, hipStreamSynchronize(s));
-        return LLFE_OK;
-    }
-    // Image.resize(size, LANCZOS, box=None, reducing_gap=2.0)
-    const double gap = 2.0;
-    int fx = (int)((double)w / ow / gap), fy = (int)((double)h / oh / gap);
-    if (fx < 1) fx = 1;
-    if (fy < 1) fy = 1;
-    if (fx > 1 || fy > 1) {
-        // _get_safe_box of the full image is the full image itself
-        const int rw = (w + fx - 1) / fx, rh = (h + fy - 1) / fy;
-        HIPCHK(ctx, ctx->d_rsz_src.ensure((size_t)rw * rh * ch));
-        HIPCHK(ctx, launch_reduce(src, w, ch, 0, 0, w, h, fx, fy, ctx->d_rsz_src.p, rw, rh, s));
-        const double box[4] = {0.0, 0.0, (double)w / fx, (double)h / fy};
-        return llfe_resize_lanczos_pil(ctx, ctx->d_rsz_src.p, rh, rw, ch, dst, oh, ow, box, stream);
-    }
-    return llfe_resize_lanczos_pil(ctx, src, h, w, ch, dst, oh, ow, nullptr, stream);
+    return thumbnail_n(ctx, src, 1, h, w, ch, max_w, max_h, dst, dst_capacity, out_h, out_w, (hipStream_t)stream);
+}
+
+int llfe_thumbnail_pil_batch(llfe_ctx *ctx, const uint8_t *src, int32_t n, int32_t h, int32_t w, int32_t ch,
+                             int32_t max_w, int32_t max_h, uint8_t *dst, int64_t dst_capacity, int32_t *out_h,
+                             int32_t *out_w, llfe_stream stream) {
+    if (!ctx || n < 0 || (n > 0 && (!src || !dst)) || !out_h || !out_w || ch <= 0 || n > 65535)
+        return LLFE_ERR_INVALID;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    if (n == 0) return llfe_thumbnail_size(w, h, max_w, max_h, out_w, out_h) < 0 ? LLFE_ERR_INVALID : LLFE_OK;
+    return thumbnail_n(ctx, src, n, h, w, ch, max_w, max_h, dst, dst_capacity, out_h, out_w, (hipStream_t)stream);
 }
 
 // cv2.resize (validate_and_preprocess_image, utils.py:118-143); tables built on the host

@@ -213,12 +213,16 @@ int64_t kmeans_scratch_stride(int64_t key_stride);
 constexpr int kMaxKmeansBatch = 4096;
 
 // ---------------------------------------------------------------- resize
+// Pillow LANCZOS / reduce (resize.hip) on n same-size images, src_img / dst_img bytes apart
 hipError_t launch_resize_h(const uint8_t *src, int src_h, int src_w, int ch, int row0, int rows, uint8_t *dst,
-                           int out_w, const int32_t *bounds, const int32_t *coeffs, int ksize, hipStream_t s);
+                           int out_w, const int32_t *bounds, const int32_t *coeffs, int ksize, hipStream_t s,
+                           int n = 1, long long src_img = 0, long long dst_img = 0);
 hipError_t launch_resize_v(const uint8_t *src, int src_w, int ch, uint8_t *dst, int out_h, const int32_t *bounds,
-                           const int32_t *coeffs, int ksize, hipStream_t s);
+                           const int32_t *coeffs, int ksize, hipStream_t s, int n = 1, long long src_img = 0,
+                           long long dst_img = 0);
 hipError_t launch_reduce(const uint8_t *src, int src_w, int ch, int x0, int y0, int x1, int y1, int fx, int fy,
-                         uint8_t *dst, int out_w, int out_h, hipStream_t s);
+                         uint8_t *dst, int out_w, int out_h, hipStream_t s, int n = 1, long long src_img = 0,
+                         long long dst_img = 0);
 
 // cv2.resize for the preprocessing modes (cvresize.hip); OpenCV interpolation codes
 constexpr int kCvInterLinear = 1, kCvInterArea = 3, kCvInterLanczos4 = 4;

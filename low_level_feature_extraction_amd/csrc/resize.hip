@@ -19,11 +19,15 @@ __device__ __forceinline__ uint8_t clip8(int v) {
     return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
 }
 
+// (blockIdx.z: image of a same-size batch; src_img / dst_img: bytes between images)
 __global__ __launch_bounds__(RT) void k_resize_h(const uint8_t *__restrict__ src, int src_w, int ch, int row0,
                                                  uint8_t *__restrict__ dst, int out_w,
                                                  const int32_t *__restrict__ bounds,
-                                                 const int32_t *__restrict__ coeffs, int ksize) {
+                                                 const int32_t *__restrict__ coeffs, int ksize, long long src_img,
+                                                 long long dst_img) {
     const int yy = blockIdx.y;
+    src += (size_t)blockIdx.z * src_img;
+    dst += (size_t)blockIdx.z * dst_img;
     const int i = blockIdx.x * RT + threadIdx.x;
     if (i >= out_w * ch) return;
     const int xx = i / ch, c = i - xx * ch;
@@ -37,8 +41,11 @@ __global__ __launch_bounds__(RT) void k_resize_h(const uint8_t *__restrict__ src
 
 __global__ __launch_bounds__(RT) void k_resize_v(const uint8_t *__restrict__ src, int src_w, int ch,
                                                  uint8_t *__restrict__ dst, const int32_t *__restrict__ bounds,
-                                                 const int32_t *__restrict__ coeffs, int ksize) {
+                                                 const int32_t *__restrict__ coeffs, int ksize, long long src_img,
+                                                 long long dst_img) {
     const int yy = blockIdx.y;
+    src += (size_t)blockIdx.z * src_img;
+    dst += (size_t)blockIdx.z * dst_img;
     const int i = blockIdx.x * RT + threadIdx.x;
     const int rowlen = src_w * ch;
     if (i >= rowlen) return;
@@ -55,8 +62,11 @@ __global__ __launch_bounds__(RT) void k_resize_v(const uint8_t *__restrict__ src
 // clipped) box; used by thumbnail(..., reducing_gap=2.0) when the input is >= 4x the
 // target in a dimension.
 __global__ __launch_bounds__(RT) void k_reduce(const uint8_t *__restrict__ src, int src_w, int ch, int x0, int y0,
-                                               int x1, int y1, int fx, int fy, uint8_t *__restrict__ dst, int out_w) {
+                                               int x1, int y1, int fx, int fy, uint8_t *__restrict__ dst, int out_w,
+                                               long long src_img, long long dst_img) {
     const int yy = blockIdx.y;
+    src += (size_t)blockIdx.z * src_img;
+    dst += (size_t)blockIdx.z * dst_img;
     const int i = blockIdx.x * RT + threadIdx.x;
     if (i >= out_w * ch) return;
     const int xx = i / ch, c = i - xx * ch;
@@ -73,24 +83,30 @@ __global__ __launch_bounds__(RT) void k_reduce(const uint8_t *__restrict__ src, 
 }  // namespace
 
 hipError_t launch_reduce(const uint8_t *src, int src_w, int ch, int x0, int y0, int x1, int y1, int fx, int fy,
-                         uint8_t *dst, int out_w, int out_h, hipStream_t s) {
-    dim3 grid((out_w * ch + RT - 1) / RT, out_h);
-    hipLaunchKernelGGL(k_reduce, grid, dim3(RT), 0, s, src, src_w, ch, x0, y0, x1, y1, fx, fy, dst, out_w);
+                         uint8_t *dst, int out_w, int out_h, hipStream_t s, int n, long long src_img,
+                         long long dst_img) {
+    dim3 grid((out_w * ch + RT - 1) / RT, out_h, n);
+    hipLaunchKernelGGL(k_reduce, grid, dim3(RT), 0, s, src, src_w, ch, x0, y0, x1, y1, fx, fy, dst, out_w, src_img,
+                       dst_img);
     return hipGetLastError();
 }
 
 hipError_t launch_resize_h(const uint8_t *src, int src_h, int src_w, int ch, int row0, int rows, uint8_t *dst,
-                           int out_w, const int32_t *bounds, const int32_t *coeffs, int ksize, hipStream_t s) {
+                           int out_w, const int32_t *bounds, const int32_t *coeffs, int ksize, hipStream_t s, int n,
+                           long long src_img, long long dst_img) {
     (void)src_h;
-    dim3 grid((out_w * ch + RT - 1) / RT, rows);
-    hipLaunchKernelGGL(k_resize_h, grid, dim3(RT), 0, s, src, src_w, ch, row0, dst, out_w, bounds, coeffs, ksize);
+    dim3 grid((out_w * ch + RT - 1) / RT, rows, n);
+    hipLaunchKernelGGL(k_resize_h, grid, dim3(RT), 0, s, src, src_w, ch, row0, dst, out_w, bounds, coeffs, ksize,
+                       src_img, dst_img);
     return hipGetLastError();
 }
 
 hipError_t launch_resize_v(const uint8_t *src, int src_w, int ch, uint8_t *dst, int out_h, const int32_t *bounds,
-                           const int32_t *coeffs, int ksize, hipStream_t s) {
-    dim3 grid((src_w * ch + RT - 1) / RT, out_h);
-    hipLaunchKernelGGL(k_resize_v, grid, dim3(RT), 0, s, src, src_w, ch, dst, bounds, coeffs, ksize);
+                           const int32_t *coeffs, int ksize, hipStream_t s, int n, long long src_img,
+                           long long dst_img) {
+    dim3 grid((src_w * ch + RT - 1) / RT, out_h, n);
+    hipLaunchKernelGGL(k_resize_v, grid, dim3(RT), 0, s, src, src_w, ch, dst, bounds, coeffs, ksize, src_img,
+                       dst_img);
     return hipGetLastError();
 }
 

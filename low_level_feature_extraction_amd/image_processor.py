@@ -42,5 +42,26 @@ class ImageProcessor:
 
     @staticmethod
     def auto_process_images(images_bytes, max_width: int = 1920, max_height: int = 1080) -> list:
-        """Batch helper: one auto_process_image per input (decode on the host)."""
-        return [ImageProcessor.auto_process_image(b, max_width, max_height) for b in images_bytes]
+        """Batched auto_process_image: host decode on the decode pool, then one GPU
+        thumbnail launch sequence per group of equally sized images
+        (llfe_thumbnail_pil_batch).  Returns arrays in input order; an input that fails
+        to decode gets the ValueError auto_process_image would raise, in its place."""
+        from .backend import Backend, thumbnail_size
+        from .decode import decode_many
+
+        decoded = decode_many(list(images_bytes))
+        out: list = [None] * len(decoded)
+        groups: dict = {}
+        for i, im in enumerate(decoded):
+            if isinstance(im, Exception):
+                out[i] = ValueError("Image processing error: Failed to decode image")
+            elif thumbnail_size(im.shape[1], im.shape[0], max_width, max_height) is None:
+                out[i] = im
+            else:
+                groups.setdefault(im.shape, []).append(i)
+        be = Backend.get() if groups else None
+        for shape, idx in groups.items():
+            res = be.thumbnail_pil_batch(np.stack([decoded[i] for i in idx]), max_width, max_height).cpu().numpy()
+            for j, i in enumerate(idx):
+                out[i] = res[j]
+        return out

@@ -271,6 +271,44 @@ def test_auto_process_image_dropin():
         ImageProcessor.auto_process_image(b"junk")
 
 
+
+@pytest.mark.parametrize("h,w", [(2160, 3840), (1500, 1000), (5000, 2400)])
+def test_thumbnail_batch_vs_pillow(backend, h, w):
+    """llfe_thumbnail_pil_batch (one launch sequence for the batch) equals Pillow per image,
+    including the reduce() pre-pass (5000 x 2400)."""
+    from PIL import Image
+
+    a = np.random.default_rng(h * 3 + w).integers(0, 256, (3, h, w, 3), dtype=np.uint8)
+    got = backend.thumbnail_pil_batch(a).cpu().numpy()
+    for i in range(3):
+        im = Image.fromarray(a[i])
+        im.thumbnail((1920, 1080), Image.Resampling.LANCZOS)
+        assert np.array_equal(got[i], np.array(im)), i
+
+
+def test_auto_process_images_batched():
+    from PIL import Image
+
+    from low_level_feature_extraction_amd import ImageProcessor
+
+    rng = np.random.default_rng(2)
+    rgbs = [rng.integers(0, 256, s, dtype=np.uint8) for s in [(2160, 3840, 3), (300, 200, 3), (2160, 3840, 3),
+                                                                  (1200, 2500, 3)]]
+    blobs = []
+    for x in rgbs:
+        buf = io.BytesIO()
+        Image.fromarray(x).save(buf, format="PNG")
+        blobs.append(buf.getvalue())
+    blobs.insert(2, b"junk")
+    out = ImageProcessor.auto_process_images(blobs)
+    assert isinstance(out[2], ValueError)
+    got = [o for j, o in enumerate(out) if j != 2]
+    for x, g in zip(rgbs, got):
+        im = Image.fromarray(x)
+        im.thumbnail((1920, 1080), Image.Resampling.LANCZOS)
+        assert np.array_equal(g, np.array(im)[:, :, ::-1])
+
+
 # --------------------------------------------------------------------------- cv2.resize modes
 # validate_and_preprocess_image (utils.py:118-143): the GPU resize (llfe_resize_cv) against
 # the oracle's OpenCV restatement, bit-exact.  Sizes cover AREA 2x / 3x (resizeAreaFast_),
