@@ -30,7 +30,7 @@ FETCH_X2 = {"k_kmeans", "k_uq_keys", "k_uq_scatter"}  # 16 B/lane streaming read
 
 LOGICAL = [  # (substring of the device kernel name, logical launch)
     ("k_stencil", "k_stencil"),
-    ("k_shadow_reduce", "k_stencil"),
+    ("shadow_reduce", "k_stencil"),
     ("k_ccl_", "k_hysteresis_dilate"),
     ("k_bits_dilate", "k_hysteresis_dilate"),
     ("k_uq_keys", "k_uq_keys"),
@@ -44,6 +44,8 @@ LOGICAL = [  # (substring of the device kernel name, logical launch)
 
 
 def logical(name: str):
+    if name.startswith("void "):  # template kernels are reported with their return type
+        name = name[5:]
     if not name.startswith("llfe::"):
         return None
     for sub, lg in LOGICAL:
