@@ -214,6 +214,16 @@ int llfe_edge_classes(llfe_ctx *ctx, const uint8_t *bgr, uint8_t *classes, int32
  * 0/255 u8; bgr and mask are device pointers (n x h x w x 3 / n x h x w). */
 int llfe_font_binary(llfe_ctx *ctx, const uint8_t *bgr, uint8_t *mask, int32_t n, int32_t h, int32_t w,
                      llfe_stream stream);
+/* TextExtractor.preprocess_image (app/services/analyze/text_extractor.py:15-46): gray
+ * (cvtColor BGR2GRAY for 3 / 4 channels, the image itself for 1), INTER_CUBIC upscale by
+ * max(2, 300 / w, 100 / h) when h < 30 or w < 100, Otsu THRESH_BINARY, bitwise_not when
+ * mean(binary) > 127.  img: device h x w x channels u8; out: device out_h x out_w u8
+ * (llfe_text_size); *threshold (host, may be NULL) receives Otsu's threshold. */
+int llfe_text_binary(llfe_ctx *ctx, const uint8_t *img, int32_t h, int32_t w, int32_t channels, uint8_t *out,
+                     int32_t *threshold, llfe_stream stream);
+/* output size of llfe_text_binary: returns 1 when the image is upscaled, 0 when not
+ * (text_extractor.py:31-37; saturate_cast<int> of w * scale, h * scale). Host only. */
+int llfe_text_size(int32_t h, int32_t w, int32_t *out_h, int32_t *out_w);
 /* sums[n], counts[n] host: adaptive-threshold shadow statistics (shadow pyc @L15-21) */
 int llfe_shadow_stats(llfe_ctx *ctx, const uint8_t *bgr, uint64_t *sums, uint64_t *counts, int32_t n, int32_t h,
                       int32_t w, llfe_stream stream);
@@ -240,6 +250,7 @@ int llfe_reduce_pil(llfe_ctx *ctx, const uint8_t *src, int32_t h, int32_t w, int
  * 118-143): LLFE_CV_INTER_AREA for "auto", LLFE_CV_INTER_LANCZOS4 for "high_quality",
  * LLFE_CV_INTER_LINEAR for "performance".  dst holds out_h x out_w x ch bytes. */
 #define LLFE_CV_INTER_LINEAR 1
+#define LLFE_CV_INTER_CUBIC 2
 #define LLFE_CV_INTER_AREA 3
 #define LLFE_CV_INTER_LANCZOS4 4
 int llfe_resize_cv(llfe_ctx *ctx, const uint8_t *src, int32_t h, int32_t w, int32_t ch, uint8_t *dst, int32_t out_h,

@@ -125,6 +125,8 @@ SIGNATURES = {
     "llfe_shape_mask": (C.c_int, [_vp, _vp, _vp, _i32, _i32, _i32, _vp]),
     "llfe_edge_classes": (C.c_int, [_vp, _vp, _vp, _i32, _i32, _i32, _vp]),
     "llfe_font_binary": (C.c_int, [_vp, _vp, _vp, _i32, _i32, _i32, _vp]),
+    "llfe_text_binary": (C.c_int, [_vp, _vp, _i32, _i32, _i32, _vp, C.POINTER(_i32), _vp]),
+    "llfe_text_size": (C.c_int, [_i32, _i32, C.POINTER(_i32), C.POINTER(_i32)]),
     "llfe_shadow_stats": (C.c_int, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _vp]),
     "llfe_color_unique": (C.c_int, [_vp, C.POINTER(LlfeBatch), _u64, _vp, _vp, _vp]),
     "llfe_kmeans": (C.c_int, [_vp, _vp, _i64, _vp, _i32, _i32, _u64, _i64, _vp, _vp]),

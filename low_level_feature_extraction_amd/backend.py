@@ -62,6 +62,14 @@ def _is_torch(x) -> bool:
     return isinstance(x, torch.Tensor)
 
 
+def text_size(h: int, w: int):
+    """Output (height, width) of TextExtractor.preprocess_image (llfe_text_size)."""
+    oh, ow = C.c_int32(0), C.c_int32(0)
+    if L.lib().llfe_text_size(int(h), int(w), C.byref(oh), C.byref(ow)) < 0:
+        raise ValueError(f"text_size: invalid {h}x{w}")
+    return oh.value, ow.value
+
+
 class Backend:
     _instances: dict = {}
     _ilock = threading.Lock()
@@ -356,6 +364,23 @@ class Backend:
         self._chk(self._lib.llfe_font_binary(self.ctx, x.data_ptr(), out.data_ptr(), n, h, w, self._stream(x)))
         return out
 
+    def text_binary(self, image):
+        """TextExtractor.preprocess_image on the GPU (text_extractor.py:15-46): one
+        H x W [x C] uint8 image (C = 1, 3 BGR or 4 BGRA) -> (out_h x out_w 0/255 device
+        tensor, Otsu threshold)."""
+        torch = _torch()
+        x = image if _is_torch(image) else torch.from_numpy(np.ascontiguousarray(image, np.uint8))
+        x = x.to(f"cuda:{self.device}").contiguous()
+        if x.dim() == 2:
+            x = x[:, :, None]
+        h, w, ch = x.shape
+        oh, ow = text_size(h, w)
+        out = torch.empty((oh, ow), dtype=torch.uint8, device=x.device)
+        t = C.c_int32(0)
+        self._chk(self._lib.llfe_text_binary(self.ctx, x.data_ptr(), h, w, ch, out.data_ptr(), C.byref(t),
+                                             self._stream(x)))
+        return out, int(t.value)
+
     def shape_mask(self, images):
         torch = _torch()
         x = self._dev_batch(images)
@@ -526,7 +551,7 @@ class Backend:
         return out
 
 
-CV_INTER = {"linear": 1, "area": 3, "lanczos4": 4}
+CV_INTER = {"linear": 1, "cubic": 2, "area": 3, "lanczos4": 4}
 PRE_MODES = {"none": 0, "auto": 1, "high_quality": 2, "performance": 3}
 _INTER_NAME = {1: "INTER_LINEAR", 3: "INTER_AREA", 4: "INTER_LANCZOS4"}
 

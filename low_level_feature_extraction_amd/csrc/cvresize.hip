@@ -9,10 +9,14 @@
 //     factors cvRound(int sum * (1.f / area)), partial border cells cvRound(sum / count);
 //   * AREA, other factors >= 1 (resizeArea_): computeResizeAreaTab weights (float), row
 //     buffers accumulated in table order, then rows in table order, cvRound;
-//   * LINEAR / LANCZOS4 / AREA-upscale (resizeGeneric_): 11-bit fixed-point taps,
-//     int32 horizontal pass, vertical LANCZOS4 (sum + 2^21) >> 22, vertical LINEAR
+//   * LINEAR / CUBIC / LANCZOS4 / AREA-upscale (resizeGeneric_): 11-bit fixed-point
+//     taps, int32 horizontal pass, vertical LANCZOS4 (sum + 2^21) >> 22, vertical LINEAR
 //     VResizeLinearVec_32s8u ((S0 >> 4) * b0 >> 16) + ((S1 >> 4) * b1 >> 16) + 2 >> 2
-//     for the row elements its 128-bit vector loops cover, FixedPtCast for the tail.
+//     for the row elements its 128-bit vector loops cover, FixedPtCast for the tail;
+//     vertical CUBIC VResizeCubicVec_32s8u (float S3*b3, then S2*b2 + t, S1*b1 + t,
+//     S0*b0 + t with b = beta / 2^22, rint, saturate; mul + add on the SSE baseline) for
+//     the elements its loop covers (steps of 16), FixedPtCast for the tail.  CUBIC is the
+//     small-image upscale of TextExtractor.preprocess_image (text_extractor.py:31-37).
 // The tables are built on the host exactly as OpenCV builds them (double / float
 // arithmetic, libm sin / cos for Lanczos); the kernels evaluate one output pixel per
 // thread.  Not a hot path (no BASELINE configuration resizes): clarity over speed.
@@ -104,6 +108,9 @@ __global__ __launch_bounds__(RT) void k_cv_generic(const uint8_t *__restrict__ s
             int32_t v;
             if (ks == 2) {
                 v = dx < xmax_px ? S[sx * cn + c] * a[0] + S[(sx + 1) * cn + c] * a[1] : S[sx * cn + c] * 2048;
+            } else if (ks == 4) {
+                v = 0;
+                for (int j = 0; j < 4; j++) v += S[min(max(sx - 1 + j, 0), w - 1) * cn + c] * a[j];
             } else {
                 v = 0;
                 for (int j = 0; j < 8; j++) v += S[min(max(sx - 3 + j, 0), w - 1) * cn + c] * a[j];
@@ -123,6 +130,17 @@ __global__ __launch_bounds__(RT) void k_cv_generic(const uint8_t *__restrict__ s
                 v = sat8((t + 2) >> 2);
             } else {
                 v = sat8((hv[0][c] * b[0] + hv[1][c] * b[1] + (1 << 21)) >> 22);
+            }
+        } else if (ks == 4) {
+            if (dx * cn + c < x_vec) {
+                const float sc = 1.f / (2048.f * 2048.f);
+                float t = __fmul_rn((float)hv[3][c], (float)b[3] * sc);
+                t = __fadd_rn(__fmul_rn((float)hv[2][c], (float)b[2] * sc), t);
+                t = __fadd_rn(__fmul_rn((float)hv[1][c], (float)b[1] * sc), t);
+                t = __fadd_rn(__fmul_rn((float)hv[0][c], (float)b[0] * sc), t);
+                v = rint_sat8(t);
+            } else {
+                v = sat8((hv[0][c] * b[0] + hv[1][c] * b[1] + hv[2][c] * b[2] + hv[3][c] * b[3] + (1 << 21)) >> 22);
             }
         } else {
             uint32_t s = 0;
@@ -154,6 +172,15 @@ inline int32_t fbits(float f) {
     int32_t b;
     std::memcpy(&b, &f, 4);
     return b;
+}
+
+// interpolateCubic, A = -0.75 (float arithmetic)
+void cubic(float x, float *coeffs) {
+    const float A = -0.75f;
+    coeffs[0] = ((A * (x + 1) - 5 * A) * (x + 1) + 8 * A) * (x + 1) - 4 * A;
+    coeffs[1] = ((A + 2) * x - (A + 3)) * x * x + 1;
+    coeffs[2] = ((A + 2) * (1 - x) - (A + 3)) * (1 - x) * (1 - x) + 1;
+    coeffs[3] = 1.f - coeffs[0] - coeffs[1] - coeffs[2];
 }
 
 // interpolateLanczos4
@@ -208,15 +235,21 @@ void area_tab(int ssize, int dsize, int cn, double scale, std::vector<int32_t> &
 }  // namespace
 
 int cv_resize_plan(int h, int w, int cn, int oh, int ow, int interp, CvResizePlan &p) {
+    if (h <= 0 || w <= 0) return -1;
+    return cv_resize_plan_scaled(h, w, cn, oh, ow, (double)ow / w, (double)oh / h, interp, p);
+}
+
+int cv_resize_plan_scaled(int h, int w, int cn, int oh, int ow, double inv_x, double inv_y, int interp,
+                          CvResizePlan &p) {
     p = CvResizePlan{};
     p.h = h, p.w = w, p.cn = cn, p.oh = oh, p.ow = ow;
     if (h <= 0 || w <= 0 || oh <= 0 || ow <= 0 || cn <= 0 || cn > 4) return -1;
-    if (interp != kCvInterLinear && interp != kCvInterArea && interp != kCvInterLanczos4) return -1;
+    if (interp != kCvInterLinear && interp != kCvInterArea && interp != kCvInterLanczos4 && interp != kCvInterCubic)
+        return -1;
     if (oh == h && ow == w) {
         p.kind = CvResizePlan::COPY;
         return 0;
     }
-    const double inv_x = (double)ow / w, inv_y = (double)oh / h;
     const double scale_x = 1. / inv_x, scale_y = 1. / inv_y;
     const int ix = (int)std::lrint(scale_x), iy = (int)std::lrint(scale_y);
     const bool fast = std::fabs(scale_x - ix) < 2.220446049250313e-16 && std::fabs(scale_y - iy) < 2.220446049250313e-16;
@@ -235,8 +268,9 @@ int cv_resize_plan(int h, int w, int cn, int oh, int ow, int interp, CvResizePla
         return 0;
     }
     p.kind = CvResizePlan::GENERIC;
-    const int ks = interp == kCvInterLanczos4 ? 8 : 2, ks2 = ks / 2;
+    const int ks = interp == kCvInterLanczos4 ? 8 : (interp == kCvInterCubic ? 4 : 2), ks2 = ks / 2;
     const bool area_mode = interp == kCvInterArea;
+    const bool wide = interp == kCvInterLanczos4 || interp == kCvInterCubic;  // no sx / fx clamp
     p.ks = ks;
     std::vector<int32_t> xofs(ow), xa((size_t)ow * ks), yofs(oh), yb((size_t)oh * ks);
     float cbuf[8];
@@ -255,14 +289,15 @@ int cv_resize_plan(int h, int w, int cn, int oh, int ow, int interp, CvResizePla
         }
         if (sx < ks2 - 1) {
             xmin = dx + 1;
-            if (sx < 0 && interp != kCvInterLanczos4) fx = 0, sx = 0;
+            if (sx < 0 && !wide) fx = 0, sx = 0;
         }
         if (sx + ks2 >= w) {
             xmax = std::min(xmax, dx);
-            if (sx >= w - 1 && interp != kCvInterLanczos4) fx = 0, sx = w - 1;
+            if (sx >= w - 1 && !wide) fx = 0, sx = w - 1;
         }
         xofs[dx] = sx;
         if (interp == kCvInterLanczos4) lanczos4(fx, cbuf);
+        else if (interp == kCvInterCubic) cubic(fx, cbuf);
         else cbuf[0] = 1.f - fx, cbuf[1] = fx;
         for (int k = 0; k < ks; k++) xa[(size_t)dx * ks + k] = sat_s16(cbuf[k] * 2048);
     }
@@ -280,6 +315,7 @@ int cv_resize_plan(int h, int w, int cn, int oh, int ow, int interp, CvResizePla
         }
         yofs[dy] = sy;
         if (interp == kCvInterLanczos4) lanczos4(fy, cbuf);
+        else if (interp == kCvInterCubic) cubic(fy, cbuf);
         else cbuf[0] = 1.f - fy, cbuf[1] = fy;
         for (int k = 0; k < ks; k++) yb[(size_t)dy * ks + k] = sat_s16(cbuf[k] * 2048);
     }
@@ -287,7 +323,8 @@ int cv_resize_plan(int h, int w, int cn, int oh, int ow, int interp, CvResizePla
     const int width = ow * cn;
     int xv = 0;
     while (xv <= width - 16) xv += 16;
-    while (xv < width - 8) xv += 8;
+    if (ks == 2)  // VResizeLinearVec_32s8u's second, 8-lane loop (VResizeCubicVec has one)
+        while (xv < width - 8) xv += 8;
     p.x_vec = xv;
     p.tab.insert(p.tab.end(), xofs.begin(), xofs.end());
     p.tab.insert(p.tab.end(), xa.begin(), xa.end());

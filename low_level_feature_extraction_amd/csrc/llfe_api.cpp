@@ -395,6 +395,8 @@ struct llfe_ctx {
     DevBuf<uint8_t> d_ragged;       // llfe_process_images: one size group's packed images
     DevBuf<int8_t> d_ragged_noise;
     DevBuf<int32_t> d_coef;
+    DevBuf<uint8_t> d_text;                  // llfe_text_binary: gray, then its upscale
+    DevBuf<unsigned long long> d_text_hist;  // 256 bins + threshold + count of 255s
     // pinned host staging; the per-chunk results are double-buffered so the host can
     // trace chunk c's contours while the GPU runs chunk c + 1
     HostBuf<uint64_t> h_bits_s[2];
@@ -1295,6 +1297,59 @@ int llfe_font_binary(llfe_ctx *ctx, const uint8_t *bgr, uint8_t *mask, int32_t n
     HIPCHK(ctx, hipSetDevice(ctx->device));
     HIPCHK(ctx, launch_font_binary(bgr, n, h, w, mask, ctx->sp, (hipStream_t)stream));
     HIPCHK(ctx, hipStreamSynchronize((hipStream_t)stream));
+    return LLFE_OK;
+}
+
+int llfe_text_size(int32_t h, int32_t w, int32_t *out_h, int32_t *out_w) {
+    if (h <= 0 || w <= 0 || !out_h || !out_w) return LLFE_ERR_INVALID;
+    if (h < 30 || w < 100) {  // scale = max(2, 300 / width, 100 / height) (Python floats)
+        const double sc = std::max(std::max(2.0, 300.0 / w), 100.0 / h);
+        *out_w = (int32_t)std::lrint(w * sc);  // saturate_cast<int>(double): round half even
+        *out_h = (int32_t)std::lrint(h * sc);
+        return 1;
+    }
+    *out_h = h;
+    *out_w = w;
+    return 0;
+}
+
+// TextExtractor.preprocess_image (text_extractor.py:15-46): gray, INTER_CUBIC upscale
+// of small images (cvresize.hip), Otsu binary and the mean > 127 inversion (text.hip)
+int llfe_text_binary(llfe_ctx *ctx, const uint8_t *img, int32_t h, int32_t w, int32_t channels, uint8_t *out,
+                     int32_t *threshold, llfe_stream stream) {
+    if (!ctx || !img || !out || h <= 0 || w <= 0) return LLFE_ERR_INVALID;
+    if (channels != 1 && channels != 3 && channels != 4)
+        return ctx->fail(LLFE_ERR_UNSUPPORTED, "llfe_text_binary: %d channels (1, 3 or 4)", channels);
+    int32_t oh, ow;
+    const int up = llfe_text_size(h, w, &oh, &ow);
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = (hipStream_t)stream;
+    const long long n = (long long)h * w, n2 = (long long)oh * ow;
+    HIPCHK(ctx, ctx->d_text.ensure((size_t)(n + (up ? n2 : 0))));
+    HIPCHK(ctx, ctx->d_text_hist.ensure(258));
+    uint8_t *gray = ctx->d_text.p, *g = gray;
+    HIPCHK(ctx, launch_text_gray(img, n, channels, gray, s));
+    if (up) {
+        const double sc = std::max(std::max(2.0, 300.0 / w), 100.0 / h);
+        CvResizePlan plan;
+        if (cv_resize_plan_scaled(h, w, 1, oh, ow, sc, sc, kCvInterCubic, plan) != 0)
+            return ctx->fail(LLFE_ERR_UNSUPPORTED, "llfe_text_binary: resize plan");
+        HIPCHK(ctx, ctx->d_coef.ensure(plan.tab.size()));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->d_coef.p, plan.tab.data(), plan.tab.size() * sizeof(int32_t),
+                                   hipMemcpyHostToDevice, s));
+        g = gray + n;
+        HIPCHK(ctx, launch_cv_resize(plan, gray, g, ctx->d_coef.p, s));
+        HIPCHK(ctx, hipStreamSynchronize(s));  // the host table dies with `plan`
+    }
+    HIPCHK(ctx, launch_text_otsu_binary(g, n2, ctx->d_text_hist.p, out, s));
+    if (threshold) {
+        unsigned long long t = 0;
+        HIPCHK(ctx, hipMemcpyAsync(&t, ctx->d_text_hist.p + 256, sizeof t, hipMemcpyDeviceToHost, s));
+        HIPCHK(ctx, hipStreamSynchronize(s));
+        *threshold = (int32_t)t;
+    } else {
+        HIPCHK(ctx, hipStreamSynchronize(s));
+    }
     return LLFE_OK;
 }
 

@@ -225,7 +225,7 @@ hipError_t launch_reduce(const uint8_t *src, int src_w, int ch, int x0, int y0, 
                          long long dst_img = 0);
 
 // cv2.resize for the preprocessing modes (cvresize.hip); OpenCV interpolation codes
-constexpr int kCvInterLinear = 1, kCvInterArea = 3, kCvInterLanczos4 = 4;
+constexpr int kCvInterLinear = 1, kCvInterCubic = 2, kCvInterArea = 3, kCvInterLanczos4 = 4;
 struct CvResizePlan {
     enum Kind { COPY, AREA_FAST, AREA, GENERIC } kind = COPY;
     int h = 0, w = 0, cn = 0, oh = 0, ow = 0;
@@ -236,7 +236,16 @@ struct CvResizePlan {
 };
 // host: OpenCV's tables for (h, w, cn) -> (oh, ow); 0 ok, -1 unsupported
 int cv_resize_plan(int h, int w, int cn, int oh, int ow, int interp, CvResizePlan &p);
+// the same with cv::resize's inverse scales given (dsize empty: the caller's fx, fy)
+int cv_resize_plan_scaled(int h, int w, int cn, int oh, int ow, double inv_x, double inv_y, int interp,
+                          CvResizePlan &p);
 hipError_t launch_cv_resize(const CvResizePlan &p, const uint8_t *src, uint8_t *dst, const int32_t *d_tab,
                             hipStream_t s);
+
+// TextExtractor.preprocess_image (text.hip): gray of n pixels (cn 1, 3 or 4); Otsu
+// binary of n gray pixels; hist = 258 u64 of device scratch (threshold in hist[256])
+hipError_t launch_text_gray(const uint8_t *img, long long n, int cn, uint8_t *gray, hipStream_t s);
+hipError_t launch_text_otsu_binary(const uint8_t *g, long long n, unsigned long long *hist, uint8_t *out,
+                                   hipStream_t s);
 
 }  // namespace llfe

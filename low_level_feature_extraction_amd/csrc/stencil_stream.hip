@@ -250,7 +250,10 @@ __device__ __forceinline__ void rowpass4(uint32_t B, const float *__restrict__ k
 }
 
 template <bool CLS, bool SHD>
-__global__ __launch_bounds__(64 * kWavesPerBlock, 4) void k_stencil_stream(
+#ifndef LLFE_ST_MINW
+#define LLFE_ST_MINW 4
+#endif
+__global__ __launch_bounds__(64 * kWavesPerBlock, LLFE_ST_MINW) void k_stencil_stream(
     const uint8_t *__restrict__ bgr, int H, int W, int strips, int segs, int seg_rows, int total_waves, int vec,
     uint8_t *__restrict__ cls, uint2 *__restrict__ wave_part, StencilParams prm) {
     const int lane = threadIdx.x & 63;
@@ -389,12 +392,19 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, 4) void k_stencil_stream(
                     const uint32_t bw = bring[kc];
 #pragma unroll
                     for (int j = 0; j < 4; j++) {
-                        // mean = saturate(rint(s)) (s <= 255 + rounding, so rint(s) <= 255)
-                        const float mean = __builtin_rintf(sj[j]);
+                        // mean = saturate(rint(s)) (0 <= s <= 255 + rounding, so rint(s) <=
+                        // 255).  s + 2^23 rounds to 2^23 + rint(s) (round-half-even, spacing
+                        // 1 in [2^23, 2^24)), so the bits of the sum are 0x4B000000 + mean and
+                        // b + 2 <= mean <=> (b + 0x4B000001) - bits < 0: one f32 add and
+                        // integer VOP2 ops, which issue at twice the rate of rint / cvt / cmp
+                        const uint32_t r = __float_as_uint(sj[j] + 8388608.0f);
                         const uint32_t b = byte_of(bw, j);
-                        const bool m = out_lane && x + j < W && (float)b + 2.0f <= mean;
-                        lsum += m ? b : 0u;
-                        lcnt += m ? 1u : 0u;
+                        uint32_t t = (uint32_t)((int32_t)(b + 0x4B000001u - r) >> 31);
+                        // halo lanes are dropped after the loop; only border waves have
+                        // output lanes with columns past W
+                        if (edge) t = (x + j < W) ? t : 0u;
+                        lsum += b & t;
+                        lcnt -= t;  // t = 0 or ~0
                     }
                 }
             }
@@ -402,6 +412,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, 4) void k_stencil_stream(
         }
     }
     if (SHD) {
+        if (!out_lane) lsum = lcnt = 0;  // halo lanes (and lanes wholly past W)
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {  // <= 240 x 4096 x 255 < 2^32 per wave
             lsum += __shfl_xor(lsum, off);

@@ -442,7 +442,7 @@ def preprocess_size(w, h, mode):
     return None
 
 
-CV_INTER = {"linear": 1, "area": 3, "lanczos4": 4}
+CV_INTER = {"linear": 1, "cubic": 2, "area": 3, "lanczos4": 4}
 
 
 def cv_resize(img, out_w, out_h, interp):
@@ -458,6 +458,49 @@ def cv_resize(img, out_w, out_h, interp):
     if lib().orc_cv_resize(_p(img), h, w, ch, _p(out), out_h, out_w, code) != 0:
         raise ValueError(f"cv_resize: unsupported {interp!r} {w}x{h} -> {out_w}x{out_h}")
     return out[:, :, 0] if squeeze else out
+
+
+def cv_resize_scaled(img, fx, fy, interp):
+    """cv2.resize(img, None, fx=fx, fy=fy, interpolation=...): dsize = saturate_cast<int>
+    of w * fx, h * fy and the given factors as the inverse scales."""
+    img = np.ascontiguousarray(img, np.uint8)
+    squeeze = img.ndim == 2
+    if squeeze:
+        img = img[:, :, None]
+    h, w, ch = img.shape
+    out_w, out_h = int(np.rint(w * fx)), int(np.rint(h * fy))
+    out = np.empty((out_h, out_w, ch), np.uint8)
+    code = CV_INTER[interp] if isinstance(interp, str) else int(interp)
+    if lib().orc_cv_resize_scaled(_p(img), h, w, ch, _p(out), out_h, out_w, C.c_double(fx), C.c_double(fy),
+                                  code) != 0:
+        raise ValueError(f"cv_resize_scaled: unsupported {interp!r} {w}x{h} x ({fx}, {fy})")
+    return out[:, :, 0] if squeeze else out
+
+
+def otsu_threshold(gray) -> int:
+    """cv2.threshold(gray, 0, 255, THRESH_BINARY + THRESH_OTSU)[0] (non-IPP path)."""
+    g = np.ascontiguousarray(gray, np.uint8)
+    return int(lib().orc_otsu_threshold(_p(g), C.c_longlong(g.size)))
+
+
+def text_size(h, w):
+    """Output size (h, w) of TextExtractor.preprocess_image (text_extractor.py:31-37)."""
+    oh, ow = C.c_int(), C.c_int()
+    lib().orc_text_size(h, w, C.byref(oh), C.byref(ow), None)
+    return oh.value, ow.value
+
+
+def text_binary(img):
+    """TextExtractor.preprocess_image (text_extractor.py:15-46) restated in llfe_oracle.c:
+    (binary u8 image, Otsu threshold)."""
+    img = np.ascontiguousarray(img, np.uint8)
+    if img.ndim == 2:
+        img = img[:, :, None]
+    h, w, cn = img.shape
+    oh, ow = text_size(h, w)
+    out = np.empty((oh, ow), np.uint8)
+    t = lib().orc_text_binary(_p(img), h, w, cn, _p(out))
+    return out, int(t)
 
 
 def preprocess(img, mode):

@@ -67,7 +67,11 @@ __global__ void k(unsigned *out, int iters) {
     if (OP == 56) asm volatile("v_cvt_f32_ubyte0 %0, %1" : "+v"(r) : "v"(b));  \
     if (OP == 57) asm volatile("v_mov_b32_sdwa %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1" : "+v"(r) : "v"(b));  \
     if (OP == 58) asm volatile("v_and_b32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD" : "+v"(r) : "v"(b));  \
-    if (OP == 59) asm volatile("v_add_u32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD" : "+v"(r) : "v"(b));
+    if (OP == 59) asm volatile("v_add_u32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD" : "+v"(r) : "v"(b)); \
+    if (OP == 60) asm volatile("v_fmac_f32 %0, %1, %1\n v_add_u32 %0, %0, %1" : "+v"(r) : "v"(b));  \
+    if (OP == 61) asm volatile("v_perm_b32 %0, %0, %1, %1\n v_and_b32 %0, %0, %1" : "+v"(r) : "v"(b));  \
+    if (OP == 62) asm volatile("v_fmac_f32 %0, %1, %1\n v_add_u32 %0, %0, %1\n v_xor_b32 %0, %0, %1" : "+v"(r) : "v"(b));  \
+    if (OP == 63) asm volatile("v_add_u32 %0, %0, %1\n v_mul_f32 %0, %0, %1" : "+v"(r) : "v"(b));
         REP8(OP1(a0) OP1(a1) OP1(a2) OP1(a3) OP1(a4) OP1(a5) OP1(a6) OP1(a7))
     }
     out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
@@ -87,7 +91,7 @@ __global__ void kpk(unsigned *out, int iters) {  // v_pk_fma_f32 on 64-bit pairs
 
 static const char *names[] = {"v_add_u32", "v_fmac_f32", "v_pk_add_u16", "v_perm_b32", "v_mov_dpp", "v_cndmask_e64",
                               "v_cvt_f32_ubyte", "v_bfe_u32", "v_dot2_u32_u16", "v_alignbit", "v_lshl_or", "v_mad_u32_u24",
-                              "v_pk_fma_f32", "v_and_b32", "v_or_b32", "v_lshlrev_b32", "v_mov_b32", "v_cndmask_e32", "v_add_f32", "v_mul_f32", "v_max_i32", "v_sub_u32", "v_add3_u32", "v_pk_add_f32", "v_add_u16", "v_cvt_f32_u32", "v_rndne_f32", "v_cmp_gt_u32", "v_med3_u32", "v_dot4_u32_u8", "v_mul_u32_u24", "v_lshrrev_b32", "v_sad_u32", "v_cvt_pk_u8_f32", "v_fma_f32", "v_pk_mul_f32", "v_xor_b32", "v_not_b32", "v_bfi_b32", "v_min_u32", "v_max_u32", "v_min_f32", "v_sub_f32", "v_lshlrev_b32_v", "v_lshrrev_b32_v", "v_ashrrev_i32", "v_pk_max_u16", "v_pk_sub_u16", "v_sub_u16", "v_mul_lo_u16", "v_max_u16", "v_add_co_u32", "v_cvt_u32_f32", "v_and_or_b32", "v_add_u32_sgpr", "v_add_u32_e64", "v_mul_f32_e64neg", "v_cvt_f32_ubyte0", "v_mov_b32_sdwa", "v_and_b32_sdwa", "v_add_u32_sdwa"};
+                              "v_pk_fma_f32", "v_and_b32", "v_or_b32", "v_lshlrev_b32", "v_mov_b32", "v_cndmask_e32", "v_add_f32", "v_mul_f32", "v_max_i32", "v_sub_u32", "v_add3_u32", "v_pk_add_f32", "v_add_u16", "v_cvt_f32_u32", "v_rndne_f32", "v_cmp_gt_u32", "v_med3_u32", "v_dot4_u32_u8", "v_mul_u32_u24", "v_lshrrev_b32", "v_sad_u32", "v_cvt_pk_u8_f32", "v_fma_f32", "v_pk_mul_f32", "v_xor_b32", "v_not_b32", "v_bfi_b32", "v_min_u32", "v_max_u32", "v_min_f32", "v_sub_f32", "v_lshlrev_b32_v", "v_lshrrev_b32_v", "v_ashrrev_i32", "v_pk_max_u16", "v_pk_sub_u16", "v_sub_u16", "v_mul_lo_u16", "v_max_u16", "v_add_co_u32", "v_cvt_u32_f32", "v_and_or_b32", "v_add_u32_sgpr", "v_add_u32_e64", "v_mul_f32_e64neg", "v_cvt_f32_ubyte0", "v_mov_b32_sdwa", "v_and_b32_sdwa", "v_add_u32_sdwa", "mix_fmac_add", "mix_perm_and", "mix_fmac_2add", "mix_add_mulf"};
 template <int OP>
 void run(unsigned *out, int wps) {
     const int blocks = 256 * wps, threads = 256, iters = 2000;  // 4 waves per block = one per SIMD
@@ -132,9 +136,6 @@ int main() {
     }
     unsigned *out;
     hipMalloc(&out, 256 * 8 * 256 * 4);
-    both<0>(out); both<1>(out); both<2>(out); both<3>(out); both<4>(out); both<5>(out); both<6>(out);
-    both<7>(out); both<8>(out); both<9>(out); both<10>(out); both<11>(out); both<12>(out);
-    both<13>(out); both<14>(out); both<15>(out); both<16>(out); both<17>(out); both<18>(out); both<19>(out); both<20>(out); both<21>(out); both<22>(out); both<24>(out); both<25>(out); both<26>(out); both<27>(out); both<28>(out); both<29>(out); both<30>(out); both<31>(out); both<32>(out); both<34>(out);
-    both<35>(out); both<36>(out); both<37>(out); both<38>(out); both<39>(out); both<40>(out); both<41>(out); both<42>(out); both<43>(out); both<44>(out); both<45>(out); both<46>(out); both<47>(out); both<48>(out); both<49>(out); both<50>(out); both<51>(out); both<52>(out); both<53>(out); both<54>(out); both<55>(out); both<56>(out); both<57>(out); both<58>(out); both<59>(out);
+    both<0>(out); both<1>(out); both<60>(out); both<61>(out); both<62>(out); both<63>(out);
     return 0;
 }
