@@ -71,7 +71,12 @@ __global__ void k(unsigned *out, int iters) {
     if (OP == 60) asm volatile("v_fmac_f32 %0, %1, %1\n v_add_u32 %0, %0, %1" : "+v"(r) : "v"(b));  \
     if (OP == 61) asm volatile("v_perm_b32 %0, %0, %1, %1\n v_and_b32 %0, %0, %1" : "+v"(r) : "v"(b));  \
     if (OP == 62) asm volatile("v_fmac_f32 %0, %1, %1\n v_add_u32 %0, %0, %1\n v_xor_b32 %0, %0, %1" : "+v"(r) : "v"(b));  \
-    if (OP == 63) asm volatile("v_add_u32 %0, %0, %1\n v_mul_f32 %0, %0, %1" : "+v"(r) : "v"(b));
+    if (OP == 63) asm volatile("v_add_u32 %0, %0, %1\n v_mul_f32 %0, %0, %1" : "+v"(r) : "v"(b)); \
+    if (OP == 64) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(r) : "v"(b));  \
+    if (OP == 65) asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(r) : "v"(b));  \
+    if (OP == 66) asm volatile("v_mul_hi_u32_u24 %0, %0, %1" : "+v"(r) : "v"(b));  \
+    if (OP == 67) asm volatile("v_bcnt_u32_b32 %0, %0, %1" : "+v"(r) : "v"(b));  \
+    if (OP == 68) asm volatile("v_lshrrev_b32 %0, 16, %0\n v_xor_b32 %0, %0, %1" : "+v"(r) : "v"(b));
         REP8(OP1(a0) OP1(a1) OP1(a2) OP1(a3) OP1(a4) OP1(a5) OP1(a6) OP1(a7))
     }
     out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
@@ -91,7 +96,7 @@ __global__ void kpk(unsigned *out, int iters) {  // v_pk_fma_f32 on 64-bit pairs
 
 static const char *names[] = {"v_add_u32", "v_fmac_f32", "v_pk_add_u16", "v_perm_b32", "v_mov_dpp", "v_cndmask_e64",
                               "v_cvt_f32_ubyte", "v_bfe_u32", "v_dot2_u32_u16", "v_alignbit", "v_lshl_or", "v_mad_u32_u24",
-                              "v_pk_fma_f32", "v_and_b32", "v_or_b32", "v_lshlrev_b32", "v_mov_b32", "v_cndmask_e32", "v_add_f32", "v_mul_f32", "v_max_i32", "v_sub_u32", "v_add3_u32", "v_pk_add_f32", "v_add_u16", "v_cvt_f32_u32", "v_rndne_f32", "v_cmp_gt_u32", "v_med3_u32", "v_dot4_u32_u8", "v_mul_u32_u24", "v_lshrrev_b32", "v_sad_u32", "v_cvt_pk_u8_f32", "v_fma_f32", "v_pk_mul_f32", "v_xor_b32", "v_not_b32", "v_bfi_b32", "v_min_u32", "v_max_u32", "v_min_f32", "v_sub_f32", "v_lshlrev_b32_v", "v_lshrrev_b32_v", "v_ashrrev_i32", "v_pk_max_u16", "v_pk_sub_u16", "v_sub_u16", "v_mul_lo_u16", "v_max_u16", "v_add_co_u32", "v_cvt_u32_f32", "v_and_or_b32", "v_add_u32_sgpr", "v_add_u32_e64", "v_mul_f32_e64neg", "v_cvt_f32_ubyte0", "v_mov_b32_sdwa", "v_and_b32_sdwa", "v_add_u32_sdwa", "mix_fmac_add", "mix_perm_and", "mix_fmac_2add", "mix_add_mulf"};
+                              "v_pk_fma_f32", "v_and_b32", "v_or_b32", "v_lshlrev_b32", "v_mov_b32", "v_cndmask_e32", "v_add_f32", "v_mul_f32", "v_max_i32", "v_sub_u32", "v_add3_u32", "v_pk_add_f32", "v_add_u16", "v_cvt_f32_u32", "v_rndne_f32", "v_cmp_gt_u32", "v_med3_u32", "v_dot4_u32_u8", "v_mul_u32_u24", "v_lshrrev_b32", "v_sad_u32", "v_cvt_pk_u8_f32", "v_fma_f32", "v_pk_mul_f32", "v_xor_b32", "v_not_b32", "v_bfi_b32", "v_min_u32", "v_max_u32", "v_min_f32", "v_sub_f32", "v_lshlrev_b32_v", "v_lshrrev_b32_v", "v_ashrrev_i32", "v_pk_max_u16", "v_pk_sub_u16", "v_sub_u16", "v_mul_lo_u16", "v_max_u16", "v_add_co_u32", "v_cvt_u32_f32", "v_and_or_b32", "v_add_u32_sgpr", "v_add_u32_e64", "v_mul_f32_e64neg", "v_cvt_f32_ubyte0", "v_mov_b32_sdwa", "v_and_b32_sdwa", "v_add_u32_sdwa", "mix_fmac_add", "mix_perm_and", "mix_fmac_2add", "mix_add_mulf", "v_mul_lo_u32", "v_mul_hi_u32", "v_mul_hi_u32_u24", "v_bcnt_u32_b32", "v_xor_lshr_mix"};
 template <int OP>
 void run(unsigned *out, int wps) {
     const int blocks = 256 * wps, threads = 256, iters = 2000;  // 4 waves per block = one per SIMD
@@ -136,6 +141,6 @@ int main() {
     }
     unsigned *out;
     hipMalloc(&out, 256 * 8 * 256 * 4);
-    both<0>(out); both<1>(out); both<60>(out); both<61>(out); both<62>(out); both<63>(out);
+    both<0>(out); both<1>(out); both<64>(out); both<65>(out); both<66>(out); both<67>(out); both<68>(out);
     return 0;
 }

@@ -16,7 +16,8 @@ half the bytes of wide coalesced streaming reads (16 B / lane), so it is doubled
 kernels that read that way (FETCH_X2); byte-wide readers are taken as reported (the
 guide calls other widths uncalibrated -- checked here: k_color_bitmap's doubled fetch
 equals its 3P input exactly, k_stencil's raw fetch lies between its 3P input and the
-no-reuse halo bound 3P x 1.75, its doubled fetch would exceed that bound).
+no-reuse halo bound 3P x 1.75, its doubled fetch would exceed that bound -- that was
+the tiled round-1 stencil; the row-streaming one is a dword-per-lane streaming reader).
 """
 from __future__ import annotations
 
@@ -26,7 +27,10 @@ import os
 import sys
 from collections import defaultdict
 
-FETCH_X2 = {"k_kmeans", "k_uq_keys", "k_uq_scatter"}  # 16 B/lane streaming readers
+# wide coalesced streaming readers: 16 B/lane (k-means, keys, scatter) and the
+# row-streaming stencil's three coalesced dwords per lane (r2c: raw fetch 0.55 x its 3P
+# input, doubled 1.09 x 3P = its 16/256-column + 10/270-row halo)
+FETCH_X2 = {"k_kmeans", "k_uq_keys", "k_uq_scatter", "k_stencil"}
 
 LOGICAL = [  # (substring of the device kernel name, logical launch)
     ("k_stencil", "k_stencil"),
