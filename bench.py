@@ -229,6 +229,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N-rank path on a one-GPU box: every rank on cuda:0, gloo for the
+    # control-plane collectives (RCCL refuses two ranks on one device)
+    share_gpu = os.environ.get("LLFE_BENCH_SHARE_GPU") == "1"
+    if share_gpu:
+        local = 0
 
     import torch
 
@@ -237,7 +242,10 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if share_gpu:
+            dist.init_process_group("gloo")  # (host tensors for its collectives: coll_dev)
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from low_level_feature_extraction_amd import shard, synth
     from low_level_feature_extraction_amd.backend import Backend
@@ -254,6 +262,8 @@ def main():
     base, _ = shard.shard_bounds(B * world, rank, world)  # weak scaling: B images per rank
     imgs = synth.synth_batch(B, H, W, seed=args.seed, device=f"cuda:{local}", index_base=base)
     torch.cuda.synchronize()
+
+    coll_dev = None if share_gpu else f"cuda:{local}"  # device of the MAX-over-ranks tensor
 
     def barrier():
         shard.barrier(device=local)
@@ -286,7 +296,7 @@ def main():
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier()
-    dt = shard.max_over_ranks(t1 - t0, device=f"cuda:{local}")
+    dt = shard.max_over_ranks(t1 - t0, device=coll_dev)
     stats = be.kernel_stats()
     # the same steps one batch at a time (llfe_process_batch), for reference
     dt_sync = None
@@ -298,7 +308,7 @@ def main():
         torch.cuda.synchronize()
         ts1 = time.perf_counter()
         barrier()
-        dt_sync = shard.max_over_ranks(ts1 - ts0, device=f"cuda:{local}")
+        dt_sync = shard.max_over_ranks(ts1 - ts0, device=coll_dev)
     # one extra, untimed step with every kernel in order on one stream: isolated kernel
     # durations for the secondary rooflines (in the timed steps the shapes kernels share
     # the GPU with the colour front, which stretches their event-timed spans)
@@ -364,7 +374,7 @@ def main():
         t = B * (args.e2e_host_steps if "h2d_gbs" in line else args.e2e_png_steps) / line["value"]
         line = dict(line)
         line["value"] = round(B * world * (args.e2e_host_steps if "h2d_gbs" in line else args.e2e_png_steps) /
-                              shard.max_over_ranks(t, device=f"cuda:{local}"), 2)
+                              shard.max_over_ranks(t, device=coll_dev), 2)
         line["per_rank"] = True
         return line
 
