@@ -217,6 +217,8 @@ def main():
     ap.add_argument("--e2e-host-steps", type=int, default=3, help="0 disables the decoded-host-array line")
     ap.add_argument("--seed", type=int, default=2025)
     ap.add_argument("--e2e-png-steps", type=int, default=2, help="0 disables the PNG end-to-end line")
+    ap.add_argument("--per-class-steps", type=int, default=2,
+                    help="steps of an all-ui and an all-photo batch (SURVEY.md 8d per-class throughput); 0 disables")
     ap.add_argument("--contours", choices=["auto", "host", "gpu"], default="auto",
                     help="where findContours + the shape loop run: the host pool from the copied-back mask "
                          "(overlaps k-means), the GPU (contours_gpu.hip), or auto (the library's choice: "
@@ -319,6 +321,27 @@ def main():
     iso = be.kernel_stats()
     be.set_concurrency(True)
     be.set_profiling(False)
+
+    # per-class throughput: the same step on an all-"ui" and an all-"photo"
+    # batch of the same size (k-means cost scales with the unique-colour count U)
+    per_class = None
+    if args.per_class_steps > 0:
+        per_class = {}
+        for kind in ("ui", "photo"):
+            cb = synth.synth_batch(B, H, W, seed=args.seed, device=f"cuda:{local}", index_base=base, kind=kind)
+            be.process(cb, feats, seed=args.seed + 2000, index_base=base)  # warm-up
+            torch.cuda.synchronize()
+            barrier()
+            tc0 = time.perf_counter()
+            for k in range(args.per_class_steps):
+                be.process(cb, feats, seed=args.seed + 3000 + k, index_base=base)
+            torch.cuda.synchronize()
+            tc1 = time.perf_counter()
+            barrier()
+            dtc = shard.max_over_ranks(tc1 - tc0, device=coll_dev)
+            per_class[kind] = {"value": round(B * world * args.per_class_steps / dtc, 2), "unit": "images/s",
+                               "ms_per_step": round(dtc / args.per_class_steps * 1e3, 3)}
+            del cb
 
     # (the e2e lines run on every rank before rank 0 reports: each rank pays its own
     # host-side work, as a serving node would)
@@ -424,6 +447,7 @@ def main():
         "dominant_kernel": dominant,
         "kernels": kernels,
         "shapes_per_image": round(n_shapes / (B * args.steps), 2),
+        "per_class": per_class,
         "cpu_baseline": cpu,
         "e2e_host": e2e_h,
         "e2e_png": e2e,

@@ -7,13 +7,14 @@ L=low_level_feature_extraction_amd/libllfe.so
 cp $L /tmp/libllfe_keep.so
 for v in tools/debug/variants/libllfe_*.so; do
     cp "$v" $L
-    timeout -k 10 300 python bench.py --cpu-baseline off --e2e-png-steps 0 --e2e-host-steps 0 --steps 5 --warmup 2 "$@" \
+    timeout -k 10 300 python bench.py --cpu-baseline off --e2e-png-steps 0 --e2e-host-steps 0 --per-class-steps 0 --steps 5 --warmup 2 "$@" \
         > gpurun_out/var.json 2> gpurun_out/var.err || { echo "$v failed"; tail -3 gpurun_out/var.err; cp /tmp/libllfe_keep.so $L; exit 1; }
     python3 -c "
 import json,sys
 d=json.loads(open('gpurun_out/var.json').read().strip().splitlines()[-1])
 k=d['kernels']
-print('%-40s img/s %8.0f  step %6.2f  stencil iso %.3f  kmeans %.3f' % (sys.argv[1], d['value'], d['ms_per_step'], d['roofline_stencil']['avg_launch_ms'], k['k_kmeans']['avg_ms']))
+iso=' '.join('%s %.3f' % (n.replace('k_', ''), v.get('isolated_ms') or 0) for n, v in k.items())
+print('%-28s img/s %8.0f step %6.2f | iso: %s' % (sys.argv[1], d['value'], d['ms_per_step'], iso))
 " "$(basename $v)"
 done
 cp /tmp/libllfe_keep.so $L
