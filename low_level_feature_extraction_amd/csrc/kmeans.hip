@@ -1131,6 +1131,29 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
             // pairwise thresholds T[k][j] = 3 L1(c_j - c_k) + 1 (uniform); -inf where the
             // pair needs no test (j == k, or an unused centre)
             const Cent cu = load_centres(sm.c);
+            // cube-centre forms L_j(q) = |c_j|^2 - 2 q.c_j = d_j(q) - |q|^2 (pairs (0,1),
+            // (2,3), (4,-)): three packed FMAs per pair instead of the six packed ops of the
+            // distances; the tests below only use differences L_a - L_b = d_a - d_b, and the
+            // margin's +1 absorbs the float rounding of either form (<= 0.1 at these
+            // magnitudes).  Unused centres get L = +inf (never the minimum, always farther).
+            f2 lw_x[3], lw_y[3], lw_z[3], lc2[3];
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const int m = 2 * j + h;
+                    const bool used = m < K;
+                    const float cx = m < kMaxK ? cu.x[m] : 0.f, cy = m < kMaxK ? cu.y[m] : 0.f,
+                                cz = m < kMaxK ? cu.z[m] : 0.f;
+                    const float wx = used ? -2.f * cx : 0.f, wy = used ? -2.f * cy : 0.f, wz = used ? -2.f * cz : 0.f;
+                    const float c2 = used ? cx * cx + cy * cy + cz * cz : __builtin_inff();
+                    if (h == 0) {
+                        lw_x[j].x = wx, lw_y[j].x = wy, lw_z[j].x = wz, lc2[j].x = c2;
+                    } else {
+                        lw_x[j].y = wx, lw_y[j].y = wy, lw_z[j].y = wz, lc2[j].y = c2;
+                    }
+                }
+            }
             float thr[kMaxK][kMaxK];
 #pragma unroll
             for (int k = 0; k < kMaxK; k++)
@@ -1194,11 +1217,9 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
                     f2 d[3];
 #pragma unroll
                     for (int j = 0; j < 3; j++) {
-                        const f2 t0 = px - c.x[j], t1 = py - c.y[j], t2 = pz - c.z[j];
-                        f2 dd = t0 * t0;
-                        dd = __builtin_elementwise_fma(t1, t1, dd);
-                        dd = __builtin_elementwise_fma(t2, t2, dd);
-                        d[j] = dd;
+                        f2 dd = __builtin_elementwise_fma(px, lw_x[j], lc2[j]);
+                        dd = __builtin_elementwise_fma(py, lw_y[j], dd);
+                        d[j] = __builtin_elementwise_fma(pz, lw_z[j], dd);
                     }
                     const float dv[5] = {d[0].x, d[0].y, d[1].x, d[1].y, d[2].x};
                     const float m1 = fminf(fminf(fminf(dv[0], dv[1]), fminf(dv[2], dv[3])), dv[4]);
