@@ -111,8 +111,8 @@ def cpu_baseline(n_images, h, w, workers):
     }
 
 
-def _encode_png(args):
-    i, h, w, seed = args
+def _encode(args):
+    i, h, w, seed, fmt = args
     import io
 
     from PIL import Image
@@ -120,7 +120,11 @@ def _encode_png(args):
     from low_level_feature_extraction_amd import synth
 
     b = io.BytesIO()
-    Image.fromarray(synth.synth_numpy(i, h, w, seed=seed)[:, :, ::-1]).save(b, "PNG")
+    im = Image.fromarray(synth.synth_numpy(i, h, w, seed=seed)[:, :, ::-1])
+    if fmt == "JPEG":
+        im.save(b, "JPEG", quality=85)
+    else:
+        im.save(b, fmt)
     return b.getvalue()
 
 
@@ -153,16 +157,16 @@ def e2e_host(be, imgs_dev, feats, steps, seed, index_base):
                       f"H2D + full GPU path per batch, two batches in flight (llfe_submit_batch / llfe_collect_batch)"}
 
 
-def e2e_png(be, B, H, W, feats, steps, distinct, seed):
-    """End-to-end from PNG bytes: host decode on the decode
-    thread pool, double-buffered against the GPU (batch k+1 decodes while batch k runs).
-    Reported beside `value`, never as it."""
+def e2e_png(be, B, H, W, feats, steps, distinct, seed, fmt="PNG"):
+    """End-to-end from encoded bytes (PNG, or JPEG quality 85):
+    host decode on the decode thread pool, double-buffered against the GPU (batch k+1
+    decodes while batch k runs).  Reported beside `value`, never as it."""
     from concurrent.futures import ThreadPoolExecutor
 
     from low_level_feature_extraction_amd import decode
 
     with ThreadPoolExecutor(max_workers=min(distinct, decode.default_decode_threads())) as ex:
-        pngs = list(ex.map(_encode_png, [(i, H, W, seed) for i in range(distinct)]))
+        pngs = list(ex.map(_encode, [(i, H, W, seed, fmt) for i in range(distinct)]))
     blobs = [pngs[i % distinct] for i in range(B)]
     threads = decode.default_decode_threads()
     t = time.perf_counter()
@@ -181,9 +185,10 @@ def e2e_png(be, B, H, W, feats, steps, distinct, seed):
     mb = sum(len(p) for p in pngs) / distinct / 2**20
     return {"value": round(B * steps / dt, 2), "unit": "images/s", "decode_threads": threads,
             "decode_ms_per_image_per_thread": round(dec_ms, 2),
-            "sample": f"{steps} x {B} PNG-encoded {W}x{H} synthetic images ({distinct} distinct, {mb:.1f} MiB each), "
-                      f"decoded on the host (libllfe PNG decoder, cv2.imdecode IMREAD_COLOR semantics) into host batches, "
-                      f"then the full GPU path incl. H2D"}
+            "bound": f"host decode on {threads} threads = this rank's usable cores / LOCAL_WORLD_SIZE",
+            "sample": f"{steps} x {B} {fmt}-encoded {W}x{H} synthetic images ({distinct} distinct, {mb:.2f} MiB each), "
+                      f"decoded on the host (libllfe {fmt} decoder, cv2.imdecode IMREAD_COLOR semantics) into host "
+                      f"batches, then the full GPU path incl. H2D"}
 
 
 def _config_name(B, H, W, feats, pre):
@@ -217,6 +222,7 @@ def main():
     ap.add_argument("--e2e-host-steps", type=int, default=3, help="0 disables the decoded-host-array line")
     ap.add_argument("--seed", type=int, default=2025)
     ap.add_argument("--e2e-png-steps", type=int, default=2, help="0 disables the PNG end-to-end line")
+    ap.add_argument("--e2e-jpeg-steps", type=int, default=2, help="0 disables the JPEG end-to-end line")
     ap.add_argument("--per-class-steps", type=int, default=2,
                     help="steps of an all-ui and an all-photo batch (SURVEY.md 8d per-class throughput); 0 disables")
     ap.add_argument("--contours", choices=["auto", "host", "gpu"], default="auto",
@@ -389,26 +395,28 @@ def main():
         workers = args.cpu_workers or usable_cores()
         cpu = cpu_baseline(args.cpu_images or 2 * workers, H, W, workers)
 
-    def all_ranks(line):
-        """Whole-job rate of an e2e line every rank ran at once: images of all ranks over
-        the slowest rank's time."""
+    def all_ranks(line, steps):
+        """Whole-job rate of an e2e line every rank ran at once (`steps` batches of B per
+        rank): images of all ranks over the slowest rank's time."""
         if line is None or world == 1:
             return line
-        t = B * (args.e2e_host_steps if "h2d_gbs" in line else args.e2e_png_steps) / line["value"]
+        t = B * steps / line["value"]
         line = dict(line)
-        line["value"] = round(B * world * (args.e2e_host_steps if "h2d_gbs" in line else args.e2e_png_steps) /
-                              shard.max_over_ranks(t, device=coll_dev), 2)
+        line["value"] = round(B * world * steps / shard.max_over_ranks(t, device=coll_dev), 2)
         line["per_rank"] = True
         return line
 
     barrier()
     e2e_h = None
     if args.e2e_host_steps > 0:
-        e2e_h = all_ranks(e2e_host(be, imgs, feats, args.e2e_host_steps, args.seed, base))
+        e2e_h = all_ranks(e2e_host(be, imgs, feats, args.e2e_host_steps, args.seed, base), args.e2e_host_steps)
     barrier()
-    e2e = None
+    e2e = e2e_j = None
     if args.e2e_png_steps > 0:  # every rank decodes its own shard with its core share
-        e2e = all_ranks(e2e_png(be, B, H, W, feats, args.e2e_png_steps, 8, args.seed))
+        e2e = all_ranks(e2e_png(be, B, H, W, feats, args.e2e_png_steps, 8, args.seed), args.e2e_png_steps)
+    barrier()
+    if args.e2e_jpeg_steps > 0:
+        e2e_j = all_ranks(e2e_png(be, B, H, W, feats, args.e2e_jpeg_steps, 8, args.seed, fmt="JPEG"), args.e2e_jpeg_steps)
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -451,6 +459,7 @@ def main():
         "cpu_baseline": cpu,
         "e2e_host": e2e_h,
         "e2e_png": e2e,
+        "e2e_jpeg": e2e_j,
     }
     print(json.dumps(out))
     if dist is not None:

@@ -4,7 +4,7 @@
 # by the drop-in tests.
 set -u -o pipefail
 mkdir -p gpurun_out/configs
-B="python bench.py --cpu-baseline off --e2e-png-steps 0 --e2e-host-steps 0 --per-class-steps 0 --steps 4 --warmup 2"
+B="python bench.py --cpu-baseline off --e2e-png-steps 0 --e2e-jpeg-steps 0 --e2e-host-steps 0 --per-class-steps 0 --steps 4 --warmup 2"
 timeout -k 10 300 $B --batch 256 --features colors > gpurun_out/configs/c1_colors_256.json &&
 timeout -k 10 300 $B --batch 256 --features colors,shapes > gpurun_out/configs/c2_colors_shapes_256.json &&
 timeout -k 10 300 $B --batch 512 > gpurun_out/configs/c3_full_512.json &&

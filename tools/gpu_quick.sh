@@ -7,7 +7,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout
 rc=$?
 tail -25 gpurun_out/gpu_quick.log
 if [ $rc -ne 0 ]; then echo "pytest exit $rc: stopping"; exit $rc; fi
-timeout -k 10 600 python bench.py --cpu-baseline off --e2e-png-steps 0 --per-class-steps 0 "$@" > gpurun_out/bench_quick.json 2> gpurun_out/bench_quick.err
+timeout -k 10 600 python bench.py --cpu-baseline off --e2e-png-steps 0 --e2e-jpeg-steps 0 --per-class-steps 0 "$@" > gpurun_out/bench_quick.json 2> gpurun_out/bench_quick.err
 brc=$?
 python3 - <<'PY'
 import json
