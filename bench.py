@@ -229,9 +229,11 @@ def main():
                     help="where findContours + the shape loop run: the host pool from the copied-back mask "
                          "(overlaps k-means), the GPU (contours_gpu.hip), or auto (the library's choice: "
                          "host unless the rank has < 8 host cores)")
-    ap.add_argument("--pipeline", choices=["on", "off"], default="off",
-                    help="on: two batches in flight (submit / collect; measured +1 %% images/s, and the "
-                         "overlap stretches the event-timed k-means span); off: one llfe_process_batch per step")
+    ap.add_argument("--pipeline", choices=["on", "off"], default="on",
+                    help="on: a serving loop with two batches in flight (llfe_submit_batch / "
+                         "llfe_collect_batch: batch k+1's front kernels fill the tail of batch k's k-means; "
+                         "kernel timings then come from the same steps run one batch at a time); "
+                         "off: one llfe_process_batch per step")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -298,7 +300,9 @@ def main():
     pipelined = args.pipeline == "on"
     run_steps(args.warmup, args.seed + 1000, pipelined)
     barrier()
-    be.set_profiling(True)
+    # hipEvent kernel timings: in the one-batch-at-a-time steps only (two batches in flight
+    # overlap, so an event-timed span would include the other batch's kernels)
+    be.set_profiling(not pipelined)
     t0 = time.perf_counter()
     n_shapes = run_steps(args.steps, args.seed, pipelined)
     torch.cuda.synchronize()
@@ -306,10 +310,11 @@ def main():
     barrier()
     dt = shard.max_over_ranks(t1 - t0, device=coll_dev)
     stats = be.kernel_stats()
-    # the same steps one batch at a time (llfe_process_batch), for reference
+    # the same steps one batch at a time (llfe_process_batch): the reference rate and,
+    # when pipelined, the kernel timings
     dt_sync = None
     if pipelined:
-        be.set_profiling(False)
+        be.set_profiling(True)
         barrier()
         ts0 = time.perf_counter()
         run_steps(args.steps, args.seed, False)
@@ -317,6 +322,9 @@ def main():
         ts1 = time.perf_counter()
         barrier()
         dt_sync = shard.max_over_ranks(ts1 - ts0, device=coll_dev)
+        stats = be.kernel_stats()
+        be.set_profiling(False)
+    dt_kernels = dt_sync if pipelined else dt  # the steps the kernel timings come from
     # one extra, untimed step with every kernel in order on one stream: isolated kernel
     # durations for the secondary rooflines (in the timed steps the shapes kernels share
     # the GPU with the colour front, which stretches their event-timed spans)
@@ -365,7 +373,7 @@ def main():
              "bytes_per_launch": bpl, "avg_launch_ms": round(avg_ms, 4)}
         if name in VALU_INSTS and avg_ms > 0:
             # PMC SQ_INSTS_VALU per launch (profiles/traffic_latest.json) over the launch's
-            # VALU issue capacity at 2.4 GHz: how close the kernel is to its compute bound
+            # VALU issue capacity (VALU_SLOTS_PER_S): how close the kernel is to its compute bound
             r["valu_busy"] = round(VALU_INSTS[name] / (VALU_SLOTS_PER_S * avg_ms * 1e-3), 3)
         return r
 
@@ -373,11 +381,11 @@ def main():
     for name, st in stats.items():
         r = roof(name)
         kernels[name] = {"launches": st["launches"], "avg_ms": r["avg_launch_ms"],
-                         "share_of_step": round(st["total_ms"] / (dt * 1e3), 4),
+                         "share_of_step": round(st["total_ms"] / (dt_kernels * 1e3), 4),
                          "gbs": r["achieved"] if st["bytes"] else None, "frac": r["frac"] if st["bytes"] else None}
     # `roofline` is the dominant kernel's (largest total time); k_kmeans' algorithmic
-    # bytes are 16 B per cube-table entry per pass (K k-means++ passes + one per Lloyd
-    # iteration, counted on the device) + 4 B per colour of the selection scans.
+    # bytes are SURVEY.md 8d's 4U per fused multi-attempt pass x (K k-means++ passes + the
+    # longest attempt's Lloyd sweeps), k_kmeans_finalize.
     dominant = max(stats, key=lambda k: stats[k]["total_ms"]) if stats else None
     roofline = roof(dominant) if dominant else None
     roofline_stencil = None

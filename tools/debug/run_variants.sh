@@ -7,7 +7,7 @@ L=low_level_feature_extraction_amd/libllfe.so
 cp $L /tmp/libllfe_keep.so
 for v in tools/debug/variants/libllfe_*.so; do
     cp "$v" $L
-    timeout -k 10 300 python bench.py --cpu-baseline off --e2e-png-steps 0 --e2e-jpeg-steps 0 --e2e-host-steps 0 --per-class-steps 0 --steps 5 --warmup 2 "$@" \
+    timeout -k 10 300 python bench.py --cpu-baseline off --e2e-png-steps 0 --e2e-jpeg-steps 0 --e2e-host-steps 0 --per-class-steps 0 --pipeline off --steps 5 --warmup 2 "$@" \
         > gpurun_out/var.json 2> gpurun_out/var.err || { echo "$v failed"; tail -3 gpurun_out/var.err; cp /tmp/libllfe_keep.so $L; exit 1; }
     python3 -c "
 import json,sys

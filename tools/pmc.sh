@@ -9,7 +9,7 @@ P=/tmp/llfe_pmc_$TAG
 OUT=gpurun_out/pmc_$TAG
 rm -rf "$P"; mkdir -p "$OUT"
 timeout -k 10 600 rocprofv3 --pmc $COUNTERS --kernel-trace --kernel-include-regex "$REGEX" -d $P -o run \
-    --output-format csv -- python3 bench.py --steps 2 --warmup 1 --cpu-baseline off --per-class-steps 0 "$@" \
+    --output-format csv -- python3 bench.py --steps 2 --warmup 1 --cpu-baseline off --per-class-steps 0 --pipeline off "$@" \
     > "$OUT/bench.json" 2> "$OUT/err.txt" || { echo "pmc pass failed"; tail -5 "$OUT/err.txt"; exit 1; }
 python3 - "$P/run_counter_collection.csv" > "$OUT/summary.txt" <<'EOF'
 import csv, sys

@@ -10,7 +10,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 P=/tmp/llfe_prof_$TAG
 rm -rf "$P"
-BENCH="bench.py --steps 3 --warmup 1 --cpu-baseline off --e2e-png-steps 0 --e2e-jpeg-steps 0 --e2e-host-steps 0 --per-class-steps 0"
+BENCH="bench.py --steps 3 --warmup 1 --cpu-baseline off --e2e-png-steps 0 --e2e-jpeg-steps 0 --e2e-host-steps 0 --per-class-steps 0 --pipeline off"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $P/trace -o run --output-format csv -- python3 $BENCH \
     > "$OUT/bench_under_trace.json" 2> "$OUT/trace.err" || { echo "trace pass failed"; tail -5 "$OUT/trace.err"; exit 1; }
 cp $P/trace/run_kernel_stats.csv "$OUT/kernel_stats.csv"
