@@ -563,28 +563,6 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
         __syncthreads();
         unsigned long long acc0 = 0, acc1 = 0, acc2 = 0, fails = 0;
         int Pcur = -1;
-        // undecided cubes' colours go through the wave's LDS ring (as in the Lloyd
-        // sweeps) and are summed 64 at a time
-        const uint32_t loff = lane_offset(lane);
-        uint32_t *stg = sm.stage[wid];
-        int head = 0, tail = 0;  // wave-uniform ring counters
-        auto sum_stage = [&](int count) {
-            __builtin_amdgcn_wave_barrier();
-            fails += (unsigned long long)count;
-            if (lane < count) {
-                const uint32_t kq = stg[(tail + lane) & (kStage - 1)];
-                const int x = unpack_r(kq), y = unpack_g(kq), z = unpack_b(kq);
-                const int D = dmin_chosen(x, y, z, ch, kk);
-                acc0 += (uint32_t)min(D, d2i(x, y, z, tx[0], ty[0], tz[0]));
-                acc1 += (uint32_t)min(D, d2i(x, y, z, tx[1], ty[1], tz[1]));
-                acc2 += (uint32_t)min(D, d2i(x, y, z, tx[2], ty[2], tz[2]));
-            }
-            tail += count;
-        };
-        auto flush_pk = [&]() {
-            while (head - tail >= 64) sum_stage(64);
-            if (head > tail) sum_stage(head - tail);
-        };
         // Round constants (wave-uniform).  Every test below is linear in the cube origin o:
         // with D_c(o) = |c|^2 - 2 o.c, d(o, c) = |o|^2 + D_c(o), so
         //   d(o, a) - d(o, b) = D_a(o) - D_b(o)          (never / always closer tests)
@@ -600,6 +578,35 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
         }
 #pragma unroll
         for (int j = 0; j < 3; j++) T2[j] = tx[j] * tx[j] + ty[j] * ty[j] + tz[j] * tz[j];
+        // undecided cubes' colours go through the wave's LDS ring (as in the Lloyd
+        // sweeps) and are summed 64 at a time
+        const uint32_t loff = lane_offset(lane);
+        uint32_t *stg = sm.stage[wid];
+        int head = 0, tail = 0;  // wave-uniform ring counters
+        auto sum_stage = [&](int count) {
+            __builtin_amdgcn_wave_barrier();
+            fails += (unsigned long long)count;
+            if (lane < count) {
+                // d(p, c) = |p|^2 + L_c(p), L_c(p) = |c|^2 - 2 p.c (exact integers): the
+                // |p|^2 term is common to D and every trial, so min(D, d(p, t)) =
+                // |p|^2 + min(min_m L_m, L_t) -- three multiply-adds per centre
+                const uint32_t kq = stg[(tail + lane) & (kStage - 1)];
+                const int x = unpack_r(kq), y = unpack_g(kq), z = unpack_b(kq);
+                const int p2 = __mul24(x, x) + __mul24(y, y) + __mul24(z, z);
+                int L = C2[0] - 2 * (__mul24(x, ch.x[0]) + __mul24(y, ch.y[0]) + __mul24(z, ch.z[0]));
+#pragma unroll
+                for (int m = 1; m < kMaxK; m++)
+                    if (m < kk) L = min(L, C2[m] - 2 * (__mul24(x, ch.x[m]) + __mul24(y, ch.y[m]) + __mul24(z, ch.z[m])));
+                acc0 += (uint32_t)(p2 + min(L, T2[0] - 2 * (__mul24(x, tx[0]) + __mul24(y, ty[0]) + __mul24(z, tz[0]))));
+                acc1 += (uint32_t)(p2 + min(L, T2[1] - 2 * (__mul24(x, tx[1]) + __mul24(y, ty[1]) + __mul24(z, tz[1]))));
+                acc2 += (uint32_t)(p2 + min(L, T2[2] - 2 * (__mul24(x, tx[2]) + __mul24(y, ty[2]) + __mul24(z, tz[2]))));
+            }
+            tail += count;
+        };
+        auto flush_pk = [&]() {
+            while (head - tail >= 64) sum_stage(64);
+            if (head > tail) sum_stage(head - tail);
+        };
         if (tid < kMaxK * kMaxK) {  // Mkk[m][k] = 6 sum max(c_m - c_k, 0)
             const int m = tid / kMaxK, k2 = tid % kMaxK;
             sm.marg[tid] = 6 * (max(sm.icc[m][0] - sm.icc[k2][0], 0) + max(sm.icc[m][1] - sm.icc[k2][1], 0) +
@@ -651,8 +658,10 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
                     // argmin_m |q - c_m|^2 = argmin_m (D_m(o) - 3 sum(c_m)), first minimum
                     int Dc[kMaxK];
 #pragma unroll
-                    for (int m = 0; m < kMaxK; m++)
-                        Dc[m] = C2[m] - 2 * (__mul24(g.ox, ch.x[m]) + __mul24(g.oy, ch.y[m]) + __mul24(g.oz, ch.z[m]));
+                    for (int m = 0; m < kMaxK; m++) {  // (only the kk chosen centres are read)
+                        Dc[m] = 0;
+                        if (m < kk) Dc[m] = C2[m] - 2 * (__mul24(g.ox, ch.x[m]) + __mul24(g.oy, ch.y[m]) + __mul24(g.oz, ch.z[m]));
+                    }
                     int k = 0, bd = Dc[0] - S3[0];
 #pragma unroll
                     for (int m = 1; m < kMaxK; m++) {
