@@ -187,43 +187,44 @@ __device__ __forceinline__ bool sobel4(uint32_t b0, uint32_t b1, uint32_t b2, ui
 
 // Canny NMS + double threshold of the lane's 4 pixels of the middle magnitude row;
 // a = above, m = middle, b = below (lo = cols c0 c1, hi = c2 c3, m | dir << 12).  Called
-// by the whole wave (DPP), branch-free per pixel.
+// by the whole wave (DPP).  In packed u16 on the (c0, c1) and (c2, c3) pairs: the four
+// directions' thresholds -- keep iff m >= T with
+//   dir 0 (left / right):           T = max(left + 1, right)
+//   dir 1 (up / down):              T = max(up + 1, down)
+//   dir 2 (up-right / down-left):   T = max(up-right, down-left) + 1
+//   dir 3 (up-left / down-right):   T = max(up-left, down-right) + 1
+// (the second neighbour takes >= for 0 / 1, > for the diagonals), then the pixel's own
+// threshold picked by v_bfi on its two direction bits, max'ed with LOW + 1, and the class
+// from saturating subtractions -- no per-pixel unpacking, compares or selects.
+__device__ __forceinline__ uint32_t bsel(uint32_t m, uint32_t a, uint32_t b) { return (a & m) | (b & ~m); }
 __device__ __forceinline__ uint32_t nms4(uint32_t alo, uint32_t ahi, uint32_t mlo, uint32_t mhi, uint32_t blo,
                                          uint32_t bhi) {
-    constexpr int LOW = 50, HIGH = 150;
-    const uint32_t aL = from_left(ahi), aR = from_right(alo);
-    const uint32_t mL = from_left(mhi), mR = from_right(mlo);
-    const uint32_t bL = from_left(bhi), bR = from_right(blo);
-    // magnitudes of columns -1 .. 4 (index c + 1)
-    auto cols = [](uint32_t L, uint32_t lo, uint32_t hi, uint32_t R, int *v) {
-        v[0] = (int)((L >> 16) & 4095u);
-        v[1] = (int)(lo & 4095u);
-        v[2] = (int)((lo >> 16) & 4095u);
-        v[3] = (int)(hi & 4095u);
-        v[4] = (int)((hi >> 16) & 4095u);
-        v[5] = (int)(R & 4095u);
+    constexpr uint32_t MK = 0x0FFF0FFFu;
+    const uint32_t A0 = alo & MK, A1 = ahi & MK, M0 = mlo & MK, M1 = mhi & MK, B0 = blo & MK, B1 = bhi & MK;
+    // the neighbour lanes' dwords: cols (c-2, c-1) from the left, (c+4, c+5) from the right
+    const uint32_t Ap = from_left(A1), An = from_right(A0), Mp = from_left(M1), Mn = from_right(M0),
+                   Bp = from_left(B1), Bn = from_right(B0);
+    const u16x2 one = {1, 1}, low1 = {51, 51}, high1 = {151, 151};
+    auto cls2 = [&](uint32_t Ac, uint32_t AL, uint32_t AR, uint32_t Mc, uint32_t ML, uint32_t MR, uint32_t Bc,
+                    uint32_t BL, uint32_t BR, uint32_t mraw) {
+        const u16x2 t0 = __builtin_elementwise_max(U(ML) + one, U(MR));
+        const u16x2 t1 = __builtin_elementwise_max(U(Ac) + one, U(Bc));
+        const u16x2 t2 = __builtin_elementwise_max(U(AR), U(BL)) + one;
+        const u16x2 t3 = __builtin_elementwise_max(U(AL), U(BR)) + one;
+        const u16x2 z = {0, 0};
+        const uint32_t m0 = W32(z - U((mraw >> 12) & 0x00010001u));  // dir bit 0 -> 0xffff per half
+        const uint32_t m1 = W32(z - U((mraw >> 13) & 0x00010001u));  // dir bit 1
+        const uint32_t T = bsel(m1, bsel(m0, W32(t3), W32(t2)), bsel(m0, W32(t1), W32(t0)));
+        const u16x2 Tm = __builtin_elementwise_max(U(T), low1);
+        const u16x2 nk = __builtin_elementwise_min(__builtin_elementwise_sub_sat(Tm, U(Mc)), one);    // 1: suppressed
+        const u16x2 ns = __builtin_elementwise_min(__builtin_elementwise_sub_sat(high1, U(Mc)), one); // 1: not strong
+        const uint32_t k2 = (W32(nk) | W32(ns)) ^ 0x00010001u;  // kept and strong
+        return W32(nk) | (k2 + k2);                             // 1 suppressed, 2 strong, 0 weak
     };
-    int A[6], M[6], Bv[6];
-    cols(aL, alo, ahi, aR, A);
-    cols(mL, mlo, mhi, mR, M);
-    cols(bL, blo, bhi, bR, Bv);
-    const uint32_t dirs[4] = {(mlo >> 12) & 15u, mlo >> 28, (mhi >> 12) & 15u, mhi >> 28};
-    uint32_t o = 0;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const int m = M[j + 1];
-        // neighbours by direction: 0 left / right, 1 up / down, 2 up-right / down-left,
-        // 3 up-left / down-right -- selected on the two bits of dir (equality chains on
-        // dir become switch tables in scratch memory)
-        const bool b0 = dirs[j] & 1u, b1 = dirs[j] & 2u;
-        const int n1 = b1 ? (b0 ? A[j] : A[j + 2]) : (b0 ? A[j + 1] : M[j]);
-        const int n2 = b1 ? (b0 ? Bv[j + 2] : Bv[j]) : (b0 ? Bv[j + 1] : M[j + 2]);
-        // the second neighbour takes >= for 0 / 1 and > for the diagonals
-        const bool keep = m > LOW && m > n1 && m + (b1 ? 0 : 1) > n2;
-        const uint32_t c = keep ? (m > HIGH ? 2u : 0u) : 1u;
-        o |= c << (8 * j);
-    }
-    return o;
+    const uint32_t mid_a = mid16(A0, A1), mid_m = mid16(M0, M1), mid_b = mid16(B0, B1);
+    const uint32_t c0 = cls2(A0, mid16(Ap, A0), mid_a, M0, mid16(Mp, M0), mid_m, B0, mid16(Bp, B0), mid_b, mlo);
+    const uint32_t c1 = cls2(A1, mid_a, mid16(A1, An), M1, mid_m, mid16(M1, Mn), B1, mid_b, mid16(B1, Bn), mhi);
+    return __builtin_amdgcn_perm(c1, c0, 0x06040200u);
 }
 
 // CV_32F Gauss11 row pass (s = 0; s = fma(x[k-5], k[k], s) left -> right) of the lane's
