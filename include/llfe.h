@@ -206,6 +206,13 @@ int llfe_gray_blur5(llfe_ctx *ctx, const uint8_t *bgr, uint8_t *blurred, int32_t
 /* dilate(Canny(blur5(gray), 50, 150), ones(3,3)) as 0/255 u8 (shape pyc @L6-30) */
 int llfe_shape_mask(llfe_ctx *ctx, const uint8_t *bgr, uint8_t *mask, int32_t n, int32_t h, int32_t w,
                     llfe_stream stream);
+/* Canny(blur5(gray), 50, 150) as 0/255 u8: the shape mask before its dilation */
+int llfe_canny(llfe_ctx *ctx, const uint8_t *bgr, uint8_t *edges, int32_t n, int32_t h, int32_t w,
+               llfe_stream stream);
+/* dilate(src, ones(3,3)) of n h x w u8 images (any values; out-of-image never wins);
+ * src and dst must not alias */
+int llfe_dilate3(llfe_ctx *ctx, const uint8_t *src, uint8_t *dst, int32_t n, int32_t h, int32_t w,
+                 llfe_stream stream);
 /* Canny NMS classes before hysteresis: 0 weak, 1 suppressed, 2 strong */
 int llfe_edge_classes(llfe_ctx *ctx, const uint8_t *bgr, uint8_t *classes, int32_t n, int32_t h, int32_t w,
                       llfe_stream stream);

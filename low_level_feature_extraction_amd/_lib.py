@@ -124,6 +124,8 @@ SIGNATURES = {
     "llfe_gray_blur5": (C.c_int, [_vp, _vp, _vp, _i32, _i32, _i32, _vp]),
     "llfe_shape_mask": (C.c_int, [_vp, _vp, _vp, _i32, _i32, _i32, _vp]),
     "llfe_edge_classes": (C.c_int, [_vp, _vp, _vp, _i32, _i32, _i32, _vp]),
+    "llfe_canny": (C.c_int, [_vp, _vp, _vp, _i32, _i32, _i32, _vp]),
+    "llfe_dilate3": (C.c_int, [_vp, _vp, _vp, _i32, _i32, _i32, _vp]),
     "llfe_font_binary": (C.c_int, [_vp, _vp, _vp, _i32, _i32, _i32, _vp]),
     "llfe_text_binary": (C.c_int, [_vp, _vp, _i32, _i32, _i32, _vp, C.POINTER(_i32), _vp]),
     "llfe_text_size": (C.c_int, [_i32, _i32, C.POINTER(_i32), C.POINTER(_i32)]),

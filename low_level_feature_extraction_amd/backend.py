@@ -389,6 +389,28 @@ class Backend:
         self._chk(self._lib.llfe_shape_mask(self.ctx, x.data_ptr(), out.data_ptr(), n, h, w, self._stream(x)))
         return out
 
+    def canny(self, images):
+        """Canny(blur5(gray), 50, 150) of the shapes path, before its dilation: n x h x w
+        u8 0/255 device tensor."""
+        torch = _torch()
+        x = self._dev_batch(images)
+        n, h, w, _ = x.shape
+        out = torch.empty((n, h, w), dtype=torch.uint8, device=x.device)
+        self._chk(self._lib.llfe_canny(self.ctx, x.data_ptr(), out.data_ptr(), n, h, w, self._stream(x)))
+        return out
+
+    def dilate3(self, masks):
+        """dilate(masks, ones(3, 3)) of an n x h x w (or h x w) u8 batch on the GPU."""
+        torch = _torch()
+        x = masks if _is_torch(masks) else torch.from_numpy(np.ascontiguousarray(masks, np.uint8))
+        x = x.to(f"cuda:{self.device}").contiguous()
+        if x.dim() == 2:
+            x = x[None]
+        n, h, w = x.shape
+        out = torch.empty_like(x)
+        self._chk(self._lib.llfe_dilate3(self.ctx, x.data_ptr(), out.data_ptr(), n, h, w, self._stream(x)))
+        return out
+
     def find_contours_gpu(self, mask: np.ndarray) -> list:
         """findContours(RETR_EXTERNAL, CHAIN_APPROX_SIMPLE) of one host u8 mask on the GPU
         contour path (the one llfe_process_batch uses) -> list of (n,2) int32, cv2 order."""

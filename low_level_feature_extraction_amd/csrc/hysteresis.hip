@@ -308,12 +308,45 @@ __global__ __launch_bounds__(NT) void k_bits_dilate(const uint64_t *__restrict__
     }
 }
 
-}  // namespace
+// Canny edges without the dilation (llfe_canny): packed edge words -> 0 / 255 bytes
+__global__ __launch_bounds__(NT) void k_bits_unpack(const uint64_t *__restrict__ eb, int n, int H, int W,
+                                                    uint8_t *__restrict__ mask_u8) {
+    const int wpr = (W + 63) / 64;
+    const size_t total = (size_t)n * H * wpr;
+    for (size_t i = (size_t)blockIdx.x * NT + threadIdx.x; i < total; i += (size_t)gridDim.x * NT) {
+        const int k = (int)(i % wpr);
+        const size_t row = i / wpr;
+        const uint64_t d = eb[i];
+        uint8_t *m = mask_u8 + row * W + (size_t)k * 64;
+        const int nx = min(64, W - k * 64);
+        for (int b = 0; b < nx; b++) m[b] = ((d >> b) & 1ull) ? 255 : 0;
+    }
+}
 
-size_t hysteresis_ids(int n, int h, int w) { return (size_t)n * tiles_x(w) * tiles_y(h) * TP; }
+// dilate(src, ones(3, 3)) of n u8 images (any values): 3x3 max, the border never wins
+// (llfe_dilate3; the shapes path dilates the packed edge bits in k_bits_dilate)
+__global__ __launch_bounds__(NT) void k_dilate3_u8(const uint8_t *__restrict__ src, int n, int H, int W,
+                                                   uint8_t *__restrict__ dst) {
+    const size_t total = (size_t)n * H * W;
+    for (size_t i = (size_t)blockIdx.x * NT + threadIdx.x; i < total; i += (size_t)gridDim.x * NT) {
+        const int x = (int)(i % W);
+        const size_t row = i / W;
+        const int y = (int)(row % H);
+        int m = 0;
+#pragma unroll
+        for (int dy = -1; dy <= 1; dy++) {
+            if ((unsigned)(y + dy) >= (unsigned)H) continue;
+            const uint8_t *r = src + (size_t)((long long)row + dy) * W;
+#pragma unroll
+            for (int dx = -1; dx <= 1; dx++)
+                if ((unsigned)(x + dx) < (unsigned)W) m = max(m, (int)r[x + dx]);
+        }
+        dst[i] = (uint8_t)m;
+    }
+}
 
-hipError_t launch_hysteresis_dilate(const uint8_t *cls, int n, int h, int w, const HystWork &wk, uint64_t *bits,
-                                    uint8_t *mask_u8, hipStream_t s) {
+// the connected-component passes up to the packed edge words wk.ebits
+hipError_t launch_ccl(const uint8_t *cls, int n, int h, int w, const HystWork &wk, hipStream_t s) {
     const int ntx = tiles_x(w), nty = tiles_y(h), ntiles = ntx * nty;
     dim3 grid(ntiles, n);
     const size_t words = (size_t)n * h * words_per_row(w);
@@ -331,6 +364,35 @@ hipError_t launch_hysteresis_dilate(const uint8_t *cls, int n, int h, int w, con
                        wk.sroot, wk.tstrong);
     hipLaunchKernelGGL(k_ccl_edge, lgrid, dim3(NT), 0, s, cls, wk.lab, h, w, ntx, nty, wk.tlist, wk.tcount, wk.tstrong,
                        wk.ebits);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+size_t hysteresis_ids(int n, int h, int w) { return (size_t)n * tiles_x(w) * tiles_y(h) * TP; }
+
+hipError_t launch_canny_edges(const uint8_t *cls, int n, int h, int w, const HystWork &wk, uint8_t *edges_u8,
+                              hipStream_t s) {
+    hipError_t e = launch_ccl(cls, n, h, w, wk, s);
+    if (e != hipSuccess) return e;
+    const size_t words = (size_t)n * h * words_per_row(w);
+    const int blocks = (int)std::min<size_t>((words + NT - 1) / NT, 65536);
+    hipLaunchKernelGGL(k_bits_unpack, dim3(blocks), dim3(NT), 0, s, wk.ebits, n, h, w, edges_u8);
+    return hipGetLastError();
+}
+
+hipError_t launch_dilate3_u8(const uint8_t *src, int n, int h, int w, uint8_t *dst, hipStream_t s) {
+    const size_t total = (size_t)n * h * w;
+    const int blocks = (int)std::min<size_t>((total + NT - 1) / NT, 65536);
+    if (total) hipLaunchKernelGGL(k_dilate3_u8, dim3(blocks), dim3(NT), 0, s, src, n, h, w, dst);
+    return hipGetLastError();
+}
+
+hipError_t launch_hysteresis_dilate(const uint8_t *cls, int n, int h, int w, const HystWork &wk, uint64_t *bits,
+                                    uint8_t *mask_u8, hipStream_t s) {
+    hipError_t e = launch_ccl(cls, n, h, w, wk, s);
+    if (e != hipSuccess) return e;
+    const size_t words = (size_t)n * h * words_per_row(w);
     const int blocks = (int)std::min<size_t>((words + NT - 1) / NT, 65536);
     hipLaunchKernelGGL(k_bits_dilate, dim3(blocks), dim3(NT), 0, s, wk.ebits, n, h, w, bits, mask_u8);
     return hipGetLastError();

@@ -486,8 +486,8 @@ int stage_input(llfe_ctx *ctx, Work &W, const llfe_batch *b, int i0, int n, cons
     return LLFE_OK;
 }
 
-// Canny hysteresis (connected components) + dilate + pack of W.d_cls.
-int run_hysteresis_dilate(llfe_ctx *ctx, Work &W, int n, int h, int w, uint64_t *bits, uint8_t *mask_u8, hipStream_t s) {
+// The hysteresis workspace of an n x h x w batch, grown on demand.
+int hyst_work(llfe_ctx *ctx, Work &W, int n, int h, int w, HystWork *out) {
     const size_t ids = hysteresis_ids(n, h, w);
     const size_t tiles = (size_t)tiles_x(w) * tiles_y(h) * n;
     HIPCHK(ctx, W.d_lab.ensure((size_t)n * h * w));
@@ -498,8 +498,16 @@ int run_hysteresis_dilate(llfe_ctx *ctx, Work &W, int n, int h, int w, uint64_t 
     HIPCHK(ctx, W.d_tstrong.ensure(tiles * (kTileW * kTileH / 32)));
     HIPCHK(ctx, W.d_ebits.ensure((size_t)n * h * words_per_row(w)));
     HIPCHK(ctx, W.d_tlist.ensure(tiles + 1));
-    HystWork wk{W.d_lab.p,     W.d_parent.p, W.d_sroot.p,       W.d_roots.p,   W.d_nroots.p,
-                W.d_tstrong.p, W.d_ebits.p,  W.d_tlist.p + 1, W.d_tlist.p};
+    *out = HystWork{W.d_lab.p,     W.d_parent.p, W.d_sroot.p,       W.d_roots.p,   W.d_nroots.p,
+                    W.d_tstrong.p, W.d_ebits.p,  W.d_tlist.p + 1, W.d_tlist.p};
+    return LLFE_OK;
+}
+
+// Canny hysteresis (connected components) + dilate + pack of W.d_cls.
+int run_hysteresis_dilate(llfe_ctx *ctx, Work &W, int n, int h, int w, uint64_t *bits, uint8_t *mask_u8, hipStream_t s) {
+    HystWork wk;
+    const int rc = hyst_work(ctx, W, n, h, w, &wk);
+    if (rc) return rc;
     TIMED(ctx, s, "k_hysteresis_dilate", (double)n * h * w * (1 + 2 + 1 + 2 + 3 * 0.125),
           launch_hysteresis_dilate(W.d_cls.p, n, h, w, wk, bits, mask_u8, s));
     return LLFE_OK;
@@ -1365,6 +1373,34 @@ int llfe_shape_mask(llfe_ctx *ctx, const uint8_t *bgr, uint8_t *mask, int32_t n,
     if (rc) return rc;
     HIPCHK(ctx, hipStreamSynchronize(s));
     ctx->prof.collect();
+    return LLFE_OK;
+}
+
+// Canny(blur5(gray), 50, 150) of the shapes path (shape pyc @L6-30) before the
+// dilation: the stencil's edge classes, then the hysteresis components, as 0 / 255
+int llfe_canny(llfe_ctx *ctx, const uint8_t *bgr, uint8_t *edges, int32_t n, int32_t h, int32_t w,
+               llfe_stream stream) {
+    if (!ctx || !valid_dims(n, h, w) || !bgr || !edges) return LLFE_ERR_INVALID;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = (hipStream_t)stream;
+    Work &W = ctx->ws[0];
+    HIPCHK(ctx, W.d_cls.ensure((size_t)n * h * w));
+    HIPCHK(ctx, launch_stencil(bgr, n, h, w, W.d_cls.p, nullptr, nullptr, nullptr, nullptr, ctx->sp, s));
+    HystWork wk;
+    const int rc = hyst_work(ctx, W, n, h, w, &wk);
+    if (rc) return rc;
+    HIPCHK(ctx, launch_canny_edges(W.d_cls.p, n, h, w, wk, edges, s));
+    HIPCHK(ctx, hipStreamSynchronize(s));
+    return LLFE_OK;
+}
+
+// dilate(src, ones(3, 3)) of the shapes path (shape pyc @L6-30) on n u8 images
+int llfe_dilate3(llfe_ctx *ctx, const uint8_t *src, uint8_t *dst, int32_t n, int32_t h, int32_t w,
+                 llfe_stream stream) {
+    if (!ctx || !valid_dims(n, h, w) || !src || !dst || src == dst) return LLFE_ERR_INVALID;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    HIPCHK(ctx, launch_dilate3_u8(src, n, h, w, dst, (hipStream_t)stream));
+    HIPCHK(ctx, hipStreamSynchronize((hipStream_t)stream));
     return LLFE_OK;
 }
 

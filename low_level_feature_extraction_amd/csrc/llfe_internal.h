@@ -60,6 +60,11 @@ struct HystWork {
 size_t hysteresis_ids(int n, int h, int w);
 hipError_t launch_hysteresis_dilate(const uint8_t *cls, int n, int h, int w, const HystWork &wk, uint64_t *bits,
                                     uint8_t *mask_u8, hipStream_t s);
+// the same connected components without the dilation: Canny's 0 / 255 edges (llfe_canny)
+hipError_t launch_canny_edges(const uint8_t *cls, int n, int h, int w, const HystWork &wk, uint8_t *edges_u8,
+                              hipStream_t s);
+// 3x3 dilate (max filter) of n u8 images (llfe_dilate3)
+hipError_t launch_dilate3_u8(const uint8_t *src, int n, int h, int w, uint8_t *dst, hipStream_t s);
 
 // External contours + shape records on the GPU (contours_gpu.hip).  Reuses the
 // hysteresis workspace (lab, parent, roots, nroots) once the dilated mask exists.

@@ -65,6 +65,35 @@ def test_shape_mask(backend, orc, h, w):
         assert np.array_equal(got[i], exp), f"mismatch {(got[i] != exp).sum()} px"
 
 
+@pytest.mark.parametrize("h,w", SIZES)
+def test_canny(backend, orc, h, w):
+    x = _imgs(h, w)
+    got = backend.canny(x).cpu().numpy()
+    for i in range(len(x)):
+        exp = orc.canny(orc.blur5(orc.bgr2gray(x[i])))
+        assert np.array_equal(got[i], exp), f"mismatch {(got[i] != exp).sum()} px"
+
+
+def test_canny_then_dilate_is_shape_mask(backend, orc):
+    x = np.stack([_smooth_random(300, 500, s) for s in range(2)])
+    edges = backend.canny(x)
+    for i in range(len(x)):
+        assert np.array_equal(edges[i].cpu().numpy(), orc.canny(orc.blur5(orc.bgr2gray(x[i]))))
+    assert np.array_equal(backend.dilate3(edges).cpu().numpy(), backend.shape_mask(x).cpu().numpy())
+
+
+@pytest.mark.parametrize("n,h,w", [(1, 1, 1), (2, 1, 9), (3, 7, 1), (2, 5, 7), (1, 64, 64), (3, 65, 130),
+                                   (2, 1080, 1920)])
+def test_dilate3(backend, orc, n, h, w):
+    rng = np.random.default_rng(n * 100000 + h * 100 + w)
+    vals = rng.integers(0, 256, (n, h, w), dtype=np.uint8)
+    sparse = np.where(rng.random((n, h, w)) < 0.02, 255, 0).astype(np.uint8)
+    for src in (vals, sparse):
+        got = backend.dilate3(src).cpu().numpy()
+        for i in range(n):
+            assert np.array_equal(got[i], orc.dilate3(src[i]))
+
+
 def test_shape_mask_smooth_random(backend, orc):
     # weak-edge heavy inputs exercise multi-launch hysteresis across tiles
     x = np.stack([_smooth_random(300, 500, s) for s in range(3)])
