@@ -140,6 +140,16 @@ def e2e_host(be, imgs_dev, feats, steps, seed, index_base):
         hb.copy_(imgs_dev.cpu())
     arrs = [hb.numpy() for hb in host]
     be.process(arrs[0][:2], feats, seed=seed)  # warm the host-input path
+    # the PCIe ceiling of this path: one plain pinned H2D copy of a batch (best of 3)
+    scratch = torch.empty_like(imgs_dev)
+    peak = 0.0
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        scratch.copy_(host[0], non_blocking=True)
+        torch.cuda.synchronize()
+        peak = max(peak, host[0].numel() / (time.perf_counter() - t) / 1e9)
+    del scratch
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     pending = []
@@ -153,6 +163,8 @@ def e2e_host(be, imgs_dev, feats, steps, seed, index_base):
     n, h, w = imgs_dev.shape[0], imgs_dev.shape[1], imgs_dev.shape[2]
     gb = n * h * w * 3 * steps / 1e9
     return {"value": round(n * steps / dt, 2), "unit": "images/s", "h2d_gbs": round(gb / dt, 2),
+            "pcie_h2d_peak_gbs": round(peak, 2), "frac_of_pcie": round(gb / dt / peak, 3),
+            "bound": "PCIe H2D (the batch's bytes at pcie_h2d_peak_gbs take longer than its kernels)",
             "sample": f"{steps} x {n} decoded {w}x{h} BGR arrays in pinned host memory (two alternating buffers), "
                       f"H2D + full GPU path per batch, two batches in flight (llfe_submit_batch / llfe_collect_batch)"}
 
@@ -219,7 +231,7 @@ def main():
     ap.add_argument("--preprocessing", default="auto", choices=["none", "auto", "high_quality", "performance"],
                     help="validate_and_preprocess_image mode the workload is quoted under (the bench checks that "
                          "it does not resize this size: BASELINE configs [3] auto at 1080p, [4] high_quality at 4K)")
-    ap.add_argument("--e2e-host-steps", type=int, default=3, help="0 disables the decoded-host-array line")
+    ap.add_argument("--e2e-host-steps", type=int, default=8, help="0 disables the decoded-host-array line")
     ap.add_argument("--seed", type=int, default=2025)
     ap.add_argument("--e2e-png-steps", type=int, default=2, help="0 disables the PNG end-to-end line")
     ap.add_argument("--e2e-jpeg-steps", type=int, default=2, help="0 disables the JPEG end-to-end line")

@@ -418,6 +418,11 @@ struct llfe_ctx {
     bool shapes_after_front = false;  // LLFE_SHAPES_AFTER_FRONT=1: shapes wait for the colour front
     bool concurrent = true;           // llfe_set_concurrency
     hipEvent_t mask_done[2] = {nullptr, nullptr};  // shapes/shadows results are on the host
+    // host-input copies of successive chunks / batches are chained (h2d_done of the last
+    // one): with two batches in flight, batch k + 1's H2D then starts after batch k's
+    // instead of splitting PCIe with it, so batch k's kernels start at half the latency
+    hipEvent_t h2d_done = nullptr;
+    bool h2d_pending = false;
     // the mask / shadow D2H runs on its own stream so the colour stage starts right after
     // the hysteresis kernels; mask_ready[slot] orders it after them, and a workspace is
     // not overwritten before the D2H that last read it (w_mask_slot) has finished
@@ -466,6 +471,8 @@ namespace {
 int stage_input(llfe_ctx *ctx, Work &W, const llfe_batch *b, int i0, int n, const uint8_t **d_img, const int8_t **d_noise,
                 hipStream_t s) {
     size_t P3 = (size_t)b->height * b->width * 3;
+    const bool h2d = !b->on_device || (b->noise && !b->noise_on_device);
+    if (h2d && ctx->h2d_pending) HIPCHK(ctx, hipStreamWaitEvent(s, ctx->h2d_done, 0));
     if (b->on_device) {
         *d_img = b->data + (size_t)i0 * P3;
     } else {
@@ -482,6 +489,10 @@ int stage_input(llfe_ctx *ctx, Work &W, const llfe_batch *b, int i0, int n, cons
             HIPCHK(ctx, hipMemcpyAsync(W.d_noise.p, b->noise + (size_t)i0 * P3, P3 * n, hipMemcpyHostToDevice, s));
             *d_noise = W.d_noise.p;
         }
+    }
+    if (h2d) {
+        HIPCHK(ctx, hipEventRecord(ctx->h2d_done, s));
+        ctx->h2d_pending = true;
     }
     return LLFE_OK;
 }
@@ -938,7 +949,7 @@ int llfe_init(int device, llfe_ctx **out) {
     c->device = device;
     for (hipEvent_t *e : {&c->chunk_done[0], &c->chunk_done[1], &c->mask_done[0], &c->mask_done[1], &c->start_ev,
                           &c->stream_done[0], &c->stream_done[1], &c->mask_ready[0], &c->mask_ready[1],
-                          &c->input_ready, &c->colour_done, &c->front_done})
+                          &c->input_ready, &c->colour_done, &c->front_done, &c->h2d_done})
         if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) {
             llfe_destroy(c);
             return LLFE_ERR_HIP;
@@ -986,7 +997,7 @@ int llfe_destroy(llfe_ctx *ctx) {
         if (st) (void)hipStreamSynchronize(st);
     for (hipEvent_t e : {ctx->chunk_done[0], ctx->chunk_done[1], ctx->mask_done[0], ctx->mask_done[1], ctx->start_ev,
                          ctx->stream_done[0], ctx->stream_done[1], ctx->mask_ready[0], ctx->mask_ready[1],
-                         ctx->input_ready, ctx->colour_done, ctx->front_done})
+                         ctx->input_ready, ctx->colour_done, ctx->front_done, ctx->h2d_done})
         if (e) (void)hipEventDestroy(e);
     for (hipStream_t st : {ctx->streams[0], ctx->streams[1], ctx->col_streams[0], ctx->col_streams[1], ctx->copy_stream})
         if (st) (void)hipStreamDestroy(st);
