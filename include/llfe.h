@@ -229,7 +229,8 @@ int llfe_font_binary(llfe_ctx *ctx, const uint8_t *bgr, uint8_t *mask, int32_t n
 int llfe_text_binary(llfe_ctx *ctx, const uint8_t *img, int32_t h, int32_t w, int32_t channels, uint8_t *out,
                      int32_t *threshold, llfe_stream stream);
 /* output size of llfe_text_binary: returns 1 when the image is upscaled, 0 when not
- * (text_extractor.py:31-37; saturate_cast<int> of w * scale, h * scale). Host only. */
+ * (text_extractor.py:31-37; saturate_cast<int> of w * scale, h * scale), negative for
+ * invalid sizes or an upscaled side past INT32_MAX. Host only. */
 int llfe_text_size(int32_t h, int32_t w, int32_t *out_h, int32_t *out_w);
 /* sums[n], counts[n] host: adaptive-threshold shadow statistics (shadow pyc @L15-21) */
 int llfe_shadow_stats(llfe_ctx *ctx, const uint8_t *bgr, uint64_t *sums, uint64_t *counts, int32_t n, int32_t h,

@@ -1323,6 +1323,7 @@ int llfe_text_size(int32_t h, int32_t w, int32_t *out_h, int32_t *out_w) {
     if (h <= 0 || w <= 0 || !out_h || !out_w) return LLFE_ERR_INVALID;
     if (h < 30 || w < 100) {  // scale = max(2, 300 / width, 100 / height) (Python floats)
         const double sc = std::max(std::max(2.0, 300.0 / w), 100.0 / h);
+        if (w * sc >= 2147483647.0 || h * sc >= 2147483647.0) return LLFE_ERR_UNSUPPORTED;
         *out_w = (int32_t)std::lrint(w * sc);  // saturate_cast<int>(double): round half even
         *out_h = (int32_t)std::lrint(h * sc);
         return 1;
@@ -1341,6 +1342,8 @@ int llfe_text_binary(llfe_ctx *ctx, const uint8_t *img, int32_t h, int32_t w, in
         return ctx->fail(LLFE_ERR_UNSUPPORTED, "llfe_text_binary: %d channels (1, 3 or 4)", channels);
     int32_t oh, ow;
     const int up = llfe_text_size(h, w, &oh, &ow);
+    if (up < 0 || !valid_dims(1, h, w) || !valid_dims(1, oh, ow))
+        return ctx->fail(LLFE_ERR_UNSUPPORTED, "llfe_text_binary: %d x %d (-> %d x %d) pixels", h, w, oh, ow);
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t s = (hipStream_t)stream;
     const long long n = (long long)h * w, n2 = (long long)oh * ow;

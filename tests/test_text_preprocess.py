@@ -176,6 +176,16 @@ def test_text_size_rule(orc):
         assert text_size(h, w) == exp == orc.text_size(h, w)
 
 
+def test_text_size_rejects_overflow():
+    from low_level_feature_extraction_amd.backend import text_size
+
+    with pytest.raises(ValueError):
+        text_size(1, 30_000_000)  # scale 100: 3e9 columns
+    with pytest.raises(ValueError):
+        text_size(0, 10)
+    assert text_size(1, 20_000_000) == (100, 2_000_000_000)
+
+
 def test_text_binary_inverts_mostly_white(orc):
     img = np.full((40, 120, 3), 250, np.uint8)
     img[10:20, 10:60] = 5  # dark text on a light page: the page binarises to 255 (mean >
