@@ -404,148 +404,158 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
                 }
             }
             __syncthreads();
-            // ---- the partition's sorted keys in KW wave chunks of whole 256-key steps
-            // (aligned to the key list, so every lane reads its 4 keys with one 16-byte
-            // load; keys outside the partition are masked): step sums of D into LDS and
-            // chunk sums.  The three trials' chunks are walked together, SEL_U steps per
-            // trip with their loads issued first -- these scans were chains of dependent
-            // scalar loads (~75 us per k-means++ round on a photo).
-            // Step sums alias the Lloyd accumulators (unused until Lloyd).
-            uint32_t(*stp)[KW][kSelSteps] = reinterpret_cast<uint32_t(*)[KW][kSelSteps]>(&sm.accA[0][0]);
-            uint32_t ca[3], cb2[3], cw0[3], cw1[3];  // partition [a, b), this wave's steps [w0, w1)
-#pragma unroll
-            for (int j = 0; j < 3; j++) {
-                const int P = sm.pj[j];
-                ca[j] = P >= 0 ? sm.pbase[P] : 0u;
-                cb2[j] = P >= 0 ? sm.pbase[P + 1] : 0u;
-                const uint32_t A = ca[j] & ~3u;
-                const uint32_t nst = (cb2[j] - A + STEP - 1) / STEP;   // steps over [A, b)
-                const uint32_t per = (nst + KW - 1) / KW;               // steps per wave (<= kSelSteps)
-                cw0[j] = A + min(nst, (uint32_t)wid * per) * STEP;
-                cw1[j] = A + min(nst, (uint32_t)(wid + 1) * per) * STEP;
-            }
-            {
-                uint32_t csum_lo[3] = {0u, 0u, 0u};  // per-lane partial chunk sums
-                unsigned long long cnt = 0;
-#pragma unroll
+            // (the scans, instantiated per number of chosen centres as the round's sweep below)
+            auto select = [&](auto KKc) __attribute__((always_inline)) {
+                constexpr int KK = decltype(KKc)::value;
+                // ---- the partition's sorted keys in KW wave chunks of whole 256-key steps
+                // (aligned to the key list, so every lane reads its 4 keys with one 16-byte
+                // load; keys outside the partition are masked): step sums of D into LDS and
+                // chunk sums.  The three trials' chunks are walked together, SEL_U steps per
+                // trip with their loads issued first -- these scans were chains of dependent
+                // scalar loads (~75 us per k-means++ round on a photo).
+                // Step sums alias the Lloyd accumulators (unused until Lloyd).
+                uint32_t(*stp)[KW][kSelSteps] = reinterpret_cast<uint32_t(*)[KW][kSelSteps]>(&sm.accA[0][0]);
+                uint32_t ca[3], cb2[3], cw0[3], cw1[3];  // partition [a, b), this wave's steps [w0, w1)
+    #pragma unroll
                 for (int j = 0; j < 3; j++) {
-                    uint32_t ls = 0;
-                    for (uint32_t s0 = cw0[j]; s0 < cw1[j]; s0 += SEL_U * STEP) {
-                        uint4 kv[SEL_U];
-#pragma unroll
-                        for (int u = 0; u < SEL_U; u++) {
-                            const uint32_t i0 = s0 + (uint32_t)u * STEP + (uint32_t)lane * 4;
-                            kv[u] = make_uint4(0u, 0u, 0u, 0u);
-                            if (i0 < cw1[j] && i0 < cb2[j] && i0 + 4 > ca[j]) kv[u] = *(const uint4 *)(pts + i0);
+                    const int P = sm.pj[j];
+                    ca[j] = P >= 0 ? sm.pbase[P] : 0u;
+                    cb2[j] = P >= 0 ? sm.pbase[P + 1] : 0u;
+                    const uint32_t A = ca[j] & ~3u;
+                    const uint32_t nst = (cb2[j] - A + STEP - 1) / STEP;   // steps over [A, b)
+                    const uint32_t per = (nst + KW - 1) / KW;               // steps per wave (<= kSelSteps)
+                    cw0[j] = A + min(nst, (uint32_t)wid * per) * STEP;
+                    cw1[j] = A + min(nst, (uint32_t)(wid + 1) * per) * STEP;
+                }
+                {
+                    uint32_t csum_lo[3] = {0u, 0u, 0u};  // per-lane partial chunk sums
+                    unsigned long long cnt = 0;
+    #pragma unroll
+                    for (int j = 0; j < 3; j++) {
+                        uint32_t ls = 0;
+                        for (uint32_t s0 = cw0[j]; s0 < cw1[j]; s0 += SEL_U * STEP) {
+                            uint4 kv[SEL_U];
+    #pragma unroll
+                            for (int u = 0; u < SEL_U; u++) {
+                                const uint32_t i0 = s0 + (uint32_t)u * STEP + (uint32_t)lane * 4;
+                                kv[u] = make_uint4(0u, 0u, 0u, 0u);
+                                if (i0 < cw1[j] && i0 < cb2[j] && i0 + 4 > ca[j]) kv[u] = *(const uint4 *)(pts + i0);
+                            }
+    #pragma unroll
+                            for (int u = 0; u < SEL_U; u++) {
+                                const uint32_t st = s0 + (uint32_t)u * STEP;
+                                if (st >= cw1[j]) break;  // (uniform)
+                                const uint32_t i0 = st + (uint32_t)lane * 4;
+                                const uint32_t kq[4] = {kv[u].x, kv[u].y, kv[u].z, kv[u].w};
+                                uint32_t sd = 0;
+    #pragma unroll
+                                for (int jj = 0; jj < 4; jj++) {
+                                    const uint32_t i = i0 + (uint32_t)jj;
+                                    const bool in = i >= ca[j] && i < cb2[j];
+                                    const int d = dmin_chosen(unpack_r(kq[jj]), unpack_g(kq[jj]), unpack_b(kq[jj]), ch, KK);
+                                    sd += in ? (uint32_t)d : 0u;
+                                }
+                                ls += sd;
+                                const uint32_t ssum = wave_sum(sd);  // <= 256 x 195075 < 2^32
+                                if (lane == 0) stp[j][wid][(st - cw0[j]) / STEP] = ssum;
+                            }
                         }
-#pragma unroll
-                        for (int u = 0; u < SEL_U; u++) {
-                            const uint32_t st = s0 + (uint32_t)u * STEP;
-                            if (st >= cw1[j]) break;  // (uniform)
-                            const uint32_t i0 = st + (uint32_t)lane * 4;
-                            const uint32_t kq[4] = {kv[u].x, kv[u].y, kv[u].z, kv[u].w};
-                            uint32_t sd = 0;
-#pragma unroll
+                        csum_lo[j] = ls;
+                        cnt += cw1[j] - cw0[j];
+                    }
+    #pragma unroll
+                    for (int j = 0; j < 3; j++) {
+                        const unsigned long long ws = wave_sum((unsigned long long)csum_lo[j]);
+                        if (lane == 0) sm.wchunk[j][wid] = ws;
+                    }
+                    if (lane == 0) atomicAdd(&sm.sel_pts, cnt);
+                }
+                __syncthreads();
+                // ... then wave j < 3 finds the chunk, the step (from the step sums) and the
+                // first crossing in that one step
+                if (wid < 3) {
+                    const int j = wid;
+                    const double pj = j == 0 ? p[0] : (j == 1 ? p[1] : p[2]);
+                    const int P = sm.pj[j];
+                    int ci = P == -2 ? 0 : N - 1;
+                    if (P >= 0) {
+                        const uint32_t a = sm.pbase[P], b = sm.pbase[P + 1];  // (not ca[j]: no dynamic private indexing)
+                        const uint32_t A = a & ~3u;
+                        const uint32_t nst = (b - A + STEP - 1) / STEP, per = (nst + KW - 1) / KW;
+                        unsigned long long e = sm.pex[j];
+                        int w = 0;
+                        for (; w < KW - 1; w++) {
+                            if ((double)(e + sm.wchunk[j][w]) >= pj) break;
+                            e += sm.wchunk[j][w];
+                        }
+                        const uint32_t w0 = A + min(nst, (uint32_t)w * per) * STEP, w1 = A + min(nst, (uint32_t)(w + 1) * per) * STEP;
+                        const int ns = (int)((w1 - w0) / STEP);
+                        // the step: inclusive prefix of the chunk's step sums, 64 at a time
+                        int sidx = ns - 1;
+                        for (int s_base = 0; s_base < ns; s_base += 64) {
+                            const int si = s_base + lane;
+                            const unsigned long long v = si < ns ? (unsigned long long)stp[j][w][si] : 0ull;
+                            unsigned long long x = v;
+    #pragma unroll
+                            for (int off = 1; off < 64; off <<= 1) {
+                                const unsigned long long y = __shfl_up(x, off);
+                                if (lane >= off) x += y;
+                            }
+                            const unsigned long long bal = __ballot(si < ns && (double)(e + x) >= pj);
+                            if (bal) {
+                                const int f = (int)__builtin_ctzll(bal);
+                                sidx = s_base + f;
+                                e += __shfl(x - v, f);
+                                break;
+                            }
+                            e += __shfl(x, 63);
+                        }
+                        int found = -1;
+                        if (ns > 0) {
+                            const uint32_t s0 = w0 + (uint32_t)sidx * STEP;
+                            const uint32_t i0 = s0 + (uint32_t)lane * 4;
+                            uint4 kv = make_uint4(0u, 0u, 0u, 0u);
+                            if (i0 < b && i0 + 4 > a) kv = *(const uint4 *)(pts + i0);
+                            const uint32_t kq[4] = {kv.x, kv.y, kv.z, kv.w};
+                            uint32_t dv[4], ls = 0;
+    #pragma unroll
                             for (int jj = 0; jj < 4; jj++) {
                                 const uint32_t i = i0 + (uint32_t)jj;
-                                const bool in = i >= ca[j] && i < cb2[j];
-                                const int d = dmin_chosen(unpack_r(kq[jj]), unpack_g(kq[jj]), unpack_b(kq[jj]), ch, kk);
-                                sd += in ? (uint32_t)d : 0u;
+                                const bool in = i >= a && i < b;
+                                dv[jj] = in ? (uint32_t)dmin_chosen(unpack_r(kq[jj]), unpack_g(kq[jj]), unpack_b(kq[jj]), ch, KK) : 0u;
+                                ls += dv[jj];
                             }
-                            ls += sd;
-                            const uint32_t ssum = wave_sum(sd);  // <= 256 x 195075 < 2^32
-                            if (lane == 0) stp[j][wid][(st - cw0[j]) / STEP] = ssum;
+                            unsigned long long x = ls;
+    #pragma unroll
+                            for (int off = 1; off < 64; off <<= 1) {
+                                const unsigned long long y = __shfl_up(x, off);
+                                if (lane >= off) x += y;
+                            }
+                            unsigned long long ee = e + x - ls;
+                            int hit = -1;
+    #pragma unroll
+                            for (int jj = 0; jj < 4; jj++) {
+                                const uint32_t i = i0 + (uint32_t)jj;
+                                ee += dv[jj];
+                                if (hit < 0 && i >= a && i < b && (double)ee >= pj) hit = jj;
+                            }
+                            const unsigned long long bal = __ballot(hit >= 0);
+                            if (bal) {
+                                const int first = (int)__builtin_ctzll(bal);
+                                found = (int)(s0 + (uint32_t)first * 4) + __shfl(hit, first);
+                            }
+                            if (lane == 0) atomicAdd(&sm.sel_pts, (unsigned long long)STEP);
                         }
+                        if (found >= 0) ci = min(found, N - 1);
                     }
-                    csum_lo[j] = ls;
-                    cnt += cw1[j] - cw0[j];
+                    if (lane == 0) sm.pj[j] = ci;
                 }
-#pragma unroll
-                for (int j = 0; j < 3; j++) {
-                    const unsigned long long ws = wave_sum((unsigned long long)csum_lo[j]);
-                    if (lane == 0) sm.wchunk[j][wid] = ws;
-                }
-                if (lane == 0) atomicAdd(&sm.sel_pts, cnt);
-            }
-            __syncthreads();
-            // ... then wave j < 3 finds the chunk, the step (from the step sums) and the
-            // first crossing in that one step
-            if (wid < 3) {
-                const int j = wid;
-                const double pj = j == 0 ? p[0] : (j == 1 ? p[1] : p[2]);
-                const int P = sm.pj[j];
-                int ci = P == -2 ? 0 : N - 1;
-                if (P >= 0) {
-                    const uint32_t a = sm.pbase[P], b = sm.pbase[P + 1];  // (not ca[j]: no dynamic private indexing)
-                    const uint32_t A = a & ~3u;
-                    const uint32_t nst = (b - A + STEP - 1) / STEP, per = (nst + KW - 1) / KW;
-                    unsigned long long e = sm.pex[j];
-                    int w = 0;
-                    for (; w < KW - 1; w++) {
-                        if ((double)(e + sm.wchunk[j][w]) >= pj) break;
-                        e += sm.wchunk[j][w];
-                    }
-                    const uint32_t w0 = A + min(nst, (uint32_t)w * per) * STEP, w1 = A + min(nst, (uint32_t)(w + 1) * per) * STEP;
-                    const int ns = (int)((w1 - w0) / STEP);
-                    // the step: inclusive prefix of the chunk's step sums, 64 at a time
-                    int sidx = ns - 1;
-                    for (int s_base = 0; s_base < ns; s_base += 64) {
-                        const int si = s_base + lane;
-                        const unsigned long long v = si < ns ? (unsigned long long)stp[j][w][si] : 0ull;
-                        unsigned long long x = v;
-#pragma unroll
-                        for (int off = 1; off < 64; off <<= 1) {
-                            const unsigned long long y = __shfl_up(x, off);
-                            if (lane >= off) x += y;
-                        }
-                        const unsigned long long bal = __ballot(si < ns && (double)(e + x) >= pj);
-                        if (bal) {
-                            const int f = (int)__builtin_ctzll(bal);
-                            sidx = s_base + f;
-                            e += __shfl(x - v, f);
-                            break;
-                        }
-                        e += __shfl(x, 63);
-                    }
-                    int found = -1;
-                    if (ns > 0) {
-                        const uint32_t s0 = w0 + (uint32_t)sidx * STEP;
-                        const uint32_t i0 = s0 + (uint32_t)lane * 4;
-                        uint4 kv = make_uint4(0u, 0u, 0u, 0u);
-                        if (i0 < b && i0 + 4 > a) kv = *(const uint4 *)(pts + i0);
-                        const uint32_t kq[4] = {kv.x, kv.y, kv.z, kv.w};
-                        uint32_t dv[4], ls = 0;
-#pragma unroll
-                        for (int jj = 0; jj < 4; jj++) {
-                            const uint32_t i = i0 + (uint32_t)jj;
-                            const bool in = i >= a && i < b;
-                            dv[jj] = in ? (uint32_t)dmin_chosen(unpack_r(kq[jj]), unpack_g(kq[jj]), unpack_b(kq[jj]), ch, kk) : 0u;
-                            ls += dv[jj];
-                        }
-                        unsigned long long x = ls;
-#pragma unroll
-                        for (int off = 1; off < 64; off <<= 1) {
-                            const unsigned long long y = __shfl_up(x, off);
-                            if (lane >= off) x += y;
-                        }
-                        unsigned long long ee = e + x - ls;
-                        int hit = -1;
-#pragma unroll
-                        for (int jj = 0; jj < 4; jj++) {
-                            const uint32_t i = i0 + (uint32_t)jj;
-                            ee += dv[jj];
-                            if (hit < 0 && i >= a && i < b && (double)ee >= pj) hit = jj;
-                        }
-                        const unsigned long long bal = __ballot(hit >= 0);
-                        if (bal) {
-                            const int first = (int)__builtin_ctzll(bal);
-                            found = (int)(s0 + (uint32_t)first * 4) + __shfl(hit, first);
-                        }
-                        if (lane == 0) atomicAdd(&sm.sel_pts, (unsigned long long)STEP);
-                    }
-                    if (found >= 0) ci = min(found, N - 1);
-                }
-                if (lane == 0) sm.pj[j] = ci;
+            };
+            switch (kk) {
+                case 1: select(std::integral_constant<int, 1>{}); break;
+                case 2: select(std::integral_constant<int, 2>{}); break;
+                case 3: select(std::integral_constant<int, 3>{}); break;
+                default: select(std::integral_constant<int, kMaxK - 1>{}); break;
             }
             __syncthreads();
             t_sel += wall_clock64() - tsel0;
@@ -558,224 +568,236 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
             }
         }
         // ---- trial sums T_j = sum min(D, d(., t_j)) per partition (kk == 0: sum d(., c0))
-        if (tid < 3 * kParts) (&sm.psum[0][0])[tid] = 0;
-        if (tid == 0) sm.next_chunk = 0;
-        __syncthreads();
-        unsigned long long acc0 = 0, acc1 = 0, acc2 = 0, fails = 0;
-        int Pcur = -1;
-        // Round constants (wave-uniform).  Every test below is linear in the cube origin o:
-        // with D_c(o) = |c|^2 - 2 o.c, d(o, c) = |o|^2 + D_c(o), so
-        //   d(o, a) - d(o, b) = D_a(o) - D_b(o)          (never / always closer tests)
-        //   sum over the cube |p - c|^2 = n (|o|^2 + D_c(o)) + 2 (o - c).S_u + S_u2
-        // and the corner margins 6 sum max(+-(a - b), 0) depend on the centres only.
-        // The pairwise corner margins live in LDS (per-lane reads indexed by the lane's
-        // owner k); the per-centre constants stay in scalar registers.
-        int C2[kMaxK], S3[kMaxK], T2[3];
-#pragma unroll
-        for (int m = 0; m < kMaxK; m++) {
-            C2[m] = ch.x[m] * ch.x[m] + ch.y[m] * ch.y[m] + ch.z[m] * ch.z[m];
-            S3[m] = 3 * (ch.x[m] + ch.y[m] + ch.z[m]);
-        }
-#pragma unroll
-        for (int j = 0; j < 3; j++) T2[j] = tx[j] * tx[j] + ty[j] * ty[j] + tz[j] * tz[j];
-        // undecided cubes' colours go through the wave's LDS ring (as in the Lloyd
-        // sweeps) and are summed 64 at a time
-        const uint32_t loff = lane_offset(lane);
-        uint32_t *stg = sm.stage[wid];
-        int head = 0, tail = 0;  // wave-uniform ring counters
-        auto sum_stage = [&](int count) {
-            __builtin_amdgcn_wave_barrier();
-            fails += (unsigned long long)count;
-            if (lane < count) {
-                // d(p, c) = |p|^2 + L_c(p), L_c(p) = |c|^2 - 2 p.c (exact integers): the
-                // |p|^2 term is common to D and every trial, so min(D, d(p, t)) =
-                // |p|^2 + min(min_m L_m, L_t) -- three multiply-adds per centre
-                const uint32_t kq = stg[(tail + lane) & (kStage - 1)];
-                const int x = unpack_r(kq), y = unpack_g(kq), z = unpack_b(kq);
-                const int p2 = __mul24(x, x) + __mul24(y, y) + __mul24(z, z);
-                int L = C2[0] - 2 * (__mul24(x, ch.x[0]) + __mul24(y, ch.y[0]) + __mul24(z, ch.z[0]));
-#pragma unroll
-                for (int m = 1; m < kMaxK; m++)
-                    if (m < kk) L = min(L, C2[m] - 2 * (__mul24(x, ch.x[m]) + __mul24(y, ch.y[m]) + __mul24(z, ch.z[m])));
-                acc0 += (uint32_t)(p2 + min(L, T2[0] - 2 * (__mul24(x, tx[0]) + __mul24(y, ty[0]) + __mul24(z, tz[0]))));
-                acc1 += (uint32_t)(p2 + min(L, T2[1] - 2 * (__mul24(x, tx[1]) + __mul24(y, ty[1]) + __mul24(z, tz[1]))));
-                acc2 += (uint32_t)(p2 + min(L, T2[2] - 2 * (__mul24(x, tx[2]) + __mul24(y, ty[2]) + __mul24(z, tz[2]))));
+        // the round's sweep, instantiated per number of chosen centres (KK = kk <= kMaxK - 1):
+        // the centre loops become straight-line code without per-centre guards
+        auto sweep = [&](auto KKc) __attribute__((always_inline)) {
+            constexpr int KK = decltype(KKc)::value;
+            if (tid < 3 * kParts) (&sm.psum[0][0])[tid] = 0;
+            if (tid == 0) sm.next_chunk = 0;
+            __syncthreads();
+            unsigned long long acc0 = 0, acc1 = 0, acc2 = 0, fails = 0;
+            int Pcur = -1;
+            // Round constants (wave-uniform).  Every test below is linear in the cube origin o:
+            // with D_c(o) = |c|^2 - 2 o.c, d(o, c) = |o|^2 + D_c(o), so
+            //   d(o, a) - d(o, b) = D_a(o) - D_b(o)          (never / always closer tests)
+            //   sum over the cube |p - c|^2 = n (|o|^2 + D_c(o)) + 2 (o - c).S_u + S_u2
+            // and the corner margins 6 sum max(+-(a - b), 0) depend on the centres only.
+            // The pairwise corner margins live in LDS (per-lane reads indexed by the lane's
+            // owner k); the per-centre constants stay in scalar registers.
+            int C2[kMaxK], S3[kMaxK], T2[3];
+    #pragma unroll
+            for (int m = 0; m < kMaxK; m++) {
+                C2[m] = ch.x[m] * ch.x[m] + ch.y[m] * ch.y[m] + ch.z[m] * ch.z[m];
+                S3[m] = 3 * (ch.x[m] + ch.y[m] + ch.z[m]);
             }
-            tail += count;
-        };
-        auto flush_pk = [&]() {
-            while (head - tail >= 64) sum_stage(64);
-            if (head > tail) sum_stage(head - tail);
-        };
-        if (tid < kMaxK * kMaxK) {  // Mkk[m][k] = 6 sum max(c_m - c_k, 0)
-            const int m = tid / kMaxK, k2 = tid % kMaxK;
-            sm.marg[tid] = 6 * (max(sm.icc[m][0] - sm.icc[k2][0], 0) + max(sm.icc[m][1] - sm.icc[k2][1], 0) +
-                                max(sm.icc[m][2] - sm.icc[k2][2], 0));
-        } else if (tid < kMaxK * kMaxK + 6 * kMaxK) {  // NA[j][k], NB[j][k]
-            const int q = tid - kMaxK * kMaxK, j = (q / kMaxK) % 3, k2 = q % kMaxK;
-            const int t[3] = {j == 0 ? tx[0] : (j == 1 ? tx[1] : tx[2]), j == 0 ? ty[0] : (j == 1 ? ty[1] : ty[2]),
-                              j == 0 ? tz[0] : (j == 1 ? tz[1] : tz[2])};
-            const int sg = q < 3 * kMaxK ? 1 : -1;  // NA: t - c_k ; NB: c_k - t
-            int acc = 0;
-#pragma unroll
-            for (int d = 0; d < 3; d++) acc += max(sg * (t[d] - sm.icc[k2][d]), 0);
-            sm.marg[tid] = 6 * acc;
-        }
-        __syncthreads();
-        const int *Mkk = sm.marg, *NA = sm.marg + kMaxK * kMaxK, *NB = sm.marg + kMaxK * kMaxK + 3 * kMaxK;
-        // waves take 64-cube chunks from a shared LDS counter, read two chunks ahead
-        // (ascending per wave, so the partition bookkeeping below still sees its
-        // partitions in order)
-        auto grab = [&]() {
-            int b = 0;
-            if (lane == 0) b = atomicAdd(&sm.next_chunk, 64);
-            return b;
-        };
-        int base = __builtin_amdgcn_readfirstlane(grab());
-        int ahead = grab();
-        CubeEnt en;
-        en.mask = 0;
-        en.id = 0;
-        en.sums = 0;
-        if (base + lane < C) en = ctab[base + lane];
-        while (base < C) {
-            const int cidx = base + lane;
-            const bool valid = cidx < C;
-            const CubeEnt e = en;
-            const int nb = __builtin_amdgcn_readfirstlane(ahead);
-            if (nb + lane < C) en = ctab[nb + lane];
-            if (nb < C) ahead = grab();
-            const CubeGeo g = cube_geo(e);
-            const int P = valid ? (int)((e.id >> 12) & 63u) : kParts;
-            uint32_t v0 = 0, v1 = 0, v2 = 0;
-            bool fail = false;
-            if (valid) {
-                if (kk == 0) {
-                    v0 = cube_sum(g, tx[0], ty[0], tz[0]);
-                    qacc += cube_sum(g, 0, 0, 0);
-                } else {
-                    // owner candidate: nearest chosen centre to the cube centre q = o + 1.5:
-                    // argmin_m |q - c_m|^2 = argmin_m (D_m(o) - 3 sum(c_m)), first minimum
-                    int Dc[kMaxK];
-#pragma unroll
-                    for (int m = 0; m < kMaxK; m++) {  // (only the kk chosen centres are read)
-                        Dc[m] = 0;
-                        if (m < kk) Dc[m] = C2[m] - 2 * (__mul24(g.ox, ch.x[m]) + __mul24(g.oy, ch.y[m]) + __mul24(g.oz, ch.z[m]));
+    #pragma unroll
+            for (int j = 0; j < 3; j++) T2[j] = tx[j] * tx[j] + ty[j] * ty[j] + tz[j] * tz[j];
+            // undecided cubes' colours go through the wave's LDS ring (as in the Lloyd
+            // sweeps) and are summed 64 at a time
+            const uint32_t loff = lane_offset(lane);
+            uint32_t *stg = sm.stage[wid];
+            int head = 0, tail = 0;  // wave-uniform ring counters
+            auto sum_stage = [&](int count) {
+                __builtin_amdgcn_wave_barrier();
+                fails += (unsigned long long)count;
+                if (lane < count) {
+                    // d(p, c) = |p|^2 + L_c(p), L_c(p) = |c|^2 - 2 p.c (exact integers): the
+                    // |p|^2 term is common to D and every trial, so min(D, d(p, t)) =
+                    // |p|^2 + min(min_m L_m, L_t) -- three multiply-adds per centre
+                    const uint32_t kq = stg[(tail + lane) & (kStage - 1)];
+                    const int x = unpack_r(kq), y = unpack_g(kq), z = unpack_b(kq);
+                    const int p2 = __mul24(x, x) + __mul24(y, y) + __mul24(z, z);
+                    int L = C2[0] - 2 * (__mul24(x, ch.x[0]) + __mul24(y, ch.y[0]) + __mul24(z, ch.z[0]));
+    #pragma unroll
+                    for (int m = 1; m < kMaxK; m++)
+                        if (m < KK) L = min(L, C2[m] - 2 * (__mul24(x, ch.x[m]) + __mul24(y, ch.y[m]) + __mul24(z, ch.z[m])));
+                    acc0 += (uint32_t)(p2 + min(L, T2[0] - 2 * (__mul24(x, tx[0]) + __mul24(y, ty[0]) + __mul24(z, tz[0]))));
+                    acc1 += (uint32_t)(p2 + min(L, T2[1] - 2 * (__mul24(x, tx[1]) + __mul24(y, ty[1]) + __mul24(z, tz[1]))));
+                    acc2 += (uint32_t)(p2 + min(L, T2[2] - 2 * (__mul24(x, tx[2]) + __mul24(y, ty[2]) + __mul24(z, tz[2]))));
+                }
+                tail += count;
+            };
+            auto flush_pk = [&]() {
+                while (head - tail >= 64) sum_stage(64);
+                if (head > tail) sum_stage(head - tail);
+            };
+            if (tid < kMaxK * kMaxK) {  // Mkk[m][k] = 6 sum max(c_m - c_k, 0)
+                const int m = tid / kMaxK, k2 = tid % kMaxK;
+                sm.marg[tid] = 6 * (max(sm.icc[m][0] - sm.icc[k2][0], 0) + max(sm.icc[m][1] - sm.icc[k2][1], 0) +
+                                    max(sm.icc[m][2] - sm.icc[k2][2], 0));
+            } else if (tid < kMaxK * kMaxK + 6 * kMaxK) {  // NA[j][k], NB[j][k]
+                const int q = tid - kMaxK * kMaxK, j = (q / kMaxK) % 3, k2 = q % kMaxK;
+                const int t[3] = {j == 0 ? tx[0] : (j == 1 ? tx[1] : tx[2]), j == 0 ? ty[0] : (j == 1 ? ty[1] : ty[2]),
+                                  j == 0 ? tz[0] : (j == 1 ? tz[1] : tz[2])};
+                const int sg = q < 3 * kMaxK ? 1 : -1;  // NA: t - c_k ; NB: c_k - t
+                int acc = 0;
+    #pragma unroll
+                for (int d = 0; d < 3; d++) acc += max(sg * (t[d] - sm.icc[k2][d]), 0);
+                sm.marg[tid] = 6 * acc;
+            }
+            __syncthreads();
+            const int *Mkk = sm.marg, *NA = sm.marg + kMaxK * kMaxK, *NB = sm.marg + kMaxK * kMaxK + 3 * kMaxK;
+            // waves take 64-cube chunks from a shared LDS counter, read two chunks ahead
+            // (ascending per wave, so the partition bookkeeping below still sees its
+            // partitions in order)
+            auto grab = [&]() {
+                int b = 0;
+                if (lane == 0) b = atomicAdd(&sm.next_chunk, 64);
+                return b;
+            };
+            int base = __builtin_amdgcn_readfirstlane(grab());
+            int ahead = grab();
+            CubeEnt en;
+            en.mask = 0;
+            en.id = 0;
+            en.sums = 0;
+            if (base + lane < C) en = ctab[base + lane];
+            while (base < C) {
+                const int cidx = base + lane;
+                const bool valid = cidx < C;
+                const CubeEnt e = en;
+                const int nb = __builtin_amdgcn_readfirstlane(ahead);
+                if (nb + lane < C) en = ctab[nb + lane];
+                if (nb < C) ahead = grab();
+                const CubeGeo g = cube_geo(e);
+                const int P = valid ? (int)((e.id >> 12) & 63u) : kParts;
+                uint32_t v0 = 0, v1 = 0, v2 = 0;
+                bool fail = false;
+                if (valid) {
+                    if (KK == 0) {
+                        v0 = cube_sum(g, tx[0], ty[0], tz[0]);
+                        qacc += cube_sum(g, 0, 0, 0);
+                    } else {
+                        // owner candidate: nearest chosen centre to the cube centre q = o + 1.5:
+                        // argmin_m |q - c_m|^2 = argmin_m (D_m(o) - 3 sum(c_m)), first minimum
+                        int Dc[kMaxK];
+    #pragma unroll
+                        for (int m = 0; m < kMaxK; m++) {  // (only the KK chosen centres are read)
+                            Dc[m] = 0;
+                            if (m < KK) Dc[m] = C2[m] - 2 * (__mul24(g.ox, ch.x[m]) + __mul24(g.oy, ch.y[m]) + __mul24(g.oz, ch.z[m]));
+                        }
+                        int k = 0, bd = Dc[0] - S3[0];
+    #pragma unroll
+                        for (int m = 1; m < kMaxK; m++) {
+                            if (m >= KK) break;
+                            const int d = Dc[m] - S3[m];
+                            if (d < bd) {
+                                bd = d;
+                                k = m;
+                            }
+                        }
+                        // owner k's values (per-lane selects from the uniform tables)
+                        int Dk = Dc[0], kx = ch.x[0], ky = ch.y[0], kz = ch.z[0];
+    #pragma unroll
+                        for (int m = 1; m < kMaxK; m++) {
+                            if (m >= KK) break;
+                            Dk = k == m ? Dc[m] : Dk;
+                            kx = k == m ? ch.x[m] : kx;
+                            ky = k == m ? ch.y[m] : ky;
+                            kz = k == m ? ch.z[m] : kz;
+                        }
+                        auto selk = [&](const int *row) { return row[k]; };  // LDS read, per-lane k
+                        // owned: no other chosen centre is ever strictly closer on the cube
+                        bool owned = true;
+    #pragma unroll
+                        for (int m = 0; m < kMaxK; m++) {
+                            if (m >= KK) break;
+                            if (m != k) owned = owned & (Dc[m] - Dk - selk(Mkk + m * kMaxK) >= 0);
+                        }
+                        // cube sums: P + n D_c(o) - 2 c.S_u, P = n |o|^2 + 2 o.S_u + S_u2
+                        const int Pc = __mul24(g.n, __mul24(g.ox, g.ox) + __mul24(g.oy, g.oy) + __mul24(g.oz, g.oz)) +
+                                       2 * (__mul24(g.ox, g.sx) + __mul24(g.oy, g.sy) + __mul24(g.oz, g.sz)) + g.s2;
+                        const uint32_t ds = (uint32_t)(Pc + __mul24(g.n, Dk) -
+                                                       2 * (__mul24(kx, g.sx) + __mul24(ky, g.sy) + __mul24(kz, g.sz)));
+                        uint32_t vv[3];
+                        bool dec = owned;
+    #pragma unroll
+                        for (int j = 0; j < 3; j++) {
+                            const int Dt = T2[j] - 2 * (__mul24(g.ox, tx[j]) + __mul24(g.oy, ty[j]) + __mul24(g.oz, tz[j]));
+                            const int f = Dt - Dk;
+                            const bool A = f - selk(NA + j * kMaxK) >= 0;  // t_j never strictly closer than c_k
+                            const bool B = f + selk(NB + j * kMaxK) <= 0;  // t_j always at least as close
+                            dec = dec & (A | B);
+                            vv[j] = A ? ds
+                                      : (uint32_t)(Pc + __mul24(g.n, Dt) -
+                                                   2 * (__mul24(tx[j], g.sx) + __mul24(ty[j], g.sy) + __mul24(tz[j], g.sz)));
+                        }
+                        v0 = vv[0];
+                        v1 = vv[1];
+                        v2 = vv[2];
+                        fail = !dec;
                     }
-                    int k = 0, bd = Dc[0] - S3[0];
-#pragma unroll
-                    for (int m = 1; m < kMaxK; m++) {
-                        if (m >= kk) break;
-                        const int d = Dc[m] - S3[m];
-                        if (d < bd) {
-                            bd = d;
-                            k = m;
+                }
+                // lanes hold ascending cube ids: visit the batch's partitions in order
+                int Pseg = __shfl(P, 0);
+                for (;;) {
+                    if (Pseg != Pcur) {
+                        if (Pcur >= 0) {
+                            flush_pk();
+                            const unsigned long long a0 = wave_sum(acc0), a1 = wave_sum(acc1), a2 = wave_sum(acc2);
+                            if (lane == 0) {
+                                atomicAdd(&sm.psum[0][Pcur], a0);
+                                atomicAdd(&sm.psum[1][Pcur], a1);
+                                atomicAdd(&sm.psum[2][Pcur], a2);
+                            }
+                        }
+                        acc0 = acc1 = acc2 = 0;
+                        Pcur = Pseg;
+                    }
+                    const bool mine = P == Pseg;
+                    if (mine && !fail) {
+                        acc0 += v0;
+                        acc1 += v1;
+                        acc2 += v2;
+                    }
+                    // undecided cubes: their colours (enumerated from the occupancy mask)
+                    // packed densely into the lanes, summed 64 at a time
+                    unsigned long long fm = __ballot(mine && fail);
+                    if (fm) {
+                        const uint32_t okey = cube_origin_key(e.id);  // read back per cube below
+                        const uint32_t mlo = (uint32_t)e.mask, mhi = (uint32_t)(e.mask >> 32);
+                        while (fm) {
+    #pragma unroll
+                            for (int u = 0; u < LLFE_KM_UNROLL; u++) {
+                                if (u > 0 && !fm) break;
+                                const int src = __builtin_ctzll(fm);
+                                fm &= fm - 1;
+                                const unsigned long long m =
+                                    ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(mhi, src) << 32) |
+                                    (uint32_t)__builtin_amdgcn_readlane(mlo, src);
+                                const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                                stg[lane_sel(m, ((uint32_t)head + r) & (kStage - 1), kStage + lane)] =
+                                    (uint32_t)__builtin_amdgcn_readlane(okey, src) | loff;
+                                head += __popcll(m);
+                            }
+                            while (head - tail >= 64) sum_stage(64);
                         }
                     }
-                    // owner k's values (per-lane selects from the uniform tables)
-                    int Dk = Dc[0], kx = ch.x[0], ky = ch.y[0], kz = ch.z[0];
-#pragma unroll
-                    for (int m = 1; m < kMaxK; m++) {
-                        if (m >= kk) break;
-                        Dk = k == m ? Dc[m] : Dk;
-                        kx = k == m ? ch.x[m] : kx;
-                        ky = k == m ? ch.y[m] : ky;
-                        kz = k == m ? ch.z[m] : kz;
-                    }
-                    auto selk = [&](const int *row) { return row[k]; };  // LDS read, per-lane k
-                    // owned: no other chosen centre is ever strictly closer on the cube
-                    bool owned = true;
-#pragma unroll
-                    for (int m = 0; m < kMaxK; m++) {
-                        if (m >= kk) break;
-                        if (m != k) owned = owned & (Dc[m] - Dk - selk(Mkk + m * kMaxK) >= 0);
-                    }
-                    // cube sums: P + n D_c(o) - 2 c.S_u, P = n |o|^2 + 2 o.S_u + S_u2
-                    const int Pc = __mul24(g.n, __mul24(g.ox, g.ox) + __mul24(g.oy, g.oy) + __mul24(g.oz, g.oz)) +
-                                   2 * (__mul24(g.ox, g.sx) + __mul24(g.oy, g.sy) + __mul24(g.oz, g.sz)) + g.s2;
-                    const uint32_t ds = (uint32_t)(Pc + __mul24(g.n, Dk) -
-                                                   2 * (__mul24(kx, g.sx) + __mul24(ky, g.sy) + __mul24(kz, g.sz)));
-                    uint32_t vv[3];
-                    bool dec = owned;
-#pragma unroll
-                    for (int j = 0; j < 3; j++) {
-                        const int Dt = T2[j] - 2 * (__mul24(g.ox, tx[j]) + __mul24(g.oy, ty[j]) + __mul24(g.oz, tz[j]));
-                        const int f = Dt - Dk;
-                        const bool A = f - selk(NA + j * kMaxK) >= 0;  // t_j never strictly closer than c_k
-                        const bool B = f + selk(NB + j * kMaxK) <= 0;  // t_j always at least as close
-                        dec = dec & (A | B);
-                        vv[j] = A ? ds
-                                  : (uint32_t)(Pc + __mul24(g.n, Dt) -
-                                               2 * (__mul24(tx[j], g.sx) + __mul24(ty[j], g.sy) + __mul24(tz[j], g.sz)));
-                    }
-                    v0 = vv[0];
-                    v1 = vv[1];
-                    v2 = vv[2];
-                    fail = !dec;
+                    const unsigned long long rest = __ballot(P > Pseg && P < kParts);
+                    if (!rest) break;
+                    Pseg = __shfl(P, (int)__builtin_ctzll(rest));
+                }
+                base = nb;
+            }
+            if (Pcur >= 0) {
+                flush_pk();
+                const unsigned long long a0 = wave_sum(acc0), a1 = wave_sum(acc1), a2 = wave_sum(acc2);
+                if (lane == 0) {
+                    atomicAdd(&sm.psum[0][Pcur], a0);
+                    atomicAdd(&sm.psum[1][Pcur], a1);
+                    atomicAdd(&sm.psum[2][Pcur], a2);
                 }
             }
-            // lanes hold ascending cube ids: visit the batch's partitions in order
-            int Pseg = __shfl(P, 0);
-            for (;;) {
-                if (Pseg != Pcur) {
-                    if (Pcur >= 0) {
-                        flush_pk();
-                        const unsigned long long a0 = wave_sum(acc0), a1 = wave_sum(acc1), a2 = wave_sum(acc2);
-                        if (lane == 0) {
-                            atomicAdd(&sm.psum[0][Pcur], a0);
-                            atomicAdd(&sm.psum[1][Pcur], a1);
-                            atomicAdd(&sm.psum[2][Pcur], a2);
-                        }
-                    }
-                    acc0 = acc1 = acc2 = 0;
-                    Pcur = Pseg;
-                }
-                const bool mine = P == Pseg;
-                if (mine && !fail) {
-                    acc0 += v0;
-                    acc1 += v1;
-                    acc2 += v2;
-                }
-                // undecided cubes: their colours (enumerated from the occupancy mask)
-                // packed densely into the lanes, summed 64 at a time
-                unsigned long long fm = __ballot(mine && fail);
-                if (fm) {
-                    const uint32_t okey = cube_origin_key(e.id);  // read back per cube below
-                    const uint32_t mlo = (uint32_t)e.mask, mhi = (uint32_t)(e.mask >> 32);
-                    while (fm) {
-#pragma unroll
-                        for (int u = 0; u < LLFE_KM_UNROLL; u++) {
-                            if (u > 0 && !fm) break;
-                            const int src = __builtin_ctzll(fm);
-                            fm &= fm - 1;
-                            const unsigned long long m =
-                                ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(mhi, src) << 32) |
-                                (uint32_t)__builtin_amdgcn_readlane(mlo, src);
-                            const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                            stg[lane_sel(m, ((uint32_t)head + r) & (kStage - 1), kStage + lane)] =
-                                (uint32_t)__builtin_amdgcn_readlane(okey, src) | loff;
-                            head += __popcll(m);
-                        }
-                        while (head - tail >= 64) sum_stage(64);
-                    }
-                }
-                const unsigned long long rest = __ballot(P > Pseg && P < kParts);
-                if (!rest) break;
-                Pseg = __shfl(P, (int)__builtin_ctzll(rest));
-            }
-            base = nb;
+            if (lane == 0 && fails) atomicAdd(&sm.fail_pts, fails);
+        };
+        switch (kk) {
+            case 0: sweep(std::integral_constant<int, 0>{}); break;
+            case 1: sweep(std::integral_constant<int, 1>{}); break;
+            case 2: sweep(std::integral_constant<int, 2>{}); break;
+            case 3: sweep(std::integral_constant<int, 3>{}); break;
+            default: sweep(std::integral_constant<int, kMaxK - 1>{}); break;
         }
-        if (Pcur >= 0) {
-            flush_pk();
-            const unsigned long long a0 = wave_sum(acc0), a1 = wave_sum(acc1), a2 = wave_sum(acc2);
-            if (lane == 0) {
-                atomicAdd(&sm.psum[0][Pcur], a0);
-                atomicAdd(&sm.psum[1][Pcur], a1);
-                atomicAdd(&sm.psum[2][Pcur], a2);
-            }
-        }
-        if (lane == 0 && fails) atomicAdd(&sm.fail_pts, fails);
         __syncthreads();
         if (wid == 0) {
 #pragma unroll
