@@ -454,7 +454,10 @@ __global__ __launch_bounds__(256) void k_stream_shadow_reduce(const uint2 *__res
 void stream_geometry(int h, int w, int &strips, int &segs, int &seg_rows) {
     strips = (w + kStripW - 1) / kStripW;
     // ~270-row segments: 10 extra rows per segment (3.7 %), 32 waves per 1080p image
-    segs = std::max(1, (h + 269) / 270);
+#ifndef LLFE_ST_SEG
+#define LLFE_ST_SEG 270
+#endif
+    segs = std::max(1, (h + LLFE_ST_SEG - 1) / LLFE_ST_SEG);
     seg_rows = (h + segs - 1) / segs;
     segs = (h + seg_rows - 1) / seg_rows;
 }
