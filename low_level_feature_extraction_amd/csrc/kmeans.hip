@@ -143,7 +143,7 @@ __device__ __forceinline__ T wave_sum(T v) {
 struct KmSmem {
     unsigned long long accA[kMaxK][KT];  // x | y << 32 per lane and cluster
     unsigned long long accB[kMaxK][KT];  // z | 1 << 32
-    unsigned long long red[20][32];
+    unsigned long long red[32][20];      // [part][cluster x component] (lanes read along v)
     unsigned long long wtot[KW][3];
     unsigned long long scan_w[KW];
     double dred[KW];
@@ -1365,7 +1365,10 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
                 bytes += 4ull * (unsigned long long)N;
             }
         }
-        // reduce 20 values (5 clusters x {x, y, z, count}) over the KT lanes
+        // reduce 20 values (5 clusters x {x, y, z, count}) over the KT lanes: part p of
+        // value v sums lanes p, p + 32, p + 64, ... so the 32 threads of a value read 32
+        // consecutive 8-byte slots per step (lanes p * 16 .. p * 16 + 15 put 16 threads on
+        // two LDS banks); integer sums, so any grouping gives the same totals
         for (int q = tid; q < 640; q += KT) {
             constexpr int LPP = KT / 32;  // lanes per part
             const int v = q >> 5, part = q & 31;
@@ -1373,16 +1376,16 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
             unsigned long long acc = 0;
             const unsigned long long *src = comp < 2 ? sm.accA[k] : sm.accB[k];
 #pragma unroll 4
-            for (int l = part * LPP; l < part * LPP + LPP; l++) {
-                unsigned long long wv = src[l];
+            for (int j = 0; j < LPP; j++) {
+                unsigned long long wv = src[part + 32 * j];
                 acc += (comp & 1) ? (wv >> 32) : (wv & 0xFFFFFFFFull);
             }
-            sm.red[v][part] = acc;
+            sm.red[part][v] = acc;
         }
         __syncthreads();
         if (tid < 20) {
             unsigned long long acc = 0;
-            for (int part = 0; part < 32; part++) acc += sm.red[tid][part];
+            for (int part = 0; part < 32; part++) acc += sm.red[part][tid];
             const int k = tid >> 2, comp = tid & 3;
             if (comp < 3) sm.sums[k][comp] = (long long)acc;
             else sm.counts[k] = (int)acc;
