@@ -124,6 +124,10 @@ constexpr int SEL_U = 4;
 #ifndef LLFE_KM_UNROLL
 #define LLFE_KM_UNROLL 4
 #endif
+#ifndef LLFE_KM_PPRUN
+#define LLFE_KM_PPRUN 4
+#endif
+constexpr int kPPRun = LLFE_KM_PPRUN;  // 64-cube chunks per k-means++ work grab
 // per-wave LDS ring of boundary colours awaiting labelling (>= 64 + 64 x unroll)
 constexpr int kStage = LLFE_KM_UNROLL <= 2 ? 256 : 512;
 
@@ -640,12 +644,18 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
             // waves take 64-cube chunks from a shared LDS counter, read two chunks ahead
             // (ascending per wave, so the partition bookkeeping below still sees its
             // partitions in order)
+            // Waves take runs of kPPRun 64-cube chunks: every partition change of a wave
+            // costs a flush (the staged colours summed as a partial batch, three wave sums,
+            // three LDS atomics), and single chunks handed out round-robin put nearly
+            // every chunk of a wave in a new partition.
+            constexpr int kRun = 64 * kPPRun;
             auto grab = [&]() {
                 int b = 0;
-                if (lane == 0) b = atomicAdd(&sm.next_chunk, 64);
+                if (lane == 0) b = atomicAdd(&sm.next_chunk, kRun);
                 return b;
             };
-            int base = __builtin_amdgcn_readfirstlane(grab());
+            int run = __builtin_amdgcn_readfirstlane(grab());  // the current run's first cube
+            int base = run;
             int ahead = grab();
             CubeEnt en;
             en.mask = 0;
@@ -656,9 +666,13 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
                 const int cidx = base + lane;
                 const bool valid = cidx < C;
                 const CubeEnt e = en;
-                const int nb = __builtin_amdgcn_readfirstlane(ahead);
+                int nb = base + 64;
+                if (nb >= run + kRun || nb >= C) {  // (uniform) next run
+                    run = __builtin_amdgcn_readfirstlane(ahead);
+                    nb = run;
+                    if (nb < C) ahead = grab();
+                }
                 if (nb + lane < C) en = ctab[nb + lane];
-                if (nb < C) ahead = grab();
                 const CubeGeo g = cube_geo(e);
                 const int P = valid ? (int)((e.id >> 12) & 63u) : kParts;
                 uint32_t v0 = 0, v1 = 0, v2 = 0;
