@@ -14,7 +14,9 @@ import json,sys
 d=json.loads(open('gpurun_out/var.json').read().strip().splitlines()[-1])
 k=d['kernels']
 iso=' '.join('%s %.3f' % (n.replace('k_', ''), v.get('isolated_ms') or 0) for n, v in k.items())
-print('%-28s img/s %8.0f step %6.2f | iso: %s' % (sys.argv[1], d['value'], d['ms_per_step'], iso))
+pc = d.get('per_class') or {}
+pcs = ' | ' + ' '.join('%s %.0f' % (c, v['value']) for c, v in pc.items()) if pc else ''
+print('%-28s img/s %8.0f step %6.2f | iso: %s%s' % (sys.argv[1], d['value'], d['ms_per_step'], iso, pcs))
 " "$(basename $v)"
 done
 cp /tmp/libllfe_keep.so $L
