@@ -79,6 +79,7 @@ __device__ __forceinline__ int label5(const P3 &p, const Cent &c, float &best) {
 // packed FP32 (v_pk_add/mul/fma_f32: two IEEE lanes, bit-identical to the scalar ops)
 // and the arg-min as min-then-first-equal (= the first strict minimum of the scan).
 typedef float f2 __attribute__((ext_vector_type(2)));
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 struct CentP {
     f2 x[3], y[3], z[3];
 };
@@ -589,6 +590,11 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
             // The pairwise corner margins live in LDS (per-lane reads indexed by the lane's
             // owner k); the per-centre constants stay in scalar registers.
             int C2[kMaxK], S3[kMaxK], T2[3];
+            u16x2 chrb[kMaxK], trb[3];  // (B, R) of the chosen centres and the trials
+    #pragma unroll
+            for (int m = 0; m < kMaxK; m++) chrb[m] = u16x2{(uint16_t)ch.z[m], (uint16_t)ch.x[m]};
+    #pragma unroll
+            for (int j = 0; j < 3; j++) trb[j] = u16x2{(uint16_t)tz[j], (uint16_t)tx[j]};
     #pragma unroll
             for (int m = 0; m < kMaxK; m++) {
                 C2[m] = ch.x[m] * ch.x[m] + ch.y[m] * ch.y[m] + ch.z[m] * ch.z[m];
@@ -605,19 +611,24 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
                 __builtin_amdgcn_wave_barrier();
                 fails += (unsigned long long)count;
                 if (lane < count) {
-                    // d(p, c) = |p|^2 + L_c(p), L_c(p) = |c|^2 - 2 p.c (exact integers): the
+                    // d(p, c) = |p|^2 - H_c(p), H_c(p) = 2 p.c - |c|^2 (exact integers): the
                     // |p|^2 term is common to D and every trial, so min(D, d(p, t)) =
-                    // |p|^2 + min(min_m L_m, L_t) -- three multiply-adds per centre
+                    // |p|^2 - max(max_m H_m, H_t).  p.c = dot2((R, B), (c_R, c_B)) + G c_G:
+                    // one v_dot2_u32_u16 and one 24-bit multiply, then one shift-add, per centre
                     const uint32_t kq = stg[(tail + lane) & (kStage - 1)];
-                    const int x = unpack_r(kq), y = unpack_g(kq), z = unpack_b(kq);
-                    const int p2 = __mul24(x, x) + __mul24(y, y) + __mul24(z, z);
-                    int L = C2[0] - 2 * (__mul24(x, ch.x[0]) + __mul24(y, ch.y[0]) + __mul24(z, ch.z[0]));
+                    const u16x2 rb = __builtin_bit_cast(u16x2, kq & 0x00FF00FFu);  // (B, R)
+                    const uint32_t g = (kq >> 8) & 255u;
+                    const uint32_t p2 = __builtin_amdgcn_udot2(rb, rb, __umul24(g, g), false);
+                    auto H = [&](u16x2 crb, uint32_t cg, int c2) {
+                        return (int)(__builtin_amdgcn_udot2(rb, crb, __umul24(g, cg), false) << 1) - c2;
+                    };
+                    int Hm = H(chrb[0], (uint32_t)ch.y[0], C2[0]);
     #pragma unroll
                     for (int m = 1; m < kMaxK; m++)
-                        if (m < KK) L = min(L, C2[m] - 2 * (__mul24(x, ch.x[m]) + __mul24(y, ch.y[m]) + __mul24(z, ch.z[m])));
-                    acc0 += (uint32_t)(p2 + min(L, T2[0] - 2 * (__mul24(x, tx[0]) + __mul24(y, ty[0]) + __mul24(z, tz[0]))));
-                    acc1 += (uint32_t)(p2 + min(L, T2[1] - 2 * (__mul24(x, tx[1]) + __mul24(y, ty[1]) + __mul24(z, tz[1]))));
-                    acc2 += (uint32_t)(p2 + min(L, T2[2] - 2 * (__mul24(x, tx[2]) + __mul24(y, ty[2]) + __mul24(z, tz[2]))));
+                        if (m < KK) Hm = max(Hm, H(chrb[m], (uint32_t)ch.y[m], C2[m]));
+                    acc0 += p2 - (uint32_t)max(Hm, H(trb[0], (uint32_t)ty[0], T2[0]));
+                    acc1 += p2 - (uint32_t)max(Hm, H(trb[1], (uint32_t)ty[1], T2[1]));
+                    acc2 += p2 - (uint32_t)max(Hm, H(trb[2], (uint32_t)ty[2], T2[2]));
                 }
                 tail += count;
             };
