@@ -694,12 +694,22 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
                         qacc += cube_sum(g, 0, 0, 0);
                     } else {
                         // owner candidate: nearest chosen centre to the cube centre q = o + 1.5:
-                        // argmin_m |q - c_m|^2 = argmin_m (D_m(o) - 3 sum(c_m)), first minimum
+                        // argmin_m |q - c_m|^2 = argmin_m (D_m(o) - 3 sum(c_m)), first minimum.
+                        // Dot products of (R, B) pairs by v_dot2_u32_u16 plus the G term by a
+                        // 24-bit multiply (all operands <= 255, sums < 2^32: exact)
+                        const u16x2 orb = u16x2{(uint16_t)g.oz, (uint16_t)g.ox};
+                        const u16x2 srb = u16x2{(uint16_t)g.sz, (uint16_t)g.sx};
+                        auto odot = [&](u16x2 crb, int cg) {  // o . c
+                            return (int)__builtin_amdgcn_udot2(orb, crb, __umul24((uint32_t)g.oy, (uint32_t)cg), false);
+                        };
+                        auto sdot = [&](u16x2 crb, int cg) {  // S_u . c
+                            return (int)__builtin_amdgcn_udot2(srb, crb, __umul24((uint32_t)g.sy, (uint32_t)cg), false);
+                        };
                         int Dc[kMaxK];
     #pragma unroll
                         for (int m = 0; m < kMaxK; m++) {  // (only the KK chosen centres are read)
                             Dc[m] = 0;
-                            if (m < KK) Dc[m] = C2[m] - 2 * (__mul24(g.ox, ch.x[m]) + __mul24(g.oy, ch.y[m]) + __mul24(g.oz, ch.z[m]));
+                            if (m < KK) Dc[m] = C2[m] - 2 * odot(chrb[m], ch.y[m]);
                         }
                         int k = 0, bd = Dc[0] - S3[0];
     #pragma unroll
@@ -712,14 +722,14 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
                             }
                         }
                         // owner k's values (per-lane selects from the uniform tables)
-                        int Dk = Dc[0], kx = ch.x[0], ky = ch.y[0], kz = ch.z[0];
+                        int Dk = Dc[0], ky = ch.y[0];
+                        u16x2 krb = chrb[0];
     #pragma unroll
                         for (int m = 1; m < kMaxK; m++) {
                             if (m >= KK) break;
                             Dk = k == m ? Dc[m] : Dk;
-                            kx = k == m ? ch.x[m] : kx;
                             ky = k == m ? ch.y[m] : ky;
-                            kz = k == m ? ch.z[m] : kz;
+                            krb = k == m ? chrb[m] : krb;
                         }
                         auto selk = [&](const int *row) { return row[k]; };  // LDS read, per-lane k
                         // owned: no other chosen centre is ever strictly closer on the cube
@@ -730,22 +740,18 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
                             if (m != k) owned = owned & (Dc[m] - Dk - selk(Mkk + m * kMaxK) >= 0);
                         }
                         // cube sums: P + n D_c(o) - 2 c.S_u, P = n |o|^2 + 2 o.S_u + S_u2
-                        const int Pc = __mul24(g.n, __mul24(g.ox, g.ox) + __mul24(g.oy, g.oy) + __mul24(g.oz, g.oz)) +
-                                       2 * (__mul24(g.ox, g.sx) + __mul24(g.oy, g.sy) + __mul24(g.oz, g.sz)) + g.s2;
-                        const uint32_t ds = (uint32_t)(Pc + __mul24(g.n, Dk) -
-                                                       2 * (__mul24(kx, g.sx) + __mul24(ky, g.sy) + __mul24(kz, g.sz)));
+                        const int Pc = __mul24(g.n, odot(orb, g.oy)) + 2 * sdot(orb, g.oy) + g.s2;
+                        const uint32_t ds = (uint32_t)(Pc + __mul24(g.n, Dk) - 2 * sdot(krb, ky));
                         uint32_t vv[3];
                         bool dec = owned;
     #pragma unroll
                         for (int j = 0; j < 3; j++) {
-                            const int Dt = T2[j] - 2 * (__mul24(g.ox, tx[j]) + __mul24(g.oy, ty[j]) + __mul24(g.oz, tz[j]));
+                            const int Dt = T2[j] - 2 * odot(trb[j], ty[j]);
                             const int f = Dt - Dk;
                             const bool A = f - selk(NA + j * kMaxK) >= 0;  // t_j never strictly closer than c_k
                             const bool B = f + selk(NB + j * kMaxK) <= 0;  // t_j always at least as close
                             dec = dec & (A | B);
-                            vv[j] = A ? ds
-                                      : (uint32_t)(Pc + __mul24(g.n, Dt) -
-                                                   2 * (__mul24(tx[j], g.sx) + __mul24(ty[j], g.sy) + __mul24(tz[j], g.sz)));
+                            vv[j] = A ? ds : (uint32_t)(Pc + __mul24(g.n, Dt) - 2 * sdot(trb[j], ty[j]));
                         }
                         v0 = vv[0];
                         v1 = vv[1];
