@@ -959,9 +959,15 @@ int llfe_init(int device, llfe_ctx **out) {
     // kernels then take the slots its retiring workgroups free).  Measured neutral.
     int prio_lo = 0, prio_hi = 0;
     (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-    if (const char *sp = getenv("LLFE_SHAPES_PRIORITY"); !sp || atoi(sp) != 1) prio_hi = prio_lo;
+    const char *sp = getenv("LLFE_SHAPES_PRIORITY");
+    // LLFE_COLOUR_PRIORITY=1: the colour streams get the higher priority instead (the
+    // unique-colour chain in front of k-means is the serial step's critical path)
+    const char *cp = getenv("LLFE_COLOUR_PRIORITY");
+    const bool shp_hi = sp && atoi(sp) == 1, col_hi = cp && atoi(cp) == 1;
     for (hipStream_t *st : {&c->streams[0], &c->streams[1], &c->col_streams[0], &c->col_streams[1], &c->copy_stream}) {
-        const int prio = (st == &c->streams[0] || st == &c->streams[1]) ? prio_hi : prio_lo;
+        const bool is_shp = st == &c->streams[0] || st == &c->streams[1];
+        const bool is_col = st == &c->col_streams[0] || st == &c->col_streams[1];
+        const int prio = (is_shp && shp_hi) || (is_col && col_hi) ? prio_hi : prio_lo;
         if (hipStreamCreateWithPriority(st, hipStreamNonBlocking, prio) != hipSuccess) {
             llfe_destroy(c);
             return LLFE_ERR_HIP;
