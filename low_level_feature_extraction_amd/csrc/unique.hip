@@ -322,7 +322,10 @@ __global__ __launch_bounds__(UT) void k_uq_part(const uint32_t *__restrict__ par
     const uint32_t *in = part + (size_t)img * key_stride + start;
     // 8 independent (coalesced) key loads in flight per thread before their LDS atomics:
     // one load per atomic in sequence left the workgroup waiting on HBM latency
-    constexpr int KB8 = 8;
+#ifndef LLFE_UQ_LOADS
+#define LLFE_UQ_LOADS 8
+#endif
+    constexpr int KB8 = LLFE_UQ_LOADS;
     for (uint32_t base = 0; base < count; base += UT * KB8) {
         uint32_t kk[KB8];
 #pragma unroll
