@@ -373,6 +373,12 @@ def main():
     # host-side work, as a serving node would)
 
     total_images = B * world * args.steps
+    # the committed PMC profile (tools/profile.sh) is of the default workload: its per-launch
+    # traffic and VALU counts only describe launches of that shape
+    profiled = (B, args.height, args.width, args.features, args.preprocessing) == \
+        (512, 1080, 1920, "colors,shapes,shadows", "auto")
+    traffic, valu_insts = (TRAFFIC, VALU_INSTS) if profiled else ({}, {})
+
     def roof(name, src=None):
         """HBM roofline of one kernel: algorithmic bytes per launch
         / its average hipEvent-timed launch duration."""
@@ -381,12 +387,12 @@ def main():
         bpl = st["bytes"] / max(st["launches"], 1)
         achieved = bpl / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
         r = {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": TRAFFIC.get(name),
+             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic.get(name),
              "bytes_per_launch": bpl, "avg_launch_ms": round(avg_ms, 4)}
-        if name in VALU_INSTS and avg_ms > 0:
+        if name in valu_insts and avg_ms > 0:
             # PMC SQ_INSTS_VALU per launch (profiles/traffic_latest.json) over the launch's
             # VALU issue capacity (VALU_SLOTS_PER_S): how close the kernel is to its compute bound
-            r["valu_busy"] = round(VALU_INSTS[name] / (VALU_SLOTS_PER_S * avg_ms * 1e-3), 3)
+            r["valu_busy"] = round(valu_insts[name] / (VALU_SLOTS_PER_S * avg_ms * 1e-3), 3)
         return r
 
     kernels = {}
