@@ -144,6 +144,9 @@ int llfe_set_concurrency(llfe_ctx *ctx, int enable);
  * LOCAL_WORLD_SIZE), else host; LLFE_CONTOURS=host|gpu overrides. */
 #define LLFE_CONTOURS_HOST 0
 #define LLFE_CONTOURS_GPU 1
+/* diagnostic: GPU mode, with every chunk then redone by the host fallback that a chunk
+ * the GPU tracer flags as unsupported takes (tests exercise that path with it) */
+#define LLFE_CONTOURS_GPU_FORCE_FALLBACK 2
 int llfe_set_contour_mode(llfe_ctx *ctx, int mode);
 int llfe_get_contour_mode(llfe_ctx *ctx); /* the current mode (or < 0) */
 /* copies up to cap entries, returns the number of kernels with statistics */

@@ -94,7 +94,7 @@ class Backend:
         if rc != L.LLFE_OK:
             raise L.LlfeError(rc, f"llfe_init(device={device}) failed (no HIP device available?)")
         self.ctx = ctx
-        self._lock = threading.Lock()
+        self._lock = threading.RLock()  # (re-entered by submit -> _call)
 
     @classmethod
     def get(cls, device: int | None = None) -> "Backend":
@@ -109,8 +109,9 @@ class Backend:
 
     def close(self):
         if self.ctx:
-            self._lib.llfe_destroy(self.ctx)
-            self.ctx = None
+            with self._lock:
+                self._lib.llfe_destroy(self.ctx)
+                self.ctx = None
 
     def __del__(self):  # pragma: no cover
         try:
@@ -120,31 +121,40 @@ class Backend:
 
     # ------------------------------------------------------------------ profiling
     def set_profiling(self, enable: bool):
-        self._chk(self._lib.llfe_set_profiling(self.ctx, int(bool(enable))))
+        self._call("llfe_set_profiling", int(bool(enable)))
 
     def set_concurrency(self, enable: bool):
         """Colour path on a second stream beside shapes / shadows (default) or all kernels
         in order on one stream (isolated kernel timings)."""
-        self._chk(self._lib.llfe_set_concurrency(self.ctx, int(bool(enable))))
+        self._call("llfe_set_concurrency", int(bool(enable)))
 
     def set_contour_mode(self, mode: str):
         """"host" (default): findContours + shape geometry on the host pool while the GPU
         runs k-means; "gpu": on the GPU (contours_gpu.hip).  Identical results."""
-        self._chk(self._lib.llfe_set_contour_mode(self.ctx, {"host": 0, "gpu": 1}[mode]))
+        self._call("llfe_set_contour_mode", CONTOUR_MODES[mode])
 
     def contour_mode(self) -> str:
-        return {0: "host", 1: "gpu"}[self._chk(self._lib.llfe_get_contour_mode(self.ctx))]
+        m = self._call("llfe_get_contour_mode")
+        return {v: k for k, v in CONTOUR_MODES.items()}[m]
 
     def kernel_stats(self) -> dict:
         """{kernel: {"launches", "total_ms", "bytes"}} accumulated while profiling."""
         arr = (L.LlfeKernelStat * 64)()
-        n = self._chk(self._lib.llfe_kernel_stats(self.ctx, arr, 64))
+        n = self._call("llfe_kernel_stats", arr, 64)
         return {arr[i].name.decode(): {"launches": int(arr[i].launches), "total_ms": float(arr[i].total_ms),
                                        "bytes": float(arr[i].bytes)} for i in range(min(n, 64))}
 
     # ------------------------------------------------------------------ helpers
     def _chk(self, rc):
         return L.check(self.ctx, rc)
+
+    def _call(self, fn: str, *args):
+        """self._lib.<fn>(ctx, *args) under the context lock, checked.  A ctx is not
+        thread-safe (llfe.h): its scratch buffers are shared by every entry point, so a
+        stage call from a request thread must not run beside a batch on the
+        MicroBatcher thread."""
+        with self._lock:
+            return self._chk(getattr(self._lib, fn)(self.ctx, *args))
 
     def _stream(self, t=None):
         if t is not None and _is_torch(t) and t.is_cuda:
@@ -228,8 +238,8 @@ class Backend:
                 t = im
                 if t.dtype != _torch().uint8 or t.dim() != 3 or t.shape[2] != 3:
                     raise ValueError(f"image {i}: expected H x W x 3 uint8, got {tuple(t.shape)} {t.dtype}")
-                if t.stride(2) != 1 or t.stride(1) != 3:
-                    t = t.contiguous()  # pixels not packed: one explicit copy
+                if t.stride(2) != 1 or t.stride(1) != 3 or t.stride(0) < 3 * t.shape[1]:
+                    t = t.contiguous()  # pixels not packed, or rows overlap (stride 0): one copy
                 ptr, h, w, stride, dev = t.data_ptr(), t.shape[0], t.shape[1], t.stride(0), int(t.is_cuda)
             else:
                 t = np.asarray(im)
@@ -305,9 +315,8 @@ class Backend:
         b = L.LlfeBatch(C.c_void_p(ptr), n, h, w, on_dev, C.c_void_p(nptr) if nptr else None, n_on_dev,
                         int(n_colors), index_base)
         ticket = C.c_int64(0)
-        with self._lock:
-            self._chk(self._lib.llfe_submit_batch(self.ctx, C.byref(b), mask, C.c_uint64(seed & (2**64 - 1)),
-                                                  self._stream(keep), C.byref(ticket)))
+        self._call("llfe_submit_batch", C.byref(b), mask, C.c_uint64(seed & (2**64 - 1)), self._stream(keep),
+                   C.byref(ticket))
         if not hasattr(self, "_inflight"):
             self._inflight = {}
         self._inflight[ticket.value] = (n, h, w, mask, keep, nkeep, b)  # inputs stay alive
@@ -344,7 +353,7 @@ class Backend:
         x = self._dev_batch(images)
         n, h, w, _ = x.shape
         out = torch.empty((n, h, w), dtype=torch.uint8, device=x.device)
-        self._chk(self._lib.llfe_gray_blur5(self.ctx, x.data_ptr(), out.data_ptr(), n, h, w, self._stream(x)))
+        self._call("llfe_gray_blur5", x.data_ptr(), out.data_ptr(), n, h, w, self._stream(x))
         return out
 
     def edge_classes(self, images):
@@ -352,7 +361,7 @@ class Backend:
         x = self._dev_batch(images)
         n, h, w, _ = x.shape
         out = torch.empty((n, h, w), dtype=torch.uint8, device=x.device)
-        self._chk(self._lib.llfe_edge_classes(self.ctx, x.data_ptr(), out.data_ptr(), n, h, w, self._stream(x)))
+        self._call("llfe_edge_classes", x.data_ptr(), out.data_ptr(), n, h, w, self._stream(x))
         return out
 
     def font_binary(self, images):
@@ -361,7 +370,7 @@ class Backend:
         x = self._dev_batch(images)
         n, h, w, _ = x.shape
         out = torch.empty((n, h, w), dtype=torch.uint8, device=x.device)
-        self._chk(self._lib.llfe_font_binary(self.ctx, x.data_ptr(), out.data_ptr(), n, h, w, self._stream(x)))
+        self._call("llfe_font_binary", x.data_ptr(), out.data_ptr(), n, h, w, self._stream(x))
         return out
 
     def text_binary(self, image):
@@ -377,8 +386,8 @@ class Backend:
         oh, ow = text_size(h, w)
         out = torch.empty((oh, ow), dtype=torch.uint8, device=x.device)
         t = C.c_int32(0)
-        self._chk(self._lib.llfe_text_binary(self.ctx, x.data_ptr(), h, w, ch, out.data_ptr(), C.byref(t),
-                                             self._stream(x)))
+        self._call("llfe_text_binary", x.data_ptr(), h, w, ch, out.data_ptr(), C.byref(t),
+                                             self._stream(x))
         return out, int(t.value)
 
     def shape_mask(self, images):
@@ -386,7 +395,7 @@ class Backend:
         x = self._dev_batch(images)
         n, h, w, _ = x.shape
         out = torch.empty((n, h, w), dtype=torch.uint8, device=x.device)
-        self._chk(self._lib.llfe_shape_mask(self.ctx, x.data_ptr(), out.data_ptr(), n, h, w, self._stream(x)))
+        self._call("llfe_shape_mask", x.data_ptr(), out.data_ptr(), n, h, w, self._stream(x))
         return out
 
     def canny(self, images):
@@ -396,7 +405,7 @@ class Backend:
         x = self._dev_batch(images)
         n, h, w, _ = x.shape
         out = torch.empty((n, h, w), dtype=torch.uint8, device=x.device)
-        self._chk(self._lib.llfe_canny(self.ctx, x.data_ptr(), out.data_ptr(), n, h, w, self._stream(x)))
+        self._call("llfe_canny", x.data_ptr(), out.data_ptr(), n, h, w, self._stream(x))
         return out
 
     def dilate3(self, masks):
@@ -408,7 +417,7 @@ class Backend:
             x = x[None]
         n, h, w = x.shape
         out = torch.empty_like(x)
-        self._chk(self._lib.llfe_dilate3(self.ctx, x.data_ptr(), out.data_ptr(), n, h, w, self._stream(x)))
+        self._call("llfe_dilate3", x.data_ptr(), out.data_ptr(), n, h, w, self._stream(x))
         return out
 
     def find_contours_gpu(self, mask: np.ndarray) -> list:
@@ -421,8 +430,9 @@ class Backend:
             pts = np.empty((cap, 2), np.int32)
             offs = np.empty(cap + 1, np.int32)
             need = C.c_int64(0)
-            nc = self._lib.llfe_find_contours_gpu(self.ctx, m.ctypes.data, h, w, pts.ctypes.data, cap,
-                                                  offs.ctypes.data, cap + 1, C.byref(need))
+            with self._lock:
+                nc = self._lib.llfe_find_contours_gpu(self.ctx, m.ctypes.data, h, w, pts.ctypes.data, cap,
+                                                      offs.ctypes.data, cap + 1, C.byref(need))
             if nc == L.LLFE_ERR_CAPACITY:
                 cap = max(int(need.value), cap * 2)
                 continue
@@ -440,8 +450,9 @@ class Backend:
             ns = np.zeros(n, np.int32)
             nc = np.zeros(n, np.int32)
             need = C.c_int64(0)
-            rc = self._lib.llfe_shapes_from_masks_gpu(self.ctx, m.ctypes.data, n, h, w, arr, cap, ns.ctypes.data,
-                                                      nc.ctypes.data, C.byref(need))
+            with self._lock:
+                rc = self._lib.llfe_shapes_from_masks_gpu(self.ctx, m.ctypes.data, n, h, w, arr, cap, ns.ctypes.data,
+                                                          nc.ctypes.data, C.byref(need))
             if rc == L.LLFE_ERR_CAPACITY:
                 cap = int(need.value)
                 continue
@@ -459,8 +470,8 @@ class Backend:
         n, h, w, _ = x.shape
         sums = np.zeros(n, np.uint64)
         cnts = np.zeros(n, np.uint64)
-        self._chk(self._lib.llfe_shadow_stats(self.ctx, x.data_ptr(), sums.ctypes.data, cnts.ctypes.data, n, h, w,
-                                              self._stream(x)))
+        self._call("llfe_shadow_stats", x.data_ptr(), sums.ctypes.data, cnts.ctypes.data, n, h, w,
+                                              self._stream(x))
         return sums, cnts
 
     def color_unique(self, images, seed=0, noise=None, index_base=0):
@@ -475,8 +486,8 @@ class Backend:
         nu = np.zeros(n, np.int64)
         b = L.LlfeBatch(C.c_void_p(x.data_ptr()), n, h, w, 1, C.c_void_p(nz.data_ptr()) if nz is not None else None,
                         1, 0, index_base)
-        self._chk(self._lib.llfe_color_unique(self.ctx, C.byref(b), C.c_uint64(seed), keys.data_ptr(),
-                                              nu.ctypes.data, self._stream(x)))
+        self._call("llfe_color_unique", C.byref(b), C.c_uint64(seed), keys.data_ptr(),
+                                              nu.ctypes.data, self._stream(x))
         return keys, nu
 
     def kmeans(self, keys, n_points, n_colors=5, seed=0, index_base=0):
@@ -484,8 +495,8 @@ class Backend:
         n = keys.shape[0]
         n_points = np.ascontiguousarray(n_points, np.int64)
         res = (L.LlfeImageResult * max(n, 1))()
-        self._chk(self._lib.llfe_kmeans(self.ctx, keys.data_ptr(), keys.shape[1], n_points.ctypes.data, n, n_colors,
-                                        C.c_uint64(seed), index_base, res, self._stream(keys)))
+        self._call("llfe_kmeans", keys.data_ptr(), keys.shape[1], n_points.ctypes.data, n, n_colors,
+                                        C.c_uint64(seed), index_base, res, self._stream(keys))
         out = []
         for i in range(n):
             r = res[i]
@@ -506,8 +517,8 @@ class Backend:
         bx = None
         if box is not None:
             bx = (C.c_double * 4)(*[float(v) for v in box])
-        self._chk(self._lib.llfe_resize_lanczos_pil(self.ctx, x.data_ptr(), h, w, ch, out.data_ptr(), out_h, out_w,
-                                                    bx, self._stream(x)))
+        self._call("llfe_resize_lanczos_pil", x.data_ptr(), h, w, ch, out.data_ptr(), out_h, out_w,
+                                                    bx, self._stream(x))
         return out
 
 
@@ -519,8 +530,8 @@ class Backend:
             x = x[:, :, None]
         h, w, ch = x.shape
         out = torch.empty(((h + fy - 1) // fy, (w + fx - 1) // fx, ch), dtype=torch.uint8, device=x.device)
-        self._chk(self._lib.llfe_reduce_pil(self.ctx, x.data_ptr(), h, w, ch, fx, fy, out.data_ptr(),
-                                            self._stream(x)))
+        self._call("llfe_reduce_pil", x.data_ptr(), h, w, ch, fx, fy, out.data_ptr(),
+                                            self._stream(x))
         return out
 
     def resize_cv(self, image, out_w, out_h, interpolation):
@@ -536,8 +547,8 @@ class Backend:
             x = x[:, :, None]
         h, w, ch = x.shape
         out = torch.empty((out_h, out_w, ch), dtype=torch.uint8, device=x.device)
-        self._chk(self._lib.llfe_resize_cv(self.ctx, x.data_ptr(), h, w, ch, out.data_ptr(), out_h, out_w, code,
-                                           self._stream(x)))
+        self._call("llfe_resize_cv", x.data_ptr(), h, w, ch, out.data_ptr(), out_h, out_w, code,
+                                           self._stream(x))
         return out[:, :, 0] if squeeze else out
 
     def thumbnail_pil(self, image, max_w=1920, max_h=1080):
@@ -551,8 +562,8 @@ class Backend:
         h, w, ch = x.shape
         out = torch.empty(h * w * ch, dtype=torch.uint8, device=x.device)
         oh, ow = C.c_int32(0), C.c_int32(0)
-        self._chk(self._lib.llfe_thumbnail_pil(self.ctx, x.data_ptr(), h, w, ch, max_w, max_h, out.data_ptr(),
-                                               out.numel(), C.byref(oh), C.byref(ow), self._stream(x)))
+        self._call("llfe_thumbnail_pil", x.data_ptr(), h, w, ch, max_w, max_h, out.data_ptr(),
+                                               out.numel(), C.byref(oh), C.byref(ow), self._stream(x))
         out = out[: oh.value * ow.value * ch].view(oh.value, ow.value, ch)
         return out[:, :, 0] if squeeze else out
 
@@ -567,12 +578,14 @@ class Backend:
         ow, oh = plan if plan else (w, h)
         out = torch.empty((n, oh, ow, ch), dtype=torch.uint8, device=x.device)
         ro, co = C.c_int32(0), C.c_int32(0)
-        self._chk(self._lib.llfe_thumbnail_pil_batch(self.ctx, x.data_ptr(), n, h, w, ch, max_w, max_h, out.data_ptr(),
-                                                     out.numel(), C.byref(ro), C.byref(co), self._stream(x)))
+        self._call("llfe_thumbnail_pil_batch", x.data_ptr(), n, h, w, ch, max_w, max_h, out.data_ptr(),
+                                                     out.numel(), C.byref(ro), C.byref(co), self._stream(x))
         assert (ro.value, co.value) == (oh, ow)
         return out
 
 
+# "gpu_force_fallback": diagnostic GPU mode whose chunks all take the host fallback
+CONTOUR_MODES = {"host": 0, "gpu": 1, "gpu_force_fallback": 2}
 CV_INTER = {"linear": 1, "cubic": 2, "area": 3, "lanczos4": 4}
 PRE_MODES = {"none": 0, "auto": 1, "high_quality": 2, "performance": 3}
 _INTER_NAME = {1: "INTER_LINEAR", 3: "INTER_AREA", 4: "INTER_LANCZOS4"}

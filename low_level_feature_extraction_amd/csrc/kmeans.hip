@@ -22,6 +22,8 @@
 //    sequentially; the difference is far below the uint8 truncation of the output).
 #include "kmeans_common.h"
 
+#include <mutex>
+
 namespace llfe {
 namespace {
 
@@ -1675,14 +1677,24 @@ hipError_t launch_kmeans(const uint32_t *keys, int64_t key_stride, const int64_t
                          hipStream_t s) {
     if (n > OMAX) return hipErrorInvalidValue;
     if (n == 0) return hipSuccess;
-    static bool attr_set = false;
+    // the dynamic-LDS attribute is per device: set once per device id, under a lock (one
+    // context per GPU per host thread, so several threads / devices can get here at once)
+    static std::mutex attr_mu;
+    static uint64_t attr_set = 0;  // bit d: set on device d
     const size_t smem = sizeof(KmSmem);
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void *)k_kmeans<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    {
+        int dev = 0;
+        hipError_t e = hipGetDevice(&dev);
         if (e != hipSuccess) return e;
-        e = hipFuncSetAttribute((const void *)k_kmeans<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-        if (e != hipSuccess) return e;
-        attr_set = true;
+        std::lock_guard<std::mutex> lk(attr_mu);
+        const uint64_t bit = dev < 64 ? 1ull << dev : 0;
+        if (!bit || !(attr_set & bit)) {
+            e = hipFuncSetAttribute((const void *)k_kmeans<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+            if (e != hipSuccess) return e;
+            e = hipFuncSetAttribute((const void *)k_kmeans<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+            if (e != hipSuccess) return e;
+            attr_set |= bit;
+        }
     }
     hipLaunchKernelGGL(k_kmeans_order, dim3(1), dim3(OT), 0, s, (const long long *)n_unique, n, order);
     if (n_colors > kMaxK) {  // general K: plain sweeps over the keys (kmeans_big.hip)

@@ -321,8 +321,7 @@ size_t shadow_tiles(int n, int h, int w) { return stencil_parts(n, h, w); }
 // iterations) over more work (512 x 1080p per pass: +10 % images/s over 256).  The
 // workspace is ~16 B per pixel + the 4 MB per-image partition cube table, held within
 // LLFE_WORKSPACE_GB (default 24 GB of the 288 GB of HBM).
-int chunk_for(int explicit_chunk, int h, int w) {
-    if (explicit_chunk > 0) return explicit_chunk;
+int chunk_for(int h, int w) {
     double gb = 24.0;
     if (const char *e = getenv("LLFE_WORKSPACE_GB"); e && atof(e) > 0) gb = atof(e);
     const double per_image = 16.0 * (double)h * (double)w + (double)kParts * kCubesPerPart * sizeof(CubeEnt);
@@ -372,12 +371,8 @@ struct llfe_ctx {
     Profiler prof;
     StencilParams sp{};
     // device workspace
-    // per-chunk device workspaces.  With LLFE_STREAMS=2 consecutive chunks run on two
-    // streams so chunk c + 1's kernels fill the CUs left idle by the tail of chunk c's
-    // k-means; measured +0.8 % end to end at 512 images per call, and it makes
-    // per-kernel timings overlap, so the default is one stream.
+    // per-slot device workspaces (two batches in flight: llfe_submit_batch)
     Work ws[2];
-    int nstreams = 1;
     hipStream_t streams[2] = {nullptr, nullptr};
     hipStream_t col_streams[2] = {nullptr, nullptr};  // colour path of workspace q
     hipEvent_t start_ev = nullptr, stream_done[2] = {nullptr, nullptr};
@@ -414,8 +409,7 @@ struct llfe_ctx {
     HostBuf<unsigned long long> h_shadow_s[2];
     HostBuf<KmeansImageOut> h_kout_s[2];
     hipEvent_t chunk_done[2] = {nullptr, nullptr};
-    hipEvent_t input_ready = nullptr, colour_done = nullptr, front_done = nullptr;  // intra-chunk stream split
-    bool shapes_after_front = false;  // LLFE_SHAPES_AFTER_FRONT=1: shapes wait for the colour front
+    hipEvent_t input_ready = nullptr, colour_done = nullptr;  // intra-chunk stream split
     bool concurrent = true;           // llfe_set_concurrency
     hipEvent_t mask_done[2] = {nullptr, nullptr};  // shapes/shadows results are on the host
     // host-input copies of successive chunks / batches are chained (h2d_done of the last
@@ -429,7 +423,6 @@ struct llfe_ctx {
     hipStream_t copy_stream = nullptr;
     hipEvent_t mask_ready[2] = {nullptr, nullptr};
     int w_mask_slot[2] = {-1, -1};
-    int chunk = 0;  // images per device pass: LLFE_CHUNK, or 0 = sized by chunk_for()
     HostBuf<KmeansImageOut> h_kout;
     // per-thread host scratch
     std::vector<std::vector<int8_t>> work;
@@ -438,7 +431,9 @@ struct llfe_ctx {
     std::vector<std::vector<llfe_shape>> img_shapes;
     std::vector<int32_t> img_ncont;
     int64_t host_fallbacks = 0;  // GPU-contour chunks traced on the host instead
-    bool force_ct_fallback = false;  // LLFE_CT_FORCE_HOST_FALLBACK=1 (tests: exercise that path)
+    // llfe_set_contour_mode(LLFE_CONTOURS_GPU_FORCE_FALLBACK): every GPU-traced chunk is
+    // redone on the host path (diagnostic: exercises the fallback)
+    bool force_ct_fallback = false;
 
     int fail(int code, const char *fmt, ...) {
         char buf[512];
@@ -687,26 +682,22 @@ int enqueue_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_
     ImgIndex index;
     rc = chunk_index(ctx, W, b, i0, n, s, &index);
     if (rc) return rc;
-    // single-slot mode: the colour path (unique colours + k-means) runs on the second
-    // stream, concurrently with shapes / shadows (both only read the input).  Measured
-    // (512 x 1080p): shapes alongside the colour front 13.1k images/s; shapes held back
-    // to share the GPU with k-means (LLFE_SHAPES_AFTER_FRONT=1) 12.8k -- the stencil
-    // waves slow the k-means attempts more than they fill its tail.
+    // the colour path (unique colours + k-means) runs on the second stream, concurrently
+    // with shapes / shadows (both only read the input).  Measured (512 x 1080p): shapes
+    // alongside the colour front 13.1k images/s; shapes held back to share the GPU with
+    // k-means 12.8k -- the stencil waves slow the k-means attempts more than they fill
+    // its tail.
     hipStream_t col_s = s;
-    if (want_col && ctx->concurrent && ctx->nstreams == 1 && (want_shp || want_shd)) {
+    if (want_col && ctx->concurrent && (want_shp || want_shd)) {
         col_s = ctx->col_streams[q];
         HIPCHK(ctx, hipEventRecord(ctx->input_ready, s));
         HIPCHK(ctx, hipStreamWaitEvent(col_s, ctx->input_ready, 0));
     }
-    // colour front (unique colours), then shapes / shadows (on the other stream unless
-    // held back), then k-means
+    // colour front (unique colours), then shapes / shadows (on the other stream), then
+    // k-means
     if (want_col) {
         rc = color_stage(ctx, W, img, noise, n, h, w, seed, index, col_s);
         if (rc) return rc;
-        if (col_s != s && ctx->shapes_after_front) {
-            HIPCHK(ctx, hipEventRecord(ctx->front_done, col_s));
-            HIPCHK(ctx, hipStreamWaitEvent(s, ctx->front_done, 0));
-        }
     }
     // d_shadow / d_bits of this workspace may still be in the previous chunk's D2H
     if (ctx->w_mask_slot[q] >= 0) HIPCHK(ctx, hipStreamWaitEvent(s, ctx->mask_done[ctx->w_mask_slot[q]], 0));
@@ -949,33 +940,19 @@ int llfe_init(int device, llfe_ctx **out) {
     c->device = device;
     for (hipEvent_t *e : {&c->chunk_done[0], &c->chunk_done[1], &c->mask_done[0], &c->mask_done[1], &c->start_ev,
                           &c->stream_done[0], &c->stream_done[1], &c->mask_ready[0], &c->mask_ready[1],
-                          &c->input_ready, &c->colour_done, &c->front_done, &c->h2d_done})
+                          &c->input_ready, &c->colour_done, &c->h2d_done})
         if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) {
             llfe_destroy(c);
             return LLFE_ERR_HIP;
         }
-    // LLFE_SHAPES_PRIORITY=1: the shapes / shadows streams get the higher priority
-    // (k-means on the colour stream fills every CU's register file; the GPU contour
-    // kernels then take the slots its retiring workgroups free).  Measured neutral.
-    int prio_lo = 0, prio_hi = 0;
-    (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-    const char *sp = getenv("LLFE_SHAPES_PRIORITY");
-    // LLFE_COLOUR_PRIORITY=1: the colour streams get the higher priority instead (the
-    // unique-colour chain in front of k-means is the serial step's critical path)
-    const char *cp = getenv("LLFE_COLOUR_PRIORITY");
-    const bool shp_hi = sp && atoi(sp) == 1, col_hi = cp && atoi(cp) == 1;
+    // all streams at the default priority: a higher priority for the shapes streams or
+    // for the colour streams measured neutral
     for (hipStream_t *st : {&c->streams[0], &c->streams[1], &c->col_streams[0], &c->col_streams[1], &c->copy_stream}) {
-        const bool is_shp = st == &c->streams[0] || st == &c->streams[1];
-        const bool is_col = st == &c->col_streams[0] || st == &c->col_streams[1];
-        const int prio = (is_shp && shp_hi) || (is_col && col_hi) ? prio_hi : prio_lo;
-        if (hipStreamCreateWithPriority(st, hipStreamNonBlocking, prio) != hipSuccess) {
+        if (hipStreamCreateWithFlags(st, hipStreamNonBlocking) != hipSuccess) {
             llfe_destroy(c);
             return LLFE_ERR_HIP;
         }
     }
-    if (const char *ch = getenv("LLFE_CHUNK"); ch && atoi(ch) > 0) c->chunk = std::min(atoi(ch), kMaxKmeansBatch);
-    if (const char *ns = getenv("LLFE_STREAMS"); ns && atoi(ns) == 2) c->nstreams = 2;
-    if (const char *sa = getenv("LLFE_SHAPES_AFTER_FRONT"); sa && atoi(sa) == 1) c->shapes_after_front = true;
     // contours on the host pool unless the process has too few host cores for them
     // (~5 cores per MI355X at 14k images/s, half of them "ui" at 0.7 ms each): then on
     // the GPU.  LLFE_CONTOURS=host / gpu overrides.
@@ -984,8 +961,6 @@ int llfe_init(int device, llfe_ctx **out) {
         if (!strcmp(cm, "gpu")) c->gpu_contours = true;
         if (!strcmp(cm, "host")) c->gpu_contours = false;
     }
-    if (const char *cc = getenv("LLFE_CONCURRENT"); cc && atoi(cc) == 0) c->concurrent = false;
-    if (const char *ff = getenv("LLFE_CT_FORCE_HOST_FALLBACK"); ff && atoi(ff) == 1) c->force_ct_fallback = true;
     gauss_kernel_f32(11, c->sp.k11);
     c->pool = new Pool(default_threads() - 1);
     int nt = c->pool->size() + 1;
@@ -1003,7 +978,7 @@ int llfe_destroy(llfe_ctx *ctx) {
         if (st) (void)hipStreamSynchronize(st);
     for (hipEvent_t e : {ctx->chunk_done[0], ctx->chunk_done[1], ctx->mask_done[0], ctx->mask_done[1], ctx->start_ev,
                          ctx->stream_done[0], ctx->stream_done[1], ctx->mask_ready[0], ctx->mask_ready[1],
-                         ctx->input_ready, ctx->colour_done, ctx->front_done, ctx->h2d_done})
+                         ctx->input_ready, ctx->colour_done, ctx->h2d_done})
         if (e) (void)hipEventDestroy(e);
     for (hipStream_t st : {ctx->streams[0], ctx->streams[1], ctx->col_streams[0], ctx->col_streams[1], ctx->copy_stream})
         if (st) (void)hipStreamDestroy(st);
@@ -1022,16 +997,19 @@ int llfe_set_profiling(llfe_ctx *ctx, int enable) {
 }
 
 int llfe_set_contour_mode(llfe_ctx *ctx, int mode) {
-    if (!ctx || (mode != LLFE_CONTOURS_HOST && mode != LLFE_CONTOURS_GPU)) return LLFE_ERR_INVALID;
+    if (!ctx || (mode != LLFE_CONTOURS_HOST && mode != LLFE_CONTOURS_GPU && mode != LLFE_CONTOURS_GPU_FORCE_FALLBACK))
+        return LLFE_ERR_INVALID;
     if (ctx->inflight[0].busy || ctx->inflight[1].busy)
         return ctx->fail(LLFE_ERR_INVALID, "llfe_set_contour_mode with submitted batches not yet collected");
-    ctx->gpu_contours = mode == LLFE_CONTOURS_GPU;
+    ctx->gpu_contours = mode != LLFE_CONTOURS_HOST;
+    ctx->force_ct_fallback = mode == LLFE_CONTOURS_GPU_FORCE_FALLBACK;
     return LLFE_OK;
 }
 
 int llfe_get_contour_mode(llfe_ctx *ctx) {
     if (!ctx) return LLFE_ERR_INVALID;
-    return ctx->gpu_contours ? LLFE_CONTOURS_GPU : LLFE_CONTOURS_HOST;
+    if (!ctx->gpu_contours) return LLFE_CONTOURS_HOST;
+    return ctx->force_ct_fallback ? LLFE_CONTOURS_GPU_FORCE_FALLBACK : LLFE_CONTOURS_GPU;
 }
 
 int llfe_set_concurrency(llfe_ctx *ctx, int enable) {
@@ -1075,10 +1053,10 @@ int llfe_process_batch(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, ui
     HIPCHK(ctx, hipEventRecord(ctx->start_ev, s));
     for (hipStream_t st : ctx->streams) HIPCHK(ctx, hipStreamWaitEvent(st, ctx->start_ev, 0));
     int prev_i0 = -1, prev_n = 0, slot = 0;
-    const int chunk = chunk_for(ctx->chunk, b->height, b->width);
+    const int chunk = chunk_for(b->height, b->width);
     for (int i0 = 0; i0 < b->n; i0 += chunk) {
         const int n = std::min(chunk, b->n - i0);
-        int rc = enqueue_chunk(ctx, b, features, seed, i0, n, slot, ctx->nstreams > 1 ? slot : 0);
+        int rc = enqueue_chunk(ctx, b, features, seed, i0, n, slot, 0);
         if (rc) return rc;
         if (prev_i0 >= 0) {
             rc = finish_chunk(ctx, b, features, prev_i0, prev_n, slot ^ 1, results, shapes, shape_capacity, total_shapes);
@@ -1164,7 +1142,7 @@ int llfe_process_images(llfe_ctx *ctx, const llfe_image_desc *images, int32_t n,
         const int oh = g.first.first, ow = g.first.second;
         const int64_t P3 = (int64_t)oh * ow * 3;
         // staging passes of at most two device chunks (the batch path pipelines them)
-        const int per = std::max(1, 2 * chunk_for(ctx->chunk, oh, ow));
+        const int per = std::max(1, 2 * chunk_for(oh, ow));
         for (size_t a = 0; a < g.second.size(); a += per) {
             const int nb = (int)std::min<size_t>(per, g.second.size() - a);
             HIPCHK(ctx, ctx->d_ragged.ensure((size_t)nb * P3));
@@ -1239,9 +1217,9 @@ int llfe_submit_batch(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uin
         return ctx->fail(LLFE_ERR_INVALID, "invalid batch n=%d h=%d w=%d", b->n, b->height, b->width);
     if (b->n_colors < 0 || b->n_colors > kMaxColors)
         return ctx->fail(LLFE_ERR_UNSUPPORTED, "n_colors=%d outside [1, %d]", b->n_colors, kMaxColors);
-    if (b->n > chunk_for(ctx->chunk, b->height, b->width))
+    if (b->n > chunk_for(b->height, b->width))
         return ctx->fail(LLFE_ERR_UNSUPPORTED, "llfe_submit_batch: n=%d exceeds one device pass (%d)", b->n,
-                         chunk_for(ctx->chunk, b->height, b->width));
+                         chunk_for(b->height, b->width));
     const int slot = (int)(ctx->next_ticket & 1);
     auto &pd = ctx->inflight[slot];
     if (pd.busy) return ctx->fail(LLFE_ERR_CAPACITY, "two batches already in flight: collect one first");
@@ -1442,7 +1420,7 @@ int llfe_shadow_stats(llfe_ctx *ctx, const uint8_t *bgr, uint64_t *sums, uint64_
 int llfe_color_unique(llfe_ctx *ctx, const llfe_batch *b, uint64_t seed, uint32_t *keys, int64_t *n_unique,
                       llfe_stream stream) {
     if (!ctx || !b || !keys || !n_unique || !valid_dims(b->n, b->height, b->width)) return LLFE_ERR_INVALID;
-    const int cmax = chunk_for(ctx->chunk, b->height, b->width);
+    const int cmax = chunk_for(b->height, b->width);
     if (b->n > cmax) return ctx->fail(LLFE_ERR_UNSUPPORTED, "llfe_color_unique: n > %d", cmax);
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t s = (hipStream_t)stream;

@@ -410,7 +410,7 @@ __global__ __launch_bounds__(NT) void k_stencil(const uint8_t *__restrict__ bgr,
 hipError_t launch_stencil(const uint8_t *bgr, int n, int h, int w, uint8_t *cls, uint8_t *blurred,
                           unsigned long long *shadow_sum, unsigned long long *shadow_cnt, uint2 *tile_part,
                           const StencilParams &p, hipStream_t s) {
-    if (!blurred && !getenv("LLFE_TILED_STENCIL"))
+    if (!blurred)
         return launch_stencil_stream(bgr, n, h, w, cls, shadow_sum, shadow_cnt, tile_part, p, s);
     int ntx = tiles_x(w), nty = tiles_y(h);
     dim3 grid(ntx * nty, n);

@@ -77,7 +77,7 @@ struct Raw {
 // REFLECT_101 columns precomputed in coff (byte offsets within a row)
 __device__ __forceinline__ Raw load_px(const uint8_t *__restrict__ img, int y, int W, int x, bool fast,
                                        const uint32_t coff[4]) {
-    const uint8_t *row = img + (uint32_t)(y * W * 3);  // an image is < 4 GiB
+    const uint8_t *row = img + (size_t)y * W * 3;  // 64-bit: h * w * 3 may pass 2^31
     Raw r;
     if (fast) {
         const uint32_t *p = (const uint32_t *)(row + (uint32_t)(x * 3));
@@ -360,7 +360,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, LLFE_ST_MINW) void k_stencil_s
                 if (yn >= ya && yn < yb) {
                     uint32_t o = 0x01010101u;
                     if (m_cand) o = nms4(a_lo, a_hi, m_lo, m_hi, b_lo, b_hi);
-                    uint8_t *dst = cimg + (uint32_t)(yn * W + x);
+                    uint8_t *dst = cimg + ((size_t)yn * W + x);
                     if (out_fast) {
                         __builtin_nontemporal_store(o, (uint32_t *)dst);
                     } else if (out_lane) {

@@ -68,6 +68,12 @@ def _image_size(b):
 
 
 
+def _raise_pillow_limit(Image) -> None:
+    lim = Image.MAX_IMAGE_PIXELS
+    if lim is not None and lim < MAX_PIXELS:
+        Image.MAX_IMAGE_PIXELS = MAX_PIXELS  # our own MAX_PIXELS check below still applies
+
+
 def decode_bgr(image_bytes: bytes) -> np.ndarray:
     """-> H x W x 3 uint8 BGR, or raises DecodeError (cv2.imdecode returned None)."""
     from PIL import Image, ImageOps, UnidentifiedImageError
@@ -79,6 +85,9 @@ def decode_bgr(image_bytes: bytes) -> np.ndarray:
         out = np.empty((1, hw[0], hw[1], 3), np.uint8)
         if _native([image_bytes], hw[0], hw[1], out, 1)[0] == 0:
             return out[0]
+    # cv2.imdecode accepts up to CV_IO_MAX_IMAGE_PIXELS; Pillow's decompression-bomb
+    # check would refuse images above 2 * MAX_IMAGE_PIXELS (~179 MP by default) at open
+    _raise_pillow_limit(Image)
     try:
         im = Image.open(io.BytesIO(image_bytes))
         if im.width * im.height > MAX_PIXELS:

@@ -17,9 +17,15 @@ import numpy as np
 
 
 def _bgr(image) -> np.ndarray:
+    """H x W x 3 BGR uint8 view of the analyzers' input.  cvtColor(BGR2GRAY) (shape pyc
+    @L18, shadow pyc @L8) takes 3- or 4-channel input and ignores alpha (a BGRA pixel
+    gives the gray value of its B, G, R), so a BGRA image drops its alpha plane here;
+    any other shape or dtype raises as cvtColor does."""
     a = np.asarray(image)
-    if a.dtype != np.uint8 or a.ndim != 3 or a.shape[2] != 3:
-        raise ValueError(f"ShapeAnalyzer expects an H x W x 3 uint8 BGR image, got {a.shape} {a.dtype}")
+    if a.dtype != np.uint8 or a.ndim != 3 or a.shape[2] not in (3, 4):
+        raise ValueError(f"ShapeAnalyzer expects an H x W x 3 (BGR) or x 4 (BGRA) uint8 image, got {a.shape} {a.dtype}")
+    if a.shape[2] == 4:
+        a = a[:, :, :3]
     return np.ascontiguousarray(a)
 
 

@@ -117,3 +117,22 @@ def test_batcher_on_gpu_matches_run_batch():
         assert g["shapes"] == r["shapes"] and g["shadows"] == r["shadows"]
         assert g["colors"].primary is not None and g["colors"].metadata.get("success", True)
     assert max(b.batch_sizes) > 1
+
+
+def test_decode_ignores_pillow_bomb_limit(monkeypatch):
+    """Pillow-decoded formats follow cv2.imdecode's CV_IO_MAX_IMAGE_PIXELS (2^30), not
+    Pillow's decompression-bomb limit: a GIF above a lowered
+    PIL.Image.MAX_IMAGE_PIXELS still decodes."""
+    import io
+
+    from PIL import Image
+
+    from low_level_feature_extraction_amd import decode
+
+    rgb = np.random.default_rng(1).integers(0, 256, (60, 70, 3), dtype=np.uint8)
+    buf = io.BytesIO()
+    Image.fromarray(rgb).convert("P").save(buf, "GIF")
+    monkeypatch.setattr(Image, "MAX_IMAGE_PIXELS", 1000)  # 2 * 1000 < 60 * 70: a bomb to Pillow
+    out = decode.decode_bgr(buf.getvalue())
+    assert out.shape == (60, 70, 3)
+    assert Image.MAX_IMAGE_PIXELS == decode.MAX_PIXELS

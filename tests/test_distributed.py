@@ -144,3 +144,32 @@ def test_gloo_world2_gathers_real_records():
         host, dec, usable = out[rank][1]
         assert host == max(1, min(usable // 2, 16))
         assert dec == max(1, min(usable // 2, 64))
+
+
+def test_gloo_world8_local8_budgets_and_ordered_records():
+    """8 ranks on one node (LOCAL_WORLD_SIZE=8, as torchrun --nproc-per-node 8 sets it):
+    every rank's host contour pool and decode pool get usable cores / 8, and the real
+    per-image records gather to rank 0 in global order (VERDICT r2 next #5)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world, n_total = 8, 19  # ragged shards: 3 ranks hold 3 images, 5 hold 2
+    procs = [ctx.Process(target=_worker_records, args=(r, world, port, n_total, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(world):
+        rank, got, threads = q.get(timeout=300)
+        out[rank] = (got, threads)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    got = out[0][0]
+    assert all(out[r][0] is None for r in range(1, world)) and len(got) == n_total
+    want = _cpu_records(0, n_total)
+    assert [r.shapes for r in got] == [r.shapes for r in want]
+    assert [(r.shadow_sum, r.shadow_count) for r in got] == [(r.shadow_sum, r.shadow_count) for r in want]
+    for rank in range(world):
+        host, dec, usable = out[rank][1]
+        assert host == max(1, min(usable // world, 16))
+        assert dec == max(1, min(usable // world, 64))

@@ -177,14 +177,15 @@ def test_batch_gpu_contour_mode_capacity_regrowth(backend, orc):
 def test_unsupported_gpu_contour_chunk_falls_back_to_host(orc, monkeypatch):
     """A chunk the GPU tracer flags as unsupported (kCtBadTrace / kCtTooWide /
     kCtDpOverflow) is traced on the host pool instead of failing the batch
-    (llfe_api.cpp gpu_shapes_of_chunk); LLFE_CT_FORCE_HOST_FALLBACK=1 takes that path."""
+    (llfe_api.cpp gpu_shapes_of_chunk); contour mode LLFE_CONTOURS_GPU_FORCE_FALLBACK takes
+    that path."""
     from low_level_feature_extraction_amd import synth
     from low_level_feature_extraction_amd.backend import Backend
 
-    monkeypatch.setenv("LLFE_CT_FORCE_HOST_FALLBACK", "1")
     be = Backend(0)
     try:
-        be.set_contour_mode("gpu")
+        be.set_contour_mode("gpu_force_fallback")
+        assert be.contour_mode() == "gpu_force_fallback"
         x = np.stack([synth.synth_numpy(i, 200, 300, seed=71) for i in range(3)])
         res = be.process(x, ("shapes", "shadows"), seed=1)
         for i in range(3):
