@@ -54,19 +54,30 @@ TRAFFIC, VALU_INSTS = _load_traffic()
 
 
 def _cpu_worker(args):
-    i, h, w = args
+    i, h, w, feats, png = args
     import numpy as np
 
     from low_level_feature_extraction_amd import synth
     from oracle import oracle as O
 
     img = synth.synth_numpy(i, h, w, seed=4321)
+    blob = synth.encode_png(img) if png else None
     t = time.perf_counter()
-    noise = O.numpy_noise(h * w, i)                              # color_extractor.py:224
-    centers, counts, nu, _ = O.dominant_colors(img, noise, 5, O.image_rng_state(0, i))
-    O.color_palette(centers, counts)                             # :231-284
-    O.analyze_shapes(img)                                        # shape pyc @L125-189
-    O.analyze_shadow_level(img)                                  # shadow pyc @L12-31
+    if png:  # cv2.imdecode stand-in (no cv2 on the box): Pillow's PNG decoder, BGR out
+        import io
+
+        from PIL import Image
+
+        img = np.ascontiguousarray(np.asarray(Image.open(io.BytesIO(blob)).convert("RGB"))[:, :, ::-1])
+    nu = 0
+    if "colors" in feats:
+        noise = O.numpy_noise(h * w, i)                              # color_extractor.py:224
+        centers, counts, nu, _ = O.dominant_colors(img, noise, 5, O.image_rng_state(0, i))
+        O.color_palette(centers, counts)                             # :231-284
+    if "shapes" in feats:
+        O.analyze_shapes(img)                                        # shape pyc @L125-189
+    if "shadows" in feats:
+        O.analyze_shadow_level(img)                                  # shadow pyc @L12-31
     return time.perf_counter() - t, int(nu)
 
 
@@ -83,10 +94,12 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
-def cpu_baseline(n_images, h, w, workers):
+def cpu_baseline(n_images, h, w, workers, feats=("colors", "shapes", "shadows"), png=False):
     """a process pool of single-threaded workers, one image per task,
     N = the cores this process may use (affinity / cgroup quota: on the GPU box
-    os.cpu_count() reports the whole machine, of which one GPU's share is a slice)."""
+    os.cpu_count() reports the whole machine, of which one GPU's share is a slice).
+    png=True: every task starts from PNG bytes (decode timed; Pillow stands in for
+    cv2.imdecode, utils.py:108-109)."""
     import multiprocessing as mp
 
     from oracle import oracle as O
@@ -95,19 +108,24 @@ def cpu_baseline(n_images, h, w, workers):
     ctx = mp.get_context("fork")
     t0 = time.perf_counter()
     with ctx.Pool(workers) as pool:
-        res = pool.map(_cpu_worker, [(i, h, w) for i in range(n_images)], chunksize=1)
+        res = pool.map(_cpu_worker, [(i, h, w, tuple(feats), png) for i in range(n_images)], chunksize=1)
     wall = time.perf_counter() - t0
+    mean = sum(r[0] for r in res) / len(res)
     return {
-        "value": round(n_images / wall, 3),
+        # steady-state rate of the pool: every core busy on one image at a time
+        "value": round(workers / mean, 3),
+        "value_wall": round(n_images / wall, 3),  # incl. pool start and image synthesis
         "unit": "images/s",
         "cores": workers,
         "kind": "port",
+        "input": "png bytes (Pillow decode timed)" if png else "decoded arrays",
         "cpu_model": cpu_model(),
         "os_cpu_count": os.cpu_count(),
-        "sample": f"{n_images} synthetic {w}x{h} images ({(n_images + 1) // 2} ui / {n_images // 2} photo), full "
-                  f"colors+shapes+shadows via the C oracle (oracle/llfe_oracle.c), {workers} single-threaded worker "
-                  f"processes (one per usable core), {wall:.1f}s wall; mean per-image CPU time "
-                  f"{sum(r[0] for r in res) / len(res):.2f}s",
+        "sample": f"{n_images} synthetic {w}x{h} images ({(n_images + 1) // 2} ui / {n_images // 2} photo), "
+                  f"{'+'.join(feats)} via the C oracle (oracle/llfe_oracle.c), {workers} single-threaded worker "
+                  f"processes (one per usable core), {wall:.1f}s wall (incl. pool start and the images' "
+                  f"synthesis, outside the per-image timer); mean per-image time {mean:.2f}s; value = cores / "
+                  f"mean per-image time",
     }
 
 
@@ -169,38 +187,59 @@ def e2e_host(be, imgs_dev, feats, steps, seed, index_base):
                       f"H2D + full GPU path per batch, two batches in flight (llfe_submit_batch / llfe_collect_batch)"}
 
 
-def e2e_png(be, B, H, W, feats, steps, distinct, seed, fmt="PNG"):
+def e2e_png(be, B, H, W, feats, steps, distinct, seed, fmt="PNG", decode_steps=2):
     """End-to-end from encoded bytes (PNG, or JPEG quality 85):
-    host decode on the decode thread pool, double-buffered against the GPU (batch k+1
-    decodes while batch k runs).  Reported beside `value`, never as it."""
+    host decode on the decode thread pool into pinned host batches, driven through the
+    same serving loop as `value` (llfe_submit_batch / llfe_collect_batch, two batches in
+    flight), so decoding batch k + 1 overlaps batch k's H2D and kernels.  Beside it, the
+    warm decode-only rate of the same threads: the e2e value is decode-bound when it is
+    within 10 % of that rate.  Reported beside `value`, never as it."""
     from concurrent.futures import ThreadPoolExecutor
+
+    import torch
 
     from low_level_feature_extraction_amd import decode
 
     with ThreadPoolExecutor(max_workers=min(distinct, decode.default_decode_threads())) as ex:
-        pngs = list(ex.map(_encode, [(i, H, W, seed, fmt) for i in range(distinct)]))
-    blobs = [pngs[i % distinct] for i in range(B)]
+        blobs_d = list(ex.map(_encode, [(i, H, W, seed, fmt) for i in range(distinct)]))
+    blobs = [blobs_d[i % distinct] for i in range(B)]
     threads = decode.default_decode_threads()
+    # three pinned batches: decoding batch k + 1 may not reuse the buffer of a batch still in flight
+    pinned = [torch.empty((B, H, W, 3), dtype=torch.uint8).pin_memory() for _ in range(3)]
+    bufs = [p.numpy() for p in pinned]
+    # warm, steady-state decode-only rate over all decode threads
+    decode.decode_batch(blobs, bufs[0], threads)
     t = time.perf_counter()
-    decode.decode_many(blobs[:threads], workers=threads)
-    dec_ms = (time.perf_counter() - t) * 1e3  # one image per thread, all threads busy
-    bufs = [np.empty((B, H, W, 3), np.uint8) for _ in range(2)]
+    for k in range(decode_steps):
+        decode.decode_batch(blobs, bufs[k % 3], threads)
+    dec_rate = B * decode_steps / (time.perf_counter() - t)
+    be.process(bufs[0][:2], feats, seed=seed)  # warm the host-input path
     with ThreadPoolExecutor(max_workers=1) as prod:
         t0 = time.perf_counter()
         fut = prod.submit(decode.decode_batch, blobs, bufs[0], threads)
+        pending = []
         for k in range(steps):
             batch = fut.result()
-            if k + 1 < steps:
-                fut = prod.submit(decode.decode_batch, blobs, bufs[(k + 1) % 2], threads)
-            be.process(batch, feats, seed=seed + k)
+            pending.append(be.submit(batch, feats, seed=seed + k))
+            if len(pending) == 2:
+                be.collect(pending.pop(0))
+            if k + 1 < steps:  # buffer (k + 1) % 3 last held batch k - 2, collected above
+                fut = prod.submit(decode.decode_batch, blobs, bufs[(k + 1) % 3], threads)
+        while pending:
+            be.collect(pending.pop(0))
         dt = time.perf_counter() - t0
-    mb = sum(len(p) for p in pngs) / distinct / 2**20
-    return {"value": round(B * steps / dt, 2), "unit": "images/s", "decode_threads": threads,
-            "decode_ms_per_image_per_thread": round(dec_ms, 2),
-            "bound": f"host decode on {threads} threads = this rank's usable cores / LOCAL_WORLD_SIZE",
+    value = B * steps / dt
+    mb = sum(len(p) for p in blobs_d) / distinct / 2**20
+    bound = (f"host decode: e2e is {value / dec_rate:.2f} of the {threads}-thread decode-only rate"
+             if value >= 0.9 * dec_rate else
+             f"not decode alone: e2e is {value / dec_rate:.2f} of the decode-only rate (GPU path / host contour pool)")
+    return {"value": round(value, 2), "unit": "images/s", "decode_threads": threads,
+            "decode_only": round(dec_rate, 2), "decode_ms_per_image_per_thread": round(threads / dec_rate * 1e3, 2),
+            "codecs": decode.decoder_info(), "contours": be.contour_mode(), "bound": bound,
             "sample": f"{steps} x {B} {fmt}-encoded {W}x{H} synthetic images ({distinct} distinct, {mb:.2f} MiB each), "
-                      f"decoded on the host (libllfe {fmt} decoder, cv2.imdecode IMREAD_COLOR semantics) into host "
-                      f"batches, then the full GPU path incl. H2D"}
+                      f"decoded on the host (libllfe {fmt} decoder, cv2.imdecode IMREAD_COLOR semantics) into pinned "
+                      f"host batches, then the full GPU path incl. H2D, two batches in flight; decode-only: "
+                      f"{decode_steps} warm batches on the same threads"}
 
 
 def _config_name(B, H, W, feats, pre):
@@ -228,6 +267,8 @@ def main():
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-images", type=int, default=0, help="0: two images per worker")
     ap.add_argument("--cpu-workers", type=int, default=0, help="0: the usable cores (affinity / cgroup)")
+    ap.add_argument("--cpu-input", choices=["decoded", "png", "both"], default="decoded",
+                    help="CPU baseline input: decoded arrays, PNG bytes (decode timed), or both (cpu_baseline_png)")
     ap.add_argument("--preprocessing", default="auto", choices=["none", "auto", "high_quality", "performance"],
                     help="validate_and_preprocess_image mode the workload is quoted under (the bench checks that "
                          "it does not resize this size: BASELINE configs [3] auto at 1080p, [4] high_quality at 4K)")
@@ -414,12 +455,18 @@ def main():
         if name in kernels:
             kernels[name]["isolated_ms"] = round(st["total_ms"] / max(st["launches"], 1), 4)
 
-    cpu = None
+    cpu = cpu_png = None
     if args.cpu_baseline == "auto" and world == 1:
         from low_level_feature_extraction_amd.decode import usable_cores
 
         workers = args.cpu_workers or usable_cores()
-        cpu = cpu_baseline(args.cpu_images or 2 * workers, H, W, workers)
+        n_cpu = args.cpu_images or 2 * workers
+        if args.cpu_input in ("decoded", "both"):
+            cpu = cpu_baseline(n_cpu, H, W, workers, feats)
+        if args.cpu_input in ("png", "both"):
+            cpu_png = cpu_baseline(n_cpu, H, W, workers, feats, png=True)
+            if cpu is None:
+                cpu = cpu_png
 
     def all_ranks(line, steps):
         """Whole-job rate of an e2e line every rank ran at once (`steps` batches of B per
@@ -483,6 +530,7 @@ def main():
         "shapes_per_image": round(n_shapes / (B * args.steps), 2),
         "per_class": per_class,
         "cpu_baseline": cpu,
+        "cpu_baseline_png": cpu_png if args.cpu_input == "both" else None,
         "e2e_host": e2e_h,
         "e2e_png": e2e,
         "e2e_jpeg": e2e_j,

@@ -330,6 +330,9 @@ int llfe_decode_png_batch(const uint8_t *const *data, const uint64_t *sizes, int
 int llfe_image_info(const uint8_t *data, uint64_t size, int32_t *width, int32_t *height);
 int llfe_decode_batch(const uint8_t *const *data, const uint64_t *sizes, int32_t n, int32_t height, int32_t width,
                       uint8_t *out_bgr, int32_t *status, int32_t threads);
+/* which codecs the host decoders run: "png=libdeflate|zlib;jpeg=libjpeg.so.8|pillow"
+ * (NUL-terminated into buf; LLFE_ERR_CAPACITY if cap is too small) */
+int llfe_decoder_info(char *buf, int32_t cap);
 
 #ifdef __cplusplus
 }

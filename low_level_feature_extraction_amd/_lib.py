@@ -153,6 +153,7 @@ SIGNATURES = {
     "llfe_decode_png_batch": (C.c_int, [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _i32]),
     "llfe_image_info": (C.c_int, [_vp, C.c_uint64, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "llfe_decode_batch": (C.c_int, [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _i32]),
+    "llfe_decoder_info": (C.c_int, [C.c_char_p, _i32]),
 }
 
 _lib = None

@@ -284,6 +284,8 @@ int decode(const uint8_t *data, size_t size, int32_t h, int32_t w, uint8_t *out,
 }  // namespace llfe_jpeg
 
 // used by png_decode.cpp's format-dispatching batch decoder
+bool llfe_jpeg_available() { return llfe_jpeg::api().ok; }
+
 int llfe_jpeg_info_one(const uint8_t *data, size_t size, int32_t *w, int32_t *h, int *ncomp) {
     return llfe_jpeg::info(data, size, w, h, ncomp);
 }

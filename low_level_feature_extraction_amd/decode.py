@@ -49,6 +49,17 @@ def _native(blobs, h, w, out, threads) -> list:
     return list(status)
 
 
+def decoder_info() -> str:
+    """Codecs the native decoders run on this host: "png=libdeflate|zlib;jpeg=..."."""
+    import ctypes as C
+
+    from . import _lib
+
+    buf = C.create_string_buffer(128)
+    _lib.lib().llfe_decoder_info(buf, 128)
+    return buf.value.decode()
+
+
 def _image_size(b):
     """(h, w) of a PNG / JPEG from its header, None for other formats or unreadable
     headers; DecodeError above MAX_PIXELS (cv2.imdecode returns None there)."""
