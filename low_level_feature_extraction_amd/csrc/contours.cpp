@@ -152,39 +152,37 @@ void external_contours_u8(const uint8_t *mask, int h, int w, std::vector<int8_t>
     out.start.push_back((int64_t)(out.xy.size() / 2));
 }
 
-// bits: h rows x wpr u64 words, bit (x & 63) of word (x >> 6)
+// bits: h rows x wpr u64 words, bit (x & 63) of word (x >> 6).  The padded int8 plane
+// stays all-zero between images (`work` is per-thread scratch): only the 64-pixel words
+// with a set bit are expanded, and exactly those are zeroed again afterwards (borders
+// only mark foreground pixels, which lie in them) -- a ui-like 1080p mask touches ~1/10
+// of the plane instead of rewriting all 2 MB of it.
 void external_contours_bits(const uint64_t *bits, int h, int w, int wpr, std::vector<int8_t> &work,
                             Contours &out) {
     const int pitch = w + 2;
-    work.resize((size_t)pitch * (h + 2));
-    std::memset(work.data(), 0, (size_t)pitch);
-    std::memset(work.data() + (size_t)(h + 1) * pitch, 0, (size_t)pitch);
-    std::vector<uint8_t> nz(h, 0);
+    const size_t need = (size_t)pitch * (h + 2);
+    if (work.size() != need) work.assign(need, 0);
+    thread_local std::vector<uint8_t> nz;
+    thread_local std::vector<uint64_t> words;  // (y << 32 | q) of expanded words
+    nz.assign(h, 0);
+    words.clear();
     for (int y = 0; y < h; y++) {
         const uint64_t *wrow = bits + (size_t)y * wpr;
-        int8_t *r = work.data() + (size_t)(y + 1) * pitch;
-        r[0] = 0;
-        r[w + 1] = 0;
-        uint64_t any = 0;
-        for (int q = 0; q < wpr; q++) any |= wrow[q];
-        nz[y] = any != 0;
-        if (!any) {
-            std::memset(r + 1, 0, (size_t)w);
-            continue;
-        }
+        int8_t *r = work.data() + (size_t)(y + 1) * pitch + 1;
         for (int q = 0; q < wpr; q++) {
-            uint64_t v = wrow[q];
-            int x0 = q * 64, n = std::min(64, w - x0);
-            int8_t *dst = r + 1 + x0;
-            if (!v) {
-                std::memset(dst, 0, (size_t)n);
-            } else if (n == 64) {
+            const uint64_t v = wrow[q];
+            if (!v) continue;
+            nz[y] = 1;
+            words.push_back((uint64_t)y << 32 | (uint32_t)q);
+            const int x0 = q * 64, n = std::min(64, w - x0);
+            int8_t *dst = r + x0;
+            if (n == 64) {
                 for (int k = 0; k < 8; k++) {
                     const uint64_t e = kExpand.t[(v >> (8 * k)) & 255];
                     std::memcpy(dst + 8 * k, &e, 8);
                 }
             } else {
-                for (int b = 0; b < n; b++) dst[b] = (int8_t)((v >> b) & 1);
+                for (int b2 = 0; b2 < n; b2++) dst[b2] = (int8_t)((v >> b2) & 1);
             }
         }
     }
@@ -192,6 +190,10 @@ void external_contours_bits(const uint64_t *bits, int h, int w, int wpr, std::ve
     out.start.clear();
     scan_external(work.data(), h, w, nz.data(), out, bits, wpr);
     out.start.push_back((int64_t)(out.xy.size() / 2));
+    for (uint64_t yq : words) {
+        const int y = (int)(yq >> 32), q = (int)(uint32_t)yq, x0 = q * 64;
+        std::memset(work.data() + (size_t)(y + 1) * pitch + 1 + x0, 0, (size_t)std::min(64, w - x0));
+    }
 }
 
 // ---------------------------------------------------------------- geometry
@@ -373,15 +375,18 @@ double hull_area(const int32_t *p, int n, std::vector<int64_t> &tmp, std::vector
     return std::fabs(a * 0.5);
 }
 
-// detect_border_radius (shape pyc @L32-61)
-double border_radius(const int32_t *p, int n, double epsilon_factor, ShapeScratch &sc) {
-    const double perimeter = closed_perimeter(p, n);
+// detect_border_radius (shape pyc @L32-61) given the contour's arcLength and contourArea
+static double border_radius_pa(const int32_t *p, int n, double epsilon_factor, double perimeter, double area,
+                               ShapeScratch &sc) {
     if (dp_vertex_count(p, n, epsilon_factor * perimeter, sc.dp, sc.stack) > 4) {
         double ha = hull_area(p, n, sc.t0, sc.t1);
-        double a = poly_area(p, n);
-        if (ha > 0) return std::max(0.0, (1 - a / ha) * 50.0);
+        if (ha > 0) return std::max(0.0, (1 - area / ha) * 50.0);
     }
     return 0.0;
+}
+
+double border_radius(const int32_t *p, int n, double epsilon_factor, ShapeScratch &sc) {
+    return border_radius_pa(p, n, epsilon_factor, closed_perimeter(p, n), poly_area(p, n), sc);
 }
 
 // One iteration of the analyze_shapes loop (shape pyc @L146-181). Returns false when
@@ -397,7 +402,7 @@ bool classify_contour(const int32_t *p, int n, ShapeScratch &sc, llfe_shape &out
         ymax = std::max(ymax, p[2 * i + 1]);
     }
     const double perimeter = closed_perimeter(p, n);
-    const double br = border_radius(p, n, 0.02, sc);
+    const double br = border_radius_pa(p, n, 0.02, perimeter, area, sc);
     const int nv = dp_vertex_count(p, n, 0.04 * perimeter, sc.dp, sc.stack);
     int type = LLFE_SHAPE_UNKNOWN;
     if (nv == 3) {
