@@ -228,8 +228,10 @@ __device__ __forceinline__ uint32_t nms4(uint32_t alo, uint32_t ahi, uint32_t ml
 }
 
 // CV_32F Gauss11 row pass (s = 0; s = fma(x[k-5], k[k], s) left -> right) of the lane's
-// 4 columns of one blurred row B; taps reach lanes L-2 .. L+2
-__device__ __forceinline__ void rowpass4(uint32_t B, const float *__restrict__ k11, f32x2 &o01, f32x2 &o23) {
+// 4 columns of one blurred row B; taps reach lanes L-2 .. L+2.  Packed FP32: columns c0
+// and c2 share one v_pk_fma_f32 chain (operand pairs (x[k], x[k+2])), c1 and c3 the
+// other ((x[k+1], x[k+3])) -- each lane of a pair is its own exact fma chain, in order
+__device__ __forceinline__ void rowpass4(uint32_t B, const float *__restrict__ k11, f32x2 &o02, f32x2 &o13) {
     const uint32_t l1 = from_left(B), l2 = from_left(l1), r1 = from_right(B), r2 = from_right(r1);
     // taps for column c0 + j: bytes (c0 - 5 + j) .. (c0 + 5 + j); index 0 = c0 - 5
     float x[14];
@@ -241,13 +243,15 @@ __device__ __forceinline__ void rowpass4(uint32_t B, const float *__restrict__ k
         x[9 + i] = (float)byte_of(r1, i);
     }
     x[13] = (float)byte_of(r2, 0);
-    float o[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    f32x2 a = {0.0f, 0.0f}, b = {0.0f, 0.0f};
 #pragma unroll
-    for (int k = 0; k < 11; k++)
-#pragma unroll
-        for (int j = 0; j < 4; j++) o[j] = __builtin_fmaf(x[k + j], k11[k], o[j]);
-    o01 = f32x2{o[0], o[1]};
-    o23 = f32x2{o[2], o[3]};
+    for (int k = 0; k < 11; k++) {
+        const f32x2 w = {k11[k], k11[k]};
+        a = __builtin_elementwise_fma(f32x2{x[k], x[k + 2]}, w, a);
+        b = __builtin_elementwise_fma(f32x2{x[k + 1], x[k + 3]}, w, b);
+    }
+    o02 = a;
+    o13 = b;
 }
 
 template <bool CLS, bool SHD>
@@ -287,6 +291,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, LLFE_ST_MINW) void k_stencil_s
     uint32_t rep_l = 0, rep_r = 0;  // bytes of the lane left of column 0 / right of W-1
     // per-column "inside the image" masks for the magnitude (Canny: no magnitude outside)
     uint32_t in_lo = 0xffffffffu, in_hi = 0xffffffffu;
+    uint32_t in_02 = 0x00010001u, in_13 = 0x00010001u;  // the same, 1 per u16 half, columns (0, 2) / (1, 3)
     if (edge) {
 #pragma unroll
         for (int j = 0; j < 4; j++) {
@@ -295,6 +300,8 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, LLFE_ST_MINW) void k_stencil_s
         }
         in_lo = ((unsigned)x < (unsigned)W ? 0xffffu : 0u) | ((unsigned)(x + 1) < (unsigned)W ? 0xffff0000u : 0u);
         in_hi = ((unsigned)(x + 2) < (unsigned)W ? 0xffffu : 0u) | ((unsigned)(x + 3) < (unsigned)W ? 0xffff0000u : 0u);
+        in_02 = ((unsigned)x < (unsigned)W ? 1u : 0u) | ((unsigned)(x + 2) < (unsigned)W ? 0x10000u : 0u);
+        in_13 = ((unsigned)(x + 1) < (unsigned)W ? 1u : 0u) | ((unsigned)(x + 3) < (unsigned)W ? 0x10000u : 0u);
     }
     float k11[11];
 #pragma unroll
@@ -381,32 +388,48 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, LLFE_ST_MINW) void k_stencil_s
                 if (yg >= ya && yg < yb) {
                     const int kc = (k + kRing - 5) % kRing;
                     const f32x2 w5 = {k11[5], k11[5]};
-                    f32x2 s01 = ra[kc] * w5, s23 = rb[kc] * w5;
+                    // (the symmetric pairs summed first: the packed adds then never feed the
+                    // next instruction, which on gfx950 costs an s_nop)
+                    f32x2 pa[5], pb[5];
 #pragma unroll
                     for (int d = 1; d <= 5; d++) {
                         const int kp = (kc + d) % kRing, kq = (kc + kRing - d) % kRing;
-                        const f32x2 wd = {k11[5 + d], k11[5 + d]};
-                        s01 = __builtin_elementwise_fma(ra[kp] + ra[kq], wd, s01);
-                        s23 = __builtin_elementwise_fma(rb[kp] + rb[kq], wd, s23);
+                        pa[d - 1] = ra[kp] + ra[kq];
+                        pb[d - 1] = rb[kp] + rb[kq];
                     }
-                    const float sj[4] = {s01.x, s01.y, s23.x, s23.y};
-                    const uint32_t bw = bring[kc];
+                    f32x2 s01 = ra[kc] * w5, s23 = rb[kc] * w5;
 #pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        // mean = saturate(rint(s)) (0 <= s <= 255 + rounding, so rint(s) <=
-                        // 255).  s + 2^23 rounds to 2^23 + rint(s) (round-half-even, spacing
-                        // 1 in [2^23, 2^24)), so the bits of the sum are 0x4B000000 + mean and
-                        // b + 2 <= mean <=> (b + 0x4B000001) - bits < 0: one f32 add and
-                        // integer VOP2 ops, which issue at twice the rate of rint / cvt / cmp
-                        const uint32_t r = __float_as_uint(sj[j] + 8388608.0f);
-                        const uint32_t b = byte_of(bw, j);
-                        uint32_t t = (uint32_t)((int32_t)(b + 0x4B000001u - r) >> 31);
-                        // halo lanes are dropped after the loop; only border waves have
-                        // output lanes with columns past W
-                        if (edge) t = (x + j < W) ? t : 0u;
-                        lsum += b & t;
-                        lcnt -= t;  // t = 0 or ~0
+                    for (int d = 1; d <= 5; d++) {
+                        const f32x2 wd = {k11[5 + d], k11[5 + d]};
+                        s01 = __builtin_elementwise_fma(pa[d - 1], wd, s01);
+                        s23 = __builtin_elementwise_fma(pb[d - 1], wd, s23);
                     }
+                    // mean = saturate(rint(s)) (0 <= s <= 255 + rounding, so rint(s) <= 255).
+                    // s + 2^23 rounds to 2^23 + rint(s) (round-half-even, spacing 1 in
+                    // [2^23, 2^24)), so the low 16 bits of the sum are the mean; then two
+                    // pixels per u16 pair: mask = min(sat(mean - (b + 1)), 1) (b + 2 <= mean),
+                    // sum += b . mask and count += 1 . mask by v_dot2_u32_u16
+                    const f32x2 two23 = {8388608.0f, 8388608.0f};
+                    // (ring pairs, and so s01 / s23 here, hold columns (c0, c2) and (c1, c3))
+                    const f32x2 q01 = s01 + two23, q23 = s23 + two23;
+                    const uint32_t mean01 = __builtin_amdgcn_perm(__float_as_uint(q01.y), __float_as_uint(q01.x), 0x05040100u);
+                    const uint32_t mean23 = __builtin_amdgcn_perm(__float_as_uint(q23.y), __float_as_uint(q23.x), 0x05040100u);
+                    const uint32_t bw = bring[kc];
+                    const u16x2 one = {1, 1};
+                    const u16x2 b01 = U(__builtin_amdgcn_perm(0u, bw, 0x0c020c00u));  // bytes 0, 2
+                    const u16x2 b23 = U(__builtin_amdgcn_perm(0u, bw, 0x0c030c01u));  // bytes 1, 3
+                    uint32_t m01 = W32(__builtin_elementwise_min(__builtin_elementwise_sub_sat(U(mean01), b01 + one), one));
+                    uint32_t m23 = W32(__builtin_elementwise_min(__builtin_elementwise_sub_sat(U(mean23), b23 + one), one));
+                    // halo lanes are dropped after the loop; only border waves have output
+                    // lanes with columns past W
+                    if (edge) {
+                        m01 &= in_02;
+                        m23 &= in_13;
+                    }
+                    lsum = __builtin_amdgcn_udot2(b01, U(m01), lsum, false);
+                    lsum = __builtin_amdgcn_udot2(b23, U(m23), lsum, false);
+                    lcnt = __builtin_amdgcn_udot2(U(m01), one, lcnt, false);
+                    lcnt = __builtin_amdgcn_udot2(U(m23), one, lcnt, false);
                 }
             }
             }
