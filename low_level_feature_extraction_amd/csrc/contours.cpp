@@ -227,9 +227,42 @@ double closed_perimeter(const int32_t *p, int n) {
 }
 
 // cv::approxPolyDP(closed=true) vertex count (OpenCV's iterative Douglas-Peucker with
-// farthest-point seeding and the collinear clean-up pass).
+// farthest-point seeding and the collinear clean-up pass).  The seeding (three
+// farthest-point sweeps) does not depend on epsilon, so one DpSeed serves both calls
+// of classify_contour (0.02 and 0.04 x perimeter).
+struct DpSeed {
+    int pos, rs_start, sx, sy;
+    double maxd;
+};
+static DpSeed dp_seed(const int32_t *src, int count) {
+    DpSeed sd{0, 0, 0, 0, 0.0};
+    int pos = 0, rs_start = 0, sx = 0, sy = 0;
+    double maxd = 0;
+    for (int it = 0; it < 3; it++) {  // two (approximately) farthest points
+        maxd = 0;
+        pos = (pos + rs_start) % count;
+        sx = src[2 * pos];
+        sy = src[2 * pos + 1];
+        if (++pos >= count) pos = 0;
+        for (int j = 1; j < count; j++) {
+            const int x = src[2 * pos], y = src[2 * pos + 1];
+            if (++pos >= count) pos = 0;
+            double dx = x - sx, dy = y - sy, d = dx * dx + dy * dy;
+            if (d > maxd) {
+                maxd = d;
+                rs_start = j;
+            }
+        }
+    }
+    sd.pos = pos;
+    sd.rs_start = rs_start;
+    sd.sx = sx;
+    sd.sy = sy;
+    sd.maxd = maxd;
+    return sd;
+}
 int dp_vertex_count(const int32_t *src, int count, double eps, std::vector<int32_t> &dst,
-                    std::vector<int> &stack) {
+                    std::vector<int> &stack, const DpSeed *seed = nullptr) {
     if (count == 0) return 0;
     dst.resize((size_t)2 * count + 2);
     stack.clear();
@@ -240,23 +273,10 @@ int dp_vertex_count(const int32_t *src, int count, double eps, std::vector<int32
     };
     eps *= eps;
     int nout = 0;
-    int pos = 0, rs_start = 0;
-    int sx = 0, sy = 0, x = 0, y = 0;
-    bool le_eps = false;
-    for (int it = 0; it < 3; it++) {  // two (approximately) farthest points
-        double maxd = 0;
-        pos = (pos + rs_start) % count;
-        rd(src, pos, sx, sy);
-        for (int j = 1; j < count; j++) {
-            rd(src, pos, x, y);
-            double dx = x - sx, dy = y - sy, d = dx * dx + dy * dy;
-            if (d > maxd) {
-                maxd = d;
-                rs_start = j;
-            }
-        }
-        le_eps = maxd <= eps;
-    }
+    const DpSeed sd = seed ? *seed : dp_seed(src, count);
+    int pos = sd.pos, rs_start = sd.rs_start;
+    int sx = sd.sx, sy = sd.sy, x = 0, y = 0;
+    const bool le_eps = sd.maxd <= eps;
     if (!le_eps) {
         int a = pos % count;
         int b = (rs_start + a) % count;
@@ -344,12 +364,45 @@ int dp_vertex_count(const int32_t *src, int count, double eps, std::vector<int32
     return newc;
 }
 
-// area of the convex hull (any correct hull gives the same area; Andrew's chain)
+// area of the convex hull (any correct hull gives the same area; Andrew's chain).  Only
+// a column's lowest and highest point can be a hull vertex, so when the contour is not
+// much wider than it has points, the chain runs over the column extremes in column order
+// (one pass to bucket, no sort); the hull -- and so the area sum -- is the same.
 double hull_area(const int32_t *p, int n, std::vector<int64_t> &tmp, std::vector<int64_t> &hull) {
     if (n < 3) return 0.0;
-    tmp.resize(n);
-    for (int i = 0; i < n; i++) tmp[i] = ((int64_t)p[2 * i] << 32) | (uint32_t)(p[2 * i + 1] + 0x40000000);
-    std::sort(tmp.begin(), tmp.end());
+    int xmin = p[0], xmax = p[0];
+    for (int i = 1; i < n; i++) {
+        xmin = std::min(xmin, p[2 * i]);
+        xmax = std::max(xmax, p[2 * i]);
+    }
+    const int64_t span = (int64_t)xmax - xmin + 1;
+    if (span <= 4 * (int64_t)n) {
+        // hull[c] = lowest | highest y + 2^30 of column xmin + c (low / high 32 bits), 0 = empty
+        hull.assign((size_t)span, 0);
+        for (int i = 0; i < n; i++) {
+            const uint32_t y = (uint32_t)(p[2 * i + 1] + 0x40000000);
+            int64_t &v = hull[(size_t)(p[2 * i] - xmin)];
+            const uint32_t lo = (uint32_t)v, hi = (uint32_t)((uint64_t)v >> 32);
+            v = v == 0 ? (int64_t)(((uint64_t)y << 32) | y)
+                       : (int64_t)(((uint64_t)std::max(hi, y) << 32) | std::min(lo, y));
+        }
+        tmp.resize((size_t)2 * span);
+        int m = 0;
+        for (int64_t c = 0; c < span; c++) {
+            const uint64_t v = (uint64_t)hull[(size_t)c];
+            if (!v) continue;
+            const int64_t xk = (int64_t)(xmin + c) << 32;
+            const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+            tmp[(size_t)m++] = xk | lo;
+            if (hi != lo) tmp[(size_t)m++] = xk | hi;
+        }
+        n = m;  // the column extremes, sorted by (x, y)
+    } else {
+        tmp.resize(n);
+        for (int i = 0; i < n; i++) tmp[i] = ((int64_t)p[2 * i] << 32) | (uint32_t)(p[2 * i + 1] + 0x40000000);
+        std::sort(tmp.begin(), tmp.end());
+    }
+    if (n < 3) return 0.0;
     auto X = [](int64_t v) { return (int64_t)(v >> 32); };
     auto Y = [](int64_t v) { return (int64_t)(uint32_t)v - 0x40000000; };
     auto cross = [&](int64_t o, int64_t a, int64_t b) {
@@ -377,8 +430,8 @@ double hull_area(const int32_t *p, int n, std::vector<int64_t> &tmp, std::vector
 
 // detect_border_radius (shape pyc @L32-61) given the contour's arcLength and contourArea
 static double border_radius_pa(const int32_t *p, int n, double epsilon_factor, double perimeter, double area,
-                               ShapeScratch &sc) {
-    if (dp_vertex_count(p, n, epsilon_factor * perimeter, sc.dp, sc.stack) > 4) {
+                               ShapeScratch &sc, const DpSeed *seed = nullptr) {
+    if (dp_vertex_count(p, n, epsilon_factor * perimeter, sc.dp, sc.stack, seed) > 4) {
         double ha = hull_area(p, n, sc.t0, sc.t1);
         if (ha > 0) return std::max(0.0, (1 - area / ha) * 50.0);
     }
@@ -402,8 +455,9 @@ bool classify_contour(const int32_t *p, int n, ShapeScratch &sc, llfe_shape &out
         ymax = std::max(ymax, p[2 * i + 1]);
     }
     const double perimeter = closed_perimeter(p, n);
-    const double br = border_radius_pa(p, n, 0.02, perimeter, area, sc);
-    const int nv = dp_vertex_count(p, n, 0.04 * perimeter, sc.dp, sc.stack);
+    const DpSeed seed = dp_seed(p, n);
+    const double br = border_radius_pa(p, n, 0.02, perimeter, area, sc, &seed);
+    const int nv = dp_vertex_count(p, n, 0.04 * perimeter, sc.dp, sc.stack, &seed);
     int type = LLFE_SHAPE_UNKNOWN;
     if (nv == 3) {
         type = LLFE_SHAPE_TRIANGLE;

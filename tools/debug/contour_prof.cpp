@@ -22,17 +22,17 @@ int main(int argc, char **argv) {
     llfe::ShapeScratch sc;
     std::vector<llfe_shape> shapes;
     using C = std::chrono::steady_clock;
-    double t_trace = 0, t_geo = 0, t_exp = 0;
+    double t_trace = 1e30, t_geo = 1e30;  // min over reps (shared, noisy host)
     for (int r = 0; r < reps; r++) {
         auto a = C::now();
         llfe::external_contours_bits(bits.data(), h, w, wpr, work, c);
         auto b = C::now();
         llfe::shapes_from_contours(c, sc, shapes);
         auto e = C::now();
-        t_trace += std::chrono::duration<double, std::milli>(b - a).count();
-        t_geo += std::chrono::duration<double, std::milli>(e - b).count();
+        t_trace = std::min(t_trace, std::chrono::duration<double, std::milli>(b - a).count());
+        t_geo = std::min(t_geo, std::chrono::duration<double, std::milli>(e - b).count());
     }
     size_t nv = c.xy.size() / 2;
-    printf("%s: contours %zu vertices %zu shapes %zu | expand+scan+trace %.3f ms   geometry %.3f ms\n",
-           argv[1], c.start.size() - 1, nv, shapes.size(), t_trace / reps, t_geo / reps);
+    printf("%s: contours %zu vertices %zu shapes %zu | expand+scan+trace %.3f ms   geometry %.3f ms (min of reps)\n",
+           argv[1], c.start.size() - 1, nv, shapes.size(), t_trace, t_geo);
 }
