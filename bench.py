@@ -331,19 +331,20 @@ def main():
     def barrier():
         shard.barrier(device=local)
 
-    def run_steps(k_steps, seed0, pipelined):
-        """k_steps full passes over the batch.  Pipelined: a serving loop that keeps two
+    def run_steps(k_steps, seed0, pipelined, batch=None):
+        """k_steps full passes over the batch (``imgs`` unless given).  Pipelined: a serving loop that keeps two
         batches in flight (llfe_submit_batch / llfe_collect_batch), so batch k + 1's
         front kernels start in the tail of batch k's k-means; every batch is still
         computed and collected inside the caller's timed region."""
         shapes = 0
+        batch = imgs if batch is None else batch
         if not pipelined:
             for k in range(k_steps):
-                shapes += sum(len(r.shapes) for r in be.process(imgs, feats, seed=seed0 + k, index_base=base))
+                shapes += sum(len(r.shapes) for r in be.process(batch, feats, seed=seed0 + k, index_base=base))
             return shapes
         pending = []
         for k in range(k_steps):
-            pending.append(be.submit(imgs, feats, seed=seed0 + k, index_base=base))
+            pending.append(be.submit(batch, feats, seed=seed0 + k, index_base=base))
             if len(pending) == 2:
                 shapes += sum(len(r.shapes) for r in be.collect(pending.pop(0)))
         while pending:
@@ -356,10 +357,12 @@ def main():
     # hipEvent kernel timings: in the one-batch-at-a-time steps only (two batches in flight
     # overlap, so an event-timed span would include the other batch's kernels)
     be.set_profiling(not pipelined)
+    be.host_contour_stats(reset=True)
     t0 = time.perf_counter()
     n_shapes = run_steps(args.steps, args.seed, pipelined)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
+    host_ct = be.host_contour_stats(reset=True)
     barrier()
     dt = shard.max_over_ranks(t1 - t0, device=coll_dev)
     stats = be.kernel_stats()
@@ -396,18 +399,24 @@ def main():
         per_class = {}
         for kind in ("ui", "photo"):
             cb = synth.synth_batch(B, H, W, seed=args.seed, device=f"cuda:{local}", index_base=base, kind=kind)
-            be.process(cb, feats, seed=args.seed + 2000, index_base=base)  # warm-up
+            run_steps(2, args.seed + 2000, pipelined, cb)  # warm-up
             torch.cuda.synchronize()
             barrier()
+            # the headline's serving loop (two batches in flight when pipelined): a class
+            # bound by the host contour pool shows it here, not the serial tail of one batch
+            be.host_contour_stats(reset=True)
             tc0 = time.perf_counter()
-            for k in range(args.per_class_steps):
-                be.process(cb, feats, seed=args.seed + 3000 + k, index_base=base)
+            run_steps(args.per_class_steps, args.seed + 3000, pipelined, cb)
             torch.cuda.synchronize()
             tc1 = time.perf_counter()
+            hc = be.host_contour_stats(reset=True)
             barrier()
             dtc = shard.max_over_ranks(tc1 - tc0, device=coll_dev)
             per_class[kind] = {"value": round(B * world * args.per_class_steps / dtc, 2), "unit": "images/s",
-                               "ms_per_step": round(dtc / args.per_class_steps * 1e3, 3)}
+                               "ms_per_step": round(dtc / args.per_class_steps * 1e3, 3), "pipelined": pipelined,
+                               # wall share of the timed steps the host contour pool was tracing
+                               "host_contour_busy": round(hc["busy_ms"] / 1e3 / (tc1 - tc0), 3),
+                               "host_contour_ms_per_image": round(hc["busy_ms"] * hc["threads"] / max(hc["images"], 1), 3)}
             del cb
 
     # (the e2e lines run on every rank before rank 0 reports: each rank pays its own
@@ -529,6 +538,8 @@ def main():
         "kernels": kernels,
         "shapes_per_image": round(n_shapes / (B * args.steps), 2),
         "per_class": per_class,
+        # wall share of the timed steps the host contour pool spent tracing (host mode)
+        "host_contour_busy": round(host_ct["busy_ms"] / 1e3 / max(t1 - t0, 1e-9), 3),
         "cpu_baseline": cpu,
         "cpu_baseline_png": cpu_png if args.cpu_input == "both" else None,
         "e2e_host": e2e_h,

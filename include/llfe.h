@@ -151,6 +151,11 @@ int llfe_set_contour_mode(llfe_ctx *ctx, int mode);
 int llfe_get_contour_mode(llfe_ctx *ctx); /* the current mode (or < 0) */
 /* copies up to cap entries, returns the number of kernels with statistics */
 int llfe_kernel_stats(llfe_ctx *ctx, llfe_kernel_stat *out, int32_t cap);
+/* host contour pool (LLFE_CONTOURS_HOST), always counted: wall milliseconds the pool spent
+ * in contour passes, images traced and the pool's thread count since the last reset
+ * (reset != 0 clears after reading).  busy_ms / elapsed wall time near 1 means a
+ * workload is bound by the host pool, not the GPU. */
+int llfe_host_contour_stats(llfe_ctx *ctx, double *busy_ms, int64_t *images, int32_t *threads, int32_t reset);
 
 /* ---- whole hot path ----------------------------------------------------
  * Replaces, per image of the batch:

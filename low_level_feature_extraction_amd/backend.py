@@ -144,6 +144,12 @@ class Backend:
         return {arr[i].name.decode(): {"launches": int(arr[i].launches), "total_ms": float(arr[i].total_ms),
                                        "bytes": float(arr[i].bytes)} for i in range(min(n, 64))}
 
+    def host_contour_stats(self, reset: bool = False) -> dict:
+        """Host contour pool: busy wall ms, images traced and threads since the last reset."""
+        ms, imgs, th = C.c_double(0), C.c_int64(0), C.c_int32(0)
+        self._call("llfe_host_contour_stats", C.byref(ms), C.byref(imgs), C.byref(th), int(reset))
+        return {"busy_ms": ms.value, "images": int(imgs.value), "threads": int(th.value)}
+
     # ------------------------------------------------------------------ helpers
     def _chk(self, rc):
         return L.check(self.ctx, rc)

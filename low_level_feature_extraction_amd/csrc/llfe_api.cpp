@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <cmath>
 #include <condition_variable>
@@ -369,6 +370,8 @@ struct llfe_ctx {
     std::string err;
     Pool *pool = nullptr;
     Profiler prof;
+    double host_ct_ms = 0;       // llfe_host_contour_stats
+    int64_t host_ct_images = 0;
     StencilParams sp{};
     // device workspace
     // per-slot device workspaces (two batches in flight: llfe_submit_batch)
@@ -769,10 +772,13 @@ void host_shapes_from_bits(llfe_ctx *ctx, const uint64_t *hb, int n, int h, int 
     const int wpr = words_per_row(w);
     ctx->img_shapes.resize(n);
     ctx->img_ncont.assign(n, 0);
+    const auto t0 = std::chrono::steady_clock::now();
     ctx->pool->parallel_for(n, [&](int i, int wid) {
         external_contours_bits(hb + (size_t)i * h * wpr, h, w, wpr, ctx->work[wid], ctx->cont[wid]);
         ctx->img_ncont[i] = shapes_from_contours(ctx->cont[wid], ctx->shs[wid], ctx->img_shapes[i]);
     });
+    ctx->host_ct_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    ctx->host_ct_images += n;
     for (int i = 0; i < n; i++) {
         llfe_image_result &r = results[i0 + i];
         r.shape_offset = total_shapes;
@@ -1030,6 +1036,18 @@ int llfe_kernel_stats(llfe_ctx *ctx, llfe_kernel_stat *out, int32_t cap) {
         out[i].bytes = st.bytes;
     }
     return n;
+}
+
+int llfe_host_contour_stats(llfe_ctx *ctx, double *busy_ms, int64_t *images, int32_t *threads, int32_t reset) {
+    if (!ctx) return LLFE_ERR_INVALID;
+    if (busy_ms) *busy_ms = ctx->host_ct_ms;
+    if (images) *images = ctx->host_ct_images;
+    if (threads) *threads = ctx->pool ? ctx->pool->size() : 0;
+    if (reset) {
+        ctx->host_ct_ms = 0;
+        ctx->host_ct_images = 0;
+    }
+    return LLFE_OK;
 }
 
 int llfe_process_batch(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_t seed,
