@@ -140,7 +140,7 @@ int llfe_set_concurrency(llfe_ctx *ctx, int enable);
  * context's host thread pool from the bit-packed mask copied back, overlapping the
  * GPU's k-means; LLFE_CONTOURS_GPU on the GPU (contours_gpu.hip; images up to 4096 wide
  * and 65535 tall, wider ones stay on the host).  Identical results either way.  Initial
- * mode: GPU when the process has fewer than 8 host cores (hardware threads /
+ * mode: GPU when the process has fewer than 4 host cores (hardware threads /
  * LOCAL_WORLD_SIZE), else host; LLFE_CONTOURS=host|gpu overrides. */
 #define LLFE_CONTOURS_HOST 0
 #define LLFE_CONTOURS_GPU 1

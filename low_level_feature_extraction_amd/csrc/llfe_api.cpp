@@ -959,10 +959,12 @@ int llfe_init(int device, llfe_ctx **out) {
             return LLFE_ERR_HIP;
         }
     }
-    // contours on the host pool unless the process has too few host cores for them
-    // (~5 cores per MI355X at 14k images/s, half of them "ui" at 0.7 ms each): then on
-    // the GPU.  LLFE_CONTOURS=host / gpu overrides.
-    c->gpu_contours = cores_per_process() < 8;
+    // contours on the host pool unless the process has too few host cores for them: a
+    // "ui" 1080p image costs 0.28-0.36 ms of one core (round 3, llfe_host_contour_stats), so
+    // 4 cores trace a 512-image 50 % ui step in ~23 ms, inside the ~28 ms GPU step (4 ranks on
+    // 4 cores each: 19.3k images/s host vs 17.7k GPU contours, profiles/r3/multi/); below 4
+    // the GPU path.  LLFE_CONTOURS=host / gpu overrides.
+    c->gpu_contours = cores_per_process() < 4;
     if (const char *cm = getenv("LLFE_CONTOURS")) {
         if (!strcmp(cm, "gpu")) c->gpu_contours = true;
         if (!strcmp(cm, "host")) c->gpu_contours = false;
