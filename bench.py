@@ -221,10 +221,12 @@ def e2e_png(be, B, H, W, feats, steps, distinct, seed, fmt="PNG", decode_steps=2
         for k in range(steps):
             batch = fut.result()
             pending.append(be.submit(batch, feats, seed=seed + k))
+            # decode batch k + 1 while batch k - 1 is collected (its contours on the host
+            # pool): buffer (k + 1) % 3 last held batch k - 2, collected one step earlier
+            if k + 1 < steps:
+                fut = prod.submit(decode.decode_batch, blobs, bufs[(k + 1) % 3], threads)
             if len(pending) == 2:
                 be.collect(pending.pop(0))
-            if k + 1 < steps:  # buffer (k + 1) % 3 last held batch k - 2, collected above
-                fut = prod.submit(decode.decode_batch, blobs, bufs[(k + 1) % 3], threads)
         while pending:
             be.collect(pending.pop(0))
         dt = time.perf_counter() - t0
@@ -274,8 +276,8 @@ def main():
                          "it does not resize this size: BASELINE configs [3] auto at 1080p, [4] high_quality at 4K)")
     ap.add_argument("--e2e-host-steps", type=int, default=8, help="0 disables the decoded-host-array line")
     ap.add_argument("--seed", type=int, default=2025)
-    ap.add_argument("--e2e-png-steps", type=int, default=2, help="0 disables the PNG end-to-end line")
-    ap.add_argument("--e2e-jpeg-steps", type=int, default=2, help="0 disables the JPEG end-to-end line")
+    ap.add_argument("--e2e-png-steps", type=int, default=4, help="0 disables the PNG end-to-end line")
+    ap.add_argument("--e2e-jpeg-steps", type=int, default=6, help="0 disables the JPEG end-to-end line")
     ap.add_argument("--per-class-steps", type=int, default=2,
                     help="steps of an all-ui and an all-photo batch (SURVEY.md 8d per-class throughput); 0 disables")
     ap.add_argument("--contours", choices=["auto", "host", "gpu"], default="auto",
