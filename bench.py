@@ -278,6 +278,10 @@ def main():
     ap.add_argument("--seed", type=int, default=2025)
     ap.add_argument("--e2e-png-steps", type=int, default=4, help="0 disables the PNG end-to-end line")
     ap.add_argument("--e2e-jpeg-steps", type=int, default=6, help="0 disables the JPEG end-to-end line")
+    ap.add_argument("--e2e-at-scale", action="store_true",
+                    help="also run the e2e lines when WORLD_SIZE > 1 (off by default: every rank would pin "
+                         "~10 GB of host batches and decode on its 1/N core share while the scaling run "
+                         "only needs `value`)")
     ap.add_argument("--per-class-steps", type=int, default=2,
                     help="steps of an all-ui and an all-photo batch (SURVEY.md 8d per-class throughput); 0 disables")
     ap.add_argument("--contours", choices=["auto", "host", "gpu"], default="auto",
@@ -292,6 +296,8 @@ def main():
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1 and not args.e2e_at_scale:
+        args.e2e_host_steps = args.e2e_png_steps = args.e2e_jpeg_steps = 0
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # rehearsal of the N-rank path on a one-GPU box: every rank on cuda:0, gloo for the
