@@ -353,7 +353,7 @@ def main():
         pending = []
         for k in range(k_steps):
             pending.append(be.submit(batch, feats, seed=seed0 + k, index_base=base))
-            if len(pending) == 2:
+            if len(pending) == be.inflight:
                 shapes += sum(len(r.shapes) for r in be.collect(pending.pop(0)))
         while pending:
             shapes += sum(len(r.shapes) for r in be.collect(pending.pop(0)))

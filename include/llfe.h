@@ -149,6 +149,10 @@ int llfe_set_concurrency(llfe_ctx *ctx, int enable);
 #define LLFE_CONTOURS_GPU_FORCE_FALLBACK 2
 int llfe_set_contour_mode(llfe_ctx *ctx, int mode);
 int llfe_get_contour_mode(llfe_ctx *ctx); /* the current mode (or < 0) */
+/* batches llfe_submit_batch keeps in flight, each on its own workspace and streams: 2 or
+ * 3 (LLFE_INFLIGHT sets a new context's depth, default 2); only with none in flight */
+int llfe_set_inflight(llfe_ctx *ctx, int32_t depth);
+int llfe_get_inflight(llfe_ctx *ctx); /* the current depth (or < 0) */
 /* copies up to cap entries, returns the number of kernels with statistics */
 int llfe_kernel_stats(llfe_ctx *ctx, llfe_kernel_stat *out, int32_t cap);
 /* host contour pool (LLFE_CONTOURS_HOST), always counted: wall milliseconds the pool spent

@@ -115,6 +115,8 @@ SIGNATURES = {
     "llfe_set_concurrency": (C.c_int, [_vp, C.c_int]),
     "llfe_set_contour_mode": (C.c_int, [_vp, C.c_int]),
     "llfe_get_contour_mode": (C.c_int, [_vp]),
+    "llfe_set_inflight": (C.c_int, [_vp, _i32]),
+    "llfe_get_inflight": (C.c_int, [_vp]),
     "llfe_submit_batch": (C.c_int, [_vp, C.POINTER(LlfeBatch), _u32, _u64, _vp, C.POINTER(C.c_int64)]),
     "llfe_collect_batch": (C.c_int, [_vp, C.c_int64, _vp, _vp, C.c_int64, C.POINTER(C.c_int64)]),
     "llfe_kernel_stats": (C.c_int, [_vp, C.POINTER(LlfeKernelStat), _i32]),

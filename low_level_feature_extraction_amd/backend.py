@@ -133,6 +133,15 @@ class Backend:
         runs k-means; "gpu": on the GPU (contours_gpu.hip).  Identical results."""
         self._call("llfe_set_contour_mode", CONTOUR_MODES[mode])
 
+    @property
+    def inflight(self) -> int:
+        """Batches ``submit`` keeps in flight (2 or 3; llfe_set_inflight)."""
+        return self._call("llfe_get_inflight")
+
+    @inflight.setter
+    def inflight(self, depth: int):
+        self._call("llfe_set_inflight", int(depth))
+
     def contour_mode(self) -> str:
         m = self._call("llfe_get_contour_mode")
         return {v: k for k, v in CONTOUR_MODES.items()}[m]
@@ -313,8 +322,8 @@ class Backend:
     # ------------------------------------------------------------------ async batches
     def submit(self, images, features=("colors", "shapes", "shadows"), seed: int = 0, noise=None,
                index_base: int = 0, n_colors: int = 5) -> int:
-        """Enqueue one batch (llfe_submit_batch) and return its ticket; at most two in
-        flight.  Results: ``collect(ticket)``, in submission order."""
+        """Enqueue one batch (llfe_submit_batch) and return its ticket; at most
+        ``inflight`` (default 2) in flight.  Results: ``collect(ticket)``, in submission order."""
         ptr, n, h, w, on_dev, keep = self._batch_view(images)
         nptr, n_on_dev, nkeep = self._noise_view(noise, n, h, w)
         mask = feature_mask(features)

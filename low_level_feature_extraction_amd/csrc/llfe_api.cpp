@@ -202,6 +202,9 @@ int pil_coeffs(int in_size, double in0, double in1, int out_size, std::vector<in
     return ksize;
 }
 
+// batches in flight at once (llfe_submit_batch; LLFE_INFLIGHT picks 2 or 3)
+constexpr int kMaxSlots = 3;
+
 // device workspace of one chunk in flight
 struct Work {
     DevBuf<uint8_t> d_in, d_cls, d_sroot;
@@ -374,12 +377,13 @@ struct llfe_ctx {
     int64_t host_ct_images = 0;
     StencilParams sp{};
     // device workspace
-    // per-slot device workspaces (two batches in flight: llfe_submit_batch)
-    Work ws[2];
-    hipStream_t streams[2] = {nullptr, nullptr};
-    hipStream_t col_streams[2] = {nullptr, nullptr};  // colour path of workspace q
-    hipEvent_t start_ev = nullptr, stream_done[2] = {nullptr, nullptr};
-    // asynchronous submissions (llfe_submit_batch / llfe_collect_batch): slot = ticket & 1
+    // per-slot device workspaces (up to kMaxSlots batches in flight: llfe_submit_batch)
+    Work ws[kMaxSlots];
+    hipStream_t streams[kMaxSlots] = {};
+    hipStream_t col_streams[kMaxSlots] = {};  // colour path of workspace q
+    hipEvent_t start_ev = nullptr, stream_done[kMaxSlots] = {};
+    // asynchronous submissions (llfe_submit_batch / llfe_collect_batch): slot = ticket % inflight_max
+    int inflight_max = 2;
     struct Pending {
         bool busy = false, done = false;
         llfe_batch b{};
@@ -387,7 +391,12 @@ struct llfe_ctx {
         std::vector<llfe_image_result> res;
         std::vector<llfe_shape> shp;
     };
-    Pending inflight[2];
+    Pending inflight[kMaxSlots];
+    bool any_inflight() const {
+        for (const Pending &p : inflight)
+            if (p.busy) return true;
+        return false;
+    }
     int64_t next_ticket = 0, next_collect = 0;
     DevBuf<uint8_t> d_rsz_tmp, d_rsz_src;
     DevBuf<uint8_t> d_ragged;       // llfe_process_images: one size group's packed images
@@ -397,24 +406,24 @@ struct llfe_ctx {
     DevBuf<unsigned long long> d_text_hist;  // 256 bins + threshold + count of 255s
     // pinned host staging; the per-chunk results are double-buffered so the host can
     // trace chunk c's contours while the GPU runs chunk c + 1
-    HostBuf<uint64_t> h_bits_s[2];
+    HostBuf<uint64_t> h_bits_s[kMaxSlots];
     // GPU contours: per-image (components, ref base, contours, kept, shape base),
     // counters and shape records of each slot
     // contours on the GPU (contours_gpu.hip) or on the host pool from the D2H'd mask
     // (default: the host pool runs them while the GPU is in k-means, which measured
     // faster on one MI355X; LLFE_CONTOURS=gpu or llfe_set_contour_mode switch)
     bool gpu_contours = false;
-    bool slot_gpu_ct[2] = {false, false};  // mode each in-flight slot was enqueued with
-    HostBuf<int> h_ct_info_s[2];
-    HostBuf<CtCounters> h_ct_ctr_s[2];
-    HostBuf<llfe_shape> h_ct_shapes_s[2];
-    int64_t h_ct_shape_cap[2] = {0, 0};
-    HostBuf<unsigned long long> h_shadow_s[2];
-    HostBuf<KmeansImageOut> h_kout_s[2];
-    hipEvent_t chunk_done[2] = {nullptr, nullptr};
+    bool slot_gpu_ct[kMaxSlots] = {};  // mode each in-flight slot was enqueued with
+    HostBuf<int> h_ct_info_s[kMaxSlots];
+    HostBuf<CtCounters> h_ct_ctr_s[kMaxSlots];
+    HostBuf<llfe_shape> h_ct_shapes_s[kMaxSlots];
+    int64_t h_ct_shape_cap[kMaxSlots] = {};
+    HostBuf<unsigned long long> h_shadow_s[kMaxSlots];
+    HostBuf<KmeansImageOut> h_kout_s[kMaxSlots];
+    hipEvent_t chunk_done[kMaxSlots] = {};
     hipEvent_t input_ready = nullptr, colour_done = nullptr;  // intra-chunk stream split
     bool concurrent = true;           // llfe_set_concurrency
-    hipEvent_t mask_done[2] = {nullptr, nullptr};  // shapes/shadows results are on the host
+    hipEvent_t mask_done[kMaxSlots] = {};  // shapes/shadows results are on the host
     // host-input copies of successive chunks / batches are chained (h2d_done of the last
     // one): with two batches in flight, batch k + 1's H2D then starts after batch k's
     // instead of splitting PCIe with it, so batch k's kernels start at half the latency
@@ -424,8 +433,8 @@ struct llfe_ctx {
     // the hysteresis kernels; mask_ready[slot] orders it after them, and a workspace is
     // not overwritten before the D2H that last read it (w_mask_slot) has finished
     hipStream_t copy_stream = nullptr;
-    hipEvent_t mask_ready[2] = {nullptr, nullptr};
-    int w_mask_slot[2] = {-1, -1};
+    hipEvent_t mask_ready[kMaxSlots] = {};
+    int w_mask_slot[kMaxSlots] = {-1, -1, -1};
     HostBuf<KmeansImageOut> h_kout;
     // per-thread host scratch
     std::vector<std::vector<int8_t>> work;
@@ -944,21 +953,27 @@ int llfe_init(int device, llfe_ctx **out) {
     if (hipSetDevice(device) != hipSuccess) return LLFE_ERR_HIP;
     llfe_ctx *c = new llfe_ctx();
     c->device = device;
-    for (hipEvent_t *e : {&c->chunk_done[0], &c->chunk_done[1], &c->mask_done[0], &c->mask_done[1], &c->start_ev,
-                          &c->stream_done[0], &c->stream_done[1], &c->mask_ready[0], &c->mask_ready[1],
-                          &c->input_ready, &c->colour_done, &c->h2d_done})
+    std::vector<hipEvent_t *> evs = {&c->start_ev, &c->input_ready, &c->colour_done, &c->h2d_done};
+    // all streams at the default priority: a higher priority for the shapes streams or
+    // for the colour streams measured neutral (DESIGN.md §3)
+    std::vector<hipStream_t *> sts = {&c->copy_stream};
+    for (int q = 0; q < kMaxSlots; q++) {
+        for (hipEvent_t *e : {&c->chunk_done[q], &c->mask_done[q], &c->stream_done[q], &c->mask_ready[q]})
+            evs.push_back(e);
+        sts.push_back(&c->streams[q]);
+        sts.push_back(&c->col_streams[q]);
+    }
+    for (hipEvent_t *e : evs)
         if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) {
             llfe_destroy(c);
             return LLFE_ERR_HIP;
         }
-    // all streams at the default priority: a higher priority for the shapes streams or
-    // for the colour streams measured neutral (DESIGN.md §3)
-    for (hipStream_t *st : {&c->streams[0], &c->streams[1], &c->col_streams[0], &c->col_streams[1], &c->copy_stream}) {
+    for (hipStream_t *st : sts)
         if (hipStreamCreateWithFlags(st, hipStreamNonBlocking) != hipSuccess) {
             llfe_destroy(c);
             return LLFE_ERR_HIP;
         }
-    }
+    if (const char *fl = getenv("LLFE_INFLIGHT")) c->inflight_max = std::min(kMaxSlots, std::max(2, atoi(fl)));
     // contours on the host pool unless the process has too few host cores for them: a
     // "ui" 1080p image costs 0.28-0.36 ms of one core (round 3, llfe_host_contour_stats), so
     // 4 cores trace a 512-image 50 % ui step in ~23 ms, inside the ~28 ms GPU step (4 ranks on
@@ -982,13 +997,19 @@ int llfe_init(int device, llfe_ctx **out) {
 int llfe_destroy(llfe_ctx *ctx) {
     if (!ctx) return LLFE_OK;
     (void)hipSetDevice(ctx->device);
-    for (hipStream_t st : {ctx->streams[0], ctx->streams[1], ctx->col_streams[0], ctx->col_streams[1], ctx->copy_stream})
+    std::vector<hipEvent_t> evs = {ctx->start_ev, ctx->input_ready, ctx->colour_done, ctx->h2d_done};
+    std::vector<hipStream_t> sts = {ctx->copy_stream};
+    for (int q = 0; q < kMaxSlots; q++) {
+        for (hipEvent_t e : {ctx->chunk_done[q], ctx->mask_done[q], ctx->stream_done[q], ctx->mask_ready[q]})
+            evs.push_back(e);
+        sts.push_back(ctx->streams[q]);
+        sts.push_back(ctx->col_streams[q]);
+    }
+    for (hipStream_t st : sts)
         if (st) (void)hipStreamSynchronize(st);
-    for (hipEvent_t e : {ctx->chunk_done[0], ctx->chunk_done[1], ctx->mask_done[0], ctx->mask_done[1], ctx->start_ev,
-                         ctx->stream_done[0], ctx->stream_done[1], ctx->mask_ready[0], ctx->mask_ready[1],
-                         ctx->input_ready, ctx->colour_done, ctx->h2d_done})
+    for (hipEvent_t e : evs)
         if (e) (void)hipEventDestroy(e);
-    for (hipStream_t st : {ctx->streams[0], ctx->streams[1], ctx->col_streams[0], ctx->col_streams[1], ctx->copy_stream})
+    for (hipStream_t st : sts)
         if (st) (void)hipStreamDestroy(st);
     delete ctx->pool;
     delete ctx;  // DevBuf / HostBuf members free themselves
@@ -1007,7 +1028,7 @@ int llfe_set_profiling(llfe_ctx *ctx, int enable) {
 int llfe_set_contour_mode(llfe_ctx *ctx, int mode) {
     if (!ctx || (mode != LLFE_CONTOURS_HOST && mode != LLFE_CONTOURS_GPU && mode != LLFE_CONTOURS_GPU_FORCE_FALLBACK))
         return LLFE_ERR_INVALID;
-    if (ctx->inflight[0].busy || ctx->inflight[1].busy)
+    if (ctx->any_inflight())
         return ctx->fail(LLFE_ERR_INVALID, "llfe_set_contour_mode with submitted batches not yet collected");
     ctx->gpu_contours = mode != LLFE_CONTOURS_HOST;
     ctx->force_ct_fallback = mode == LLFE_CONTOURS_GPU_FORCE_FALLBACK;
@@ -1019,6 +1040,16 @@ int llfe_get_contour_mode(llfe_ctx *ctx) {
     if (!ctx->gpu_contours) return LLFE_CONTOURS_HOST;
     return ctx->force_ct_fallback ? LLFE_CONTOURS_GPU_FORCE_FALLBACK : LLFE_CONTOURS_GPU;
 }
+
+int llfe_set_inflight(llfe_ctx *ctx, int32_t depth) {
+    if (!ctx || depth < 2 || depth > kMaxSlots) return LLFE_ERR_INVALID;
+    if (ctx->any_inflight())
+        return ctx->fail(LLFE_ERR_INVALID, "llfe_set_inflight with submitted batches not yet collected");
+    ctx->inflight_max = depth;
+    return LLFE_OK;
+}
+
+int llfe_get_inflight(llfe_ctx *ctx) { return ctx ? ctx->inflight_max : LLFE_ERR_INVALID; }
 
 int llfe_set_concurrency(llfe_ctx *ctx, int enable) {
     if (!ctx) return LLFE_ERR_INVALID;
@@ -1060,7 +1091,7 @@ int llfe_process_batch(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, ui
         return ctx->fail(LLFE_ERR_INVALID, "invalid batch n=%d h=%d w=%d", b->n, b->height, b->width);
     if (b->n_colors < 0 || b->n_colors > kMaxColors)
         return ctx->fail(LLFE_ERR_UNSUPPORTED, "n_colors=%d outside [1, %d]", b->n_colors, kMaxColors);
-    if (ctx->inflight[0].busy || ctx->inflight[1].busy)
+    if (ctx->any_inflight())
         return ctx->fail(LLFE_ERR_INVALID, "llfe_process_batch with submitted batches not yet collected");
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t s = (hipStream_t)stream;
@@ -1240,9 +1271,9 @@ int llfe_submit_batch(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uin
     if (b->n > chunk_for(b->height, b->width))
         return ctx->fail(LLFE_ERR_UNSUPPORTED, "llfe_submit_batch: n=%d exceeds one device pass (%d)", b->n,
                          chunk_for(b->height, b->width));
-    const int slot = (int)(ctx->next_ticket & 1);
+    const int slot = (int)(ctx->next_ticket % ctx->inflight_max);
     auto &pd = ctx->inflight[slot];
-    if (pd.busy) return ctx->fail(LLFE_ERR_CAPACITY, "two batches already in flight: collect one first");
+    if (pd.busy) return ctx->fail(LLFE_ERR_CAPACITY, "%d batches already in flight: collect one first", ctx->inflight_max);
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(ctx, hipEventRecord(ctx->start_ev, s));
@@ -1263,7 +1294,7 @@ int llfe_collect_batch(llfe_ctx *ctx, int64_t ticket, llfe_image_result *results
                        int64_t shape_capacity, int64_t *shapes_needed) {
     if (!ctx || !results) return LLFE_ERR_INVALID;
     if (ticket != ctx->next_collect) return ctx->fail(LLFE_ERR_INVALID, "collect tickets in submission order");
-    const int slot = (int)(ticket & 1);
+    const int slot = (int)(ticket % ctx->inflight_max);
     auto &pd = ctx->inflight[slot];
     if (!pd.busy) return ctx->fail(LLFE_ERR_INVALID, "ticket %lld was not submitted", (long long)ticket);
     HIPCHK(ctx, hipSetDevice(ctx->device));

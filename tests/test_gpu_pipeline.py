@@ -120,6 +120,36 @@ def test_submit_collect_matches_process(backend):
     _same(backend.process(x, feats, seed=7, index_base=100), ref_x)  # sync path still fine
 
 
+def test_three_batches_in_flight(backend):
+    """llfe_set_inflight(3): a third workspace; tickets cycle over three slots and still
+    match llfe_process_batch, a fourth submission is refused, and the depth only changes
+    with nothing in flight."""
+    feats = ("colors", "shapes", "shadows")
+    xs = [_batch(4, 120 + 10 * j, 200, seed=40 + j) for j in range(3)]
+    refs = [backend.process(x, feats, seed=j, index_base=10 * j) for j, x in enumerate(xs)]
+    assert backend.inflight == 2
+    with pytest.raises(Exception):
+        backend.inflight = 4
+    backend.inflight = 3
+    try:
+        tickets = [backend.submit(x, feats, seed=j, index_base=10 * j) for j, x in enumerate(xs)]
+        with pytest.raises(Exception):
+            backend.submit(xs[0], feats)
+        with pytest.raises(Exception):
+            backend.inflight = 2
+        want = [0, 1, 2]
+        for rnd in range(5):  # steady state: slot t % 3 reused with another batch's shape
+            _same(backend.collect(tickets.pop(0)), refs[want.pop(0)])
+            j = (rnd + 1) % 3
+            tickets.append(backend.submit(xs[j], feats, seed=j, index_base=10 * j))
+            want.append(j)
+        while tickets:
+            _same(backend.collect(tickets.pop(0)), refs[want.pop(0)])
+    finally:
+        backend.inflight = 2
+    assert backend.inflight == 2
+
+
 def test_many_shapes_capacity_retry(backend, orc):
     x = np.zeros((1, 540, 960, 3), np.uint8)
     for y in range(6, 530, 24):  # a grid of separated 12 x 12 squares -> ~880 shapes
