@@ -208,7 +208,7 @@ constexpr int kMaxSlots = 3;
 // device workspace of one chunk in flight
 struct Work {
     DevBuf<uint8_t> d_in, d_cls, d_sroot;
-    DevBuf<int8_t> d_noise;
+    DevBuf<int8_t> d_noise, d_nfield;  // d_nfield: the launch's noise field (unique.hip)
     DevBuf<uint64_t> d_bits, d_ebits;
     DevBuf<unsigned long long> d_shadow;
     DevBuf<int> d_order, d_parent, d_nroots, d_tlist;
@@ -601,14 +601,19 @@ int color_stage(llfe_ctx *ctx, Work &W, const uint8_t *img, const int8_t *noise,
     uint32_t *hist = W.d_pmeta.p, *cursor = hist + (size_t)n * kParts, *uq = cursor + (size_t)n * kParts,
              *cc = uq + (size_t)n * kParts;
     HIPCHK(ctx, hipMemsetAsync(hist, 0, sizeof(uint32_t) * 2 * n * kParts, s));
-    TIMED(ctx, s, "k_uq_keys", (double)n * P * (noise ? 10 : 7),
-          launch_uq_keys(img, noise, n, h, w, seed, index, key_stride, W.d_raw.p, hist, s));
-    TIMED(ctx, s, "k_uq_scatter", (double)n * P * 8,
-          launch_uq_scatter(W.d_raw.p, n, P, key_stride, hist, cursor, W.d_keys.p, s));
+    if (!noise) {
+        HIPCHK(ctx, W.d_nfield.ensure((size_t)noise_field_pixels(P)));
+        HIPCHK(ctx, launch_uq_noise(noise, W.d_nfield.p, P, seed, s));
+    }
+    // keys are computed twice (histogram, then scatter) instead of written and read back:
+    // the field / parity noise and BGR reads cost less than 8 B of key traffic per pixel
+    TIMED(ctx, s, "k_uq_hist", (double)n * P * (noise ? 6 : 4),
+          launch_uq_hist(img, noise, W.d_nfield.p, n, h, w, seed, index, hist, s));
+    TIMED(ctx, s, "k_uq_scatter", (double)n * P * (noise ? 10 : 8),
+          launch_uq_scatter(img, noise, W.d_nfield.p, n, h, w, seed, index, key_stride, hist, cursor, W.d_keys.p, s));
     // the partitions' sorted unique keys overwrite the (dead) raw keys
     TIMED(ctx, s, "k_uq_part", (double)n * P * 4,
-          launch_uq_part(W.d_keys.p, n, key_stride, hist, W.d_raw.p, W.d_segcubes.p, uq, cc,
-                         s));
+          launch_uq_part(W.d_keys.p, n, key_stride, hist, cursor, W.d_raw.p, W.d_segcubes.p, uq, cc, s));
     TIMED(ctx, s, "k_uq_gather", 0,
           launch_uq_gather(W.d_raw.p, n, key_stride, hist, uq, cc, W.d_segcubes.p, W.d_keys.p, W.d_cubes.p,
                            cube_stride, W.d_nuniq.p, W.d_ncubes.p, s));

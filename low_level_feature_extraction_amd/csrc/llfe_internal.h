@@ -191,12 +191,18 @@ struct KmeansCubes {
 //            counts -> uq, cc (n x 64)
 //   gather:  contiguous sorted keys -> `keys` (may alias part), cube table -> `cubes`,
 //            n_unique, n_cubes
-hipError_t launch_uq_keys(const uint8_t *bgr, const int8_t *noise, int n, int h, int w, uint64_t seed,
-                          ImgIndex index, int64_t key_stride, uint32_t *raw, uint32_t *hist, hipStream_t s);
-hipError_t launch_uq_scatter(const uint32_t *raw, int n, int64_t P, int64_t key_stride, const uint32_t *hist,
-                             uint32_t *cursor, uint32_t *part, hipStream_t s);
-hipError_t launch_uq_part(const uint32_t *part, int n, int64_t key_stride, const uint32_t *hist, uint32_t *skeys,
-                          CubeEnt *seg_cubes, uint32_t *uq, uint32_t *cc, hipStream_t s);
+// noise: the caller's parity noise (n x P x 3 int8) or null -> the launch's noise field
+// (noise_field_pixels(P) bytes at `field`, written by launch_uq_noise; unique.hip)
+int64_t noise_field_pixels(int64_t P);
+hipError_t launch_uq_noise(const int8_t *noise, int8_t *field, int64_t P, uint64_t seed, hipStream_t s);
+hipError_t launch_uq_hist(const uint8_t *bgr, const int8_t *noise, const int8_t *field, int n, int h, int w,
+                          uint64_t seed, ImgIndex index, uint32_t *hist, hipStream_t s);
+hipError_t launch_uq_scatter(const uint8_t *bgr, const int8_t *noise, const int8_t *field, int n, int h, int w,
+                             uint64_t seed, ImgIndex index, int64_t key_stride, const uint32_t *hist, uint32_t *cursor,
+                             uint32_t *part, hipStream_t s);
+hipError_t launch_uq_part(const uint32_t *part, int n, int64_t key_stride, const uint32_t *hist,
+                          const uint32_t *written, uint32_t *skeys, CubeEnt *seg_cubes, uint32_t *uq, uint32_t *cc,
+                          hipStream_t s);
 hipError_t launch_uq_gather(const uint32_t *skeys, int n, int64_t key_stride, const uint32_t *hist, const uint32_t *uq,
                             const uint32_t *cc, const CubeEnt *seg_cubes, uint32_t *keys, CubeEnt *cubes,
                             int64_t cube_stride, int64_t *n_unique, int32_t *n_cubes, hipStream_t s);

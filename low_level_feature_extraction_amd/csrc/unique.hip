@@ -8,9 +8,10 @@
 // (64 partitions; a partition is a contiguous range of the sorted key space), and each
 // partition is deduplicated in a 32 KB LDS bitmap by one workgroup.
 //
-//   k_uq_keys     pixel -> key r<<16|g<<8|b (4 B) + per-image histogram of R
-//   k_uq_scatter  counting sort of the keys by R (block-local LDS sort, 64 global
-//                 cursors per image, coalesced runs out)
+//   k_uq_noise    the launch's noise field (no caller noise): one image's worth, hashed
+//   k_uq_hist     pixel -> key r<<16|g<<8|b -> per-image histogram of R (keys not stored)
+//   k_uq_scatter  the same keys again, counting-sorted by R (block-local LDS sort, 64
+//                 global cursors per image, coalesced runs out)
 //   k_uq_part     one 1024-thread workgroup per (image, R): LDS bitmap of the partition's
 //                 4 x 256 x 256 colours -> its sorted unique keys (written in place of the
 //                 partition) and its 4x4x4 cubes (occupancy mask + exact sums, CubeEnt)
@@ -48,7 +49,7 @@ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
     return x;
 }
 
-__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
@@ -65,68 +66,136 @@ __device__ __forceinline__ uint32_t key_of(int b, int g, int r, int nb, int ng, 
     return ((uint32_t)r << 16) | ((uint32_t)g << 8) | (uint32_t)b;
 }
 
-// grid (blocks, n).  noise: parity-mode int8 stream in RGB order (p*3 + c) or null
-// (counter-based: two 32-bit hashes of (image stream, pixel) -> three 21-bit uniforms).
-__global__ __launch_bounds__(KB) void k_uq_keys(const uint8_t *__restrict__ bgr, const int8_t *__restrict__ noise,
-                                                long long P, long long key_stride, unsigned long long seed,
-                                                ImgIndex index, uint32_t *__restrict__ keys,
-                                                uint32_t *__restrict__ hist) {
+// Noise source of a launch.  Parity mode: the caller's int8 arrays (RGB order p*3 + c,
+// image stride P*3).  Field mode (no caller noise): ONE counter-hashed field of L pixels
+// (L = P rounded up to 16) per launch, k_uq_noise, read by image i rotated by its own
+// offset o_i (a multiple of 16 pixels from a hash of (stream, global index)):
+// noise_i(p) = field[(p + o_i) mod L].  Within an image every pixel draws a distinct field
+// entry, so its noise is i.i.d. int8(N(0, 0.5)) as before; hashing one image's worth per
+// launch instead of every pixel of every image takes the two 32-bit hashes (four
+// quarter-rate multiplies) off the per-pixel path.  A field pixel is one byte, the three
+// channel values n in [-2, 2] in base 5: (nr + 2) * 25 + (ng + 2) * 5 + (nb + 2) -- one
+// coalesced 16-B load per 16 pixels (|n| = 3 has probability 1e-9 and is not drawn).
+struct NoiseSrc {
+    const int8_t *p;
+    long long L;                // 0: parity mode
+    unsigned long long stream;  // field mode
+};
+
+__device__ __forceinline__ long long field_offset(const NoiseSrc &ns, long long gidx) {
+    if (!ns.L) return 0;
+    const uint64_t h = mix64(ns.stream ^ mix64((uint64_t)gidx + 0x4C4C46454C4C4645ull));
+    return (long long)(h % (uint64_t)(ns.L / PPT)) * PPT;
+}
+
+// the noise of pixels p0 .. p0 + 15 of image `img` (p0 a multiple of 16)
+template <bool kField>
+__device__ __forceinline__ const int8_t *noise_at(const NoiseSrc &ns, int img, long long P, long long off,
+                                                   long long p0) {
+    if (!kField) return ns.p + ((size_t)img * P + p0) * 3;
+    long long q = p0 + off;
+    if (q >= ns.L) q -= ns.L;
+    return ns.p + q;
+}
+
+// true when the 64 lanes of the wave hold the 64 consecutive full 16-pixel chunks of one
+// 16-B aligned 3 KB span (lane l at sp = base + 48 l): wave-uniform
+__device__ __forceinline__ bool wave_span(const uint8_t *sp, long long p0, long long P) {
+    const int lane = __lane_id();
+    return __ballot(1) == ~0ull && p0 - 16LL * lane + 1024 <= P && ((((uintptr_t)sp) - 48u * lane) & 15) == 0;
+}
+
+// keys r<<16|g<<8|b of pixels p0 .. p0 + cnt - 1 (cnt <= 16; entries past cnt undefined).
+// span (wave_span): the wave reads its 3 KB of BGR with coalesced 16-B loads (lane l
+// bytes 16 l + 1024 k) and hands each lane its 48 B through the wave's 3 KB of LDS `wst`
+// (reads at a 48-B stride touch all 64 banks once per 16 lanes), instead of 16-B loads at
+// a 48-B lane stride
+template <bool kField>
+__device__ __forceinline__ void chunk_keys(const uint8_t *__restrict__ sp, const int8_t *__restrict__ np_, int cnt,
+                                           bool span, uint4 *wst, uint32_t kv[PPT]) {
+    uint8_t px[3 * PPT];
+    if (span) {
+        const int lane = __lane_id();
+        const uint4 *g = (const uint4 *)(sp - 48 * lane);
+        const uint4 a = g[lane], b = g[64 + lane], c = g[128 + lane];
+        wst[lane] = a;
+        wst[64 + lane] = b;
+        wst[128 + lane] = c;
+        __builtin_amdgcn_wave_barrier();
+        *(uint4 *)&px[0] = wst[3 * lane];
+        *(uint4 *)&px[16] = wst[3 * lane + 1];
+        *(uint4 *)&px[32] = wst[3 * lane + 2];
+        __builtin_amdgcn_wave_barrier();
+    } else if (cnt == PPT && (((uintptr_t)sp) & 15) == 0) {
+        *(uint4 *)&px[0] = ((const uint4 *)sp)[0];
+        *(uint4 *)&px[16] = ((const uint4 *)sp)[1];
+        *(uint4 *)&px[32] = ((const uint4 *)sp)[2];
+    } else {
+        for (int i = 0; i < 3 * PPT; i++) px[i] = i < cnt * 3 ? sp[i] : 0;
+    }
+    if (kField) {
+        uint8_t code[PPT];
+        if (cnt == PPT) {  // (the field is 16-B aligned and offsets are multiples of 16)
+            *(uint4 *)&code[0] = *(const uint4 *)np_;
+        } else {
+            for (int i = 0; i < PPT; i++) code[i] = i < cnt ? (uint8_t)np_[i] : 62;  // 62: no noise
+        }
+#pragma unroll
+        for (int i = 0; i < PPT; i++) {
+            // base-5 digits by 24-bit multiplies: c / 25 = (41 c) >> 10 (c < 125), r / 5 = (13 r) >> 6 (r < 25)
+            const int c = code[i];
+            const int q25 = (c * 41) >> 10, r = c - 25 * q25;
+            const int q5 = (r * 13) >> 6, r5 = r - 5 * q5;
+            kv[i] = key_of(px[3 * i], px[3 * i + 1], px[3 * i + 2], r5 - 2, q5 - 2, q25 - 2);
+        }
+    } else {
+        int8_t nv[3 * PPT];
+        if (cnt == PPT && (((uintptr_t)np_) & 15) == 0) {
+            *(uint4 *)&nv[0] = ((const uint4 *)np_)[0];
+            *(uint4 *)&nv[16] = ((const uint4 *)np_)[1];
+            *(uint4 *)&nv[32] = ((const uint4 *)np_)[2];
+        } else {
+            for (int i = 0; i < 3 * PPT; i++) nv[i] = i < cnt * 3 ? np_[i] : 0;
+        }
+#pragma unroll
+        for (int i = 0; i < PPT; i++)
+            kv[i] = key_of(px[3 * i], px[3 * i + 1], px[3 * i + 2], nv[3 * i + 2], nv[3 * i + 1], nv[3 * i]);
+    }
+}
+
+// grid (ceil(L / 256)): the noise field, pixel q from the counter lo(stream) + golden32 *
+// (q + 1); two hash32 of it (the second keyed by hi(stream)) give three 21-bit uniforms
+__global__ __launch_bounds__(256) void k_uq_noise(int8_t *__restrict__ field, long long L, unsigned long long stream) {
+    const long long q = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (q >= L) return;
+    const uint32_t ctr = (uint32_t)stream + 0x9E3779B9u * (uint32_t)(q + 1);
+    const uint32_t key2 = (uint32_t)(stream >> 32) | 1u;
+    const uint32_t h1 = hash32(ctr), h2 = hash32(ctr ^ key2);
+    const int nr = noise21(h1 & 0x1FFFFFu), ng = noise21((h1 >> 21) | ((h2 & 0x3FFu) << 11)), nb = noise21(h2 >> 11);
+    field[q] = (int8_t)((nr + 2) * 25 + (ng + 2) * 5 + (nb + 2));
+}
+
+// grid (blocks, n): per-image histogram of the keys' red quarter R = r >> 2 (the keys
+// themselves are recomputed by k_uq_scatter rather than written and read back)
+template <bool kField>
+__global__ __launch_bounds__(KB) void k_uq_hist(const uint8_t *__restrict__ bgr, NoiseSrc ns, long long P,
+                                                ImgIndex index, uint32_t *__restrict__ hist) {
     __shared__ uint32_t lh[NPART];
+    __shared__ uint4 wst[KB / 64][192];
     const int img = blockIdx.y;
     const uint8_t *src = bgr + (size_t)img * P * 3;
-    const int8_t *nz = noise ? noise + (size_t)img * P * 3 : nullptr;
-    uint32_t *out = keys + (size_t)img * key_stride;
-    const uint64_t stream = mix64(seed ^ mix64((uint64_t)index.at(img) + 0x4C4C46454C4C4645ull));
+    const long long off = field_offset(ns, index.at(img));
     if (threadIdx.x < NPART) lh[threadIdx.x] = 0;
     __syncthreads();
     const long long nchunks = (P + PPT - 1) / PPT;
     for (long long c = (long long)blockIdx.x * KB + threadIdx.x; c < nchunks; c += (long long)gridDim.x * KB) {
         const long long p0 = c * PPT;
         const int cnt = (int)min((long long)PPT, P - p0);
-        uint8_t px[3 * PPT];
-        int8_t nv[3 * PPT];
-        const uint8_t *sp = src + p0 * 3;
-        if (cnt == PPT && (((uintptr_t)sp) & 15) == 0) {
-            *(uint4 *)&px[0] = ((const uint4 *)sp)[0];
-            *(uint4 *)&px[16] = ((const uint4 *)sp)[1];
-            *(uint4 *)&px[32] = ((const uint4 *)sp)[2];
-        } else {
-            for (int i = 0; i < 3 * PPT; i++) px[i] = i < cnt * 3 ? sp[i] : 0;
-        }
-        if (nz) {
-            const int8_t *np_ = nz + p0 * 3;
-            if (cnt == PPT && (((uintptr_t)np_) & 15) == 0) {
-                *(uint4 *)&nv[0] = ((const uint4 *)np_)[0];
-                *(uint4 *)&nv[16] = ((const uint4 *)np_)[1];
-                *(uint4 *)&nv[32] = ((const uint4 *)np_)[2];
-            } else {
-                for (int i = 0; i < 3 * PPT; i++) nv[i] = i < cnt * 3 ? np_[i] : 0;
-            }
-        }
         uint32_t kv[PPT];
-        uint32_t run_bin = 0xFFFFFFFFu, run_len = 0;
-        // counter of pixel p: lo(stream) + golden32 * (p + 1), stepped by one add per pixel;
-        // two hash32 of it (the second keyed by hi(stream)) give the 63 noise bits
-        uint32_t ctr = (uint32_t)stream + 0x9E3779B9u * (uint32_t)(p0 + 1);
-        const uint32_t key2 = (uint32_t)(stream >> 32) | 1u;
-#pragma unroll
-        for (int i = 0; i < PPT; i++) {
-            int nr, ng, nb;
-            if (nz) {
-                nr = nv[3 * i];
-                ng = nv[3 * i + 1];
-                nb = nv[3 * i + 2];
-            } else {
-                const uint32_t h1 = hash32(ctr), h2 = hash32(ctr ^ key2);
-                ctr += 0x9E3779B9u;
-                nr = noise21(h1 & 0x1FFFFFu);
-                ng = noise21((h1 >> 21) | ((h2 & 0x3FFu) << 11));
-                nb = noise21(h2 >> 11);
-            }
-            kv[i] = key_of(px[3 * i], px[3 * i + 1], px[3 * i + 2], nb, ng, nr);
-        }
-        // partition histogram: neighbouring pixels usually share their red quarter, so a
-        // lane whose 16 pixels all do adds them with one LDS atomic; the others count runs
+        const bool span = wave_span(src + p0 * 3, p0, P);
+        chunk_keys<kField>(src + p0 * 3, noise_at<kField>(ns, img, P, off, p0), cnt, span, wst[threadIdx.x >> 6], kv);
+        // neighbouring pixels usually share their red quarter, so a lane whose 16 pixels
+        // all do adds them with one LDS atomic; the others count runs
         const uint32_t bin0 = kv[0] >> 18;
         bool same = cnt == PPT;
 #pragma unroll
@@ -134,9 +203,10 @@ __global__ __launch_bounds__(KB) void k_uq_keys(const uint8_t *__restrict__ bgr,
         if (same) {
             atomicAdd(&lh[bin0], (uint32_t)PPT);
         } else {
+            uint32_t run_bin = 0xFFFFFFFFu, run_len = 0;
 #pragma unroll
             for (int i = 0; i < PPT; i++) {
-                if (i < cnt) {  // run-length histogram
+                if (i < cnt) {
                     const uint32_t bin = kv[i] >> 18;
                     if (bin != run_bin) {
                         if (run_len) atomicAdd(&lh[run_bin], run_len);
@@ -147,14 +217,6 @@ __global__ __launch_bounds__(KB) void k_uq_keys(const uint8_t *__restrict__ bgr,
                 }
             }
             if (run_len) atomicAdd(&lh[run_bin], run_len);
-        }
-        uint32_t *op = out + p0;
-        if (cnt == PPT && (((uintptr_t)op) & 15) == 0) {
-#pragma unroll
-            for (int q = 0; q < PPT / 4; q++)
-                ((uint4 *)op)[q] = make_uint4(kv[4 * q], kv[4 * q + 1], kv[4 * q + 2], kv[4 * q + 3]);
-        } else {
-            for (int i = 0; i < cnt; i++) op[i] = kv[i];
         }
     }
     __syncthreads();
@@ -175,13 +237,16 @@ __device__ __forceinline__ uint32_t part_base(const uint32_t *h, int lane, uint3
 
 constexpr int SK = KB * PPT;  // keys per scatter block step
 
-__global__ __launch_bounds__(KB) void k_uq_scatter(const uint32_t *__restrict__ keys, long long P, long long key_stride,
+template <bool kField>
+__global__ __launch_bounds__(KB) void k_uq_scatter(const uint8_t *__restrict__ bgr, NoiseSrc ns, long long P,
+                                                   long long key_stride, ImgIndex index,
                                                    const uint32_t *__restrict__ hist, uint32_t *__restrict__ cursor,
                                                    uint32_t *__restrict__ part) {
     __shared__ uint32_t base[NPART], cnt[NPART], lbase[NPART], gbase[NPART];
-    __shared__ uint32_t stage[SK];
+    __shared__ __attribute__((aligned(16))) uint32_t stage[SK];
     const int img = blockIdx.y, t = threadIdx.x;
-    const uint32_t *in = keys + (size_t)img * key_stride;
+    const uint8_t *src = bgr + (size_t)img * P * 3;
+    const long long off = field_offset(ns, index.at(img));
     uint32_t *out = part + (size_t)img * key_stride;
     if (t < 64) {
         uint32_t tot;
@@ -195,19 +260,11 @@ __global__ __launch_bounds__(KB) void k_uq_scatter(const uint32_t *__restrict__ 
         if (t < NPART) cnt[t] = 0;
         __syncthreads();
         uint32_t kv[PPT], pos[PPT];
-        if (n == PPT && (((uintptr_t)(in + p0)) & 15) == 0) {
-#pragma unroll
-            for (int q = 0; q < PPT / 4; q++) {
-                const uint4 v = ((const uint4 *)(in + p0))[q];
-                kv[4 * q] = v.x;
-                kv[4 * q + 1] = v.y;
-                kv[4 * q + 2] = v.z;
-                kv[4 * q + 3] = v.w;
-            }
-        } else {
-#pragma unroll
-            for (int i = 0; i < PPT; i++) kv[i] = i < n ? in[p0 + i] : 0u;
-        }
+        // (the staging uses this wave's 3 KB of `stage`, free until the keys are sorted into it)
+        const bool span = wave_span(src + p0 * 3, p0, P);
+        if (n > 0)
+            chunk_keys<kField>(src + p0 * 3, noise_at<kField>(ns, img, P, off, p0), n, span,
+                               (uint4 *)stage + 192 * (t >> 6), kv);
         // rank within the block's bin: one LDS atomic per run of equal bins.  Static
         // register indexing only: the atomic sits on each run's last key and returns the
         // run's base, which a backward pass hands to the run's other keys.
@@ -290,11 +347,12 @@ __device__ __forceinline__ unsigned long long scan_u64_1024(unsigned long long v
     return r;
 }
 
-// grid (64, n).  Reads the partition's keys from `part`, writes (in place of those
-// keys, so capacity is the partition size) the sorted unique keys to `skeys`, and up
-// to 4096 cube entries to `seg_cubes`.
+// grid (64, n).  Reads the partition's keys from `part` (`written` of them: the
+// partition's hist count), writes (in place of those keys, so capacity is the partition
+// size) the sorted unique keys to `skeys`, and up to 4096 cube entries to `seg_cubes`.
 __global__ __launch_bounds__(UT) void k_uq_part(const uint32_t *__restrict__ part, long long key_stride,
-                                                const uint32_t *__restrict__ hist, uint32_t *__restrict__ skeys,
+                                                const uint32_t *__restrict__ hist, const uint32_t *__restrict__ written,
+                                                uint32_t *__restrict__ skeys,
                                                 CubeEnt *__restrict__ seg_cubes,
                                                 uint32_t *__restrict__ uq, uint32_t *__restrict__ cc) {
     __shared__ __attribute__((aligned(16))) uint32_t W[4 * 2048];  // rows r = 4R + i, word g << 3 | b >> 5
@@ -306,24 +364,25 @@ __global__ __launch_bounds__(UT) void k_uq_part(const uint32_t *__restrict__ par
         const uint32_t b = part_base(hist + (size_t)img * NPART, t, &tot);
         if (t == R) {
             sbase = b;
-            scount = hist[(size_t)img * NPART + R];
+            scount = written[(size_t)img * NPART + R];
         }
     }
-    for (int i = t; i < 4 * 2048 / 4; i += UT) ((uint4 *)W)[i] = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();
     const uint32_t start = sbase, count = scount;
-    if (count == 0) {
+    if (count == 0) {  // (most partitions of a flat "ui" image): before zeroing the bitmap
         if (t == 0) {
             uq[(size_t)img * NPART + R] = 0;
             cc[(size_t)img * NPART + R] = 0;
         }
         return;
     }
+    for (int i = t; i < 4 * 2048 / 4; i += UT) ((uint4 *)W)[i] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
     const uint32_t *in = part + (size_t)img * key_stride + start;
-    // 8 independent (coalesced) key loads in flight per thread before their LDS atomics:
-    // one load per atomic in sequence left the workgroup waiting on HBM latency
+    // 16 independent (coalesced) key loads in flight per thread before their LDS atomics
+    // (8: +5 % kernel time, 4: +10 %): the workgroup otherwise waits on HBM latency
 #ifndef LLFE_UQ_LOADS
-#define LLFE_UQ_LOADS 8
+#define LLFE_UQ_LOADS 16
 #endif
     constexpr int KB8 = LLFE_UQ_LOADS;
     for (uint32_t base = 0; base < count; base += UT * KB8) {
@@ -336,28 +395,43 @@ __global__ __launch_bounds__(UT) void k_uq_part(const uint32_t *__restrict__ par
 #pragma unroll
         for (int j = 0; j < KB8; j++) {
             const uint32_t k = kk[j];
-            if (k != 0xFFFFFFFFu) atomicOr(&W[((k >> 16) & 3u) * 2048 + ((k >> 5) & 2047u)], 1u << (k & 31u));
+            // flat regions put one colour in every lane: test the bit with a (broadcast)
+            // read first, so a wave does not serialise 64 atomics on one LDS word
+            const uint32_t wi = ((k >> 16) & 3u) * 2048 + ((k >> 5) & 2047u), bit = 1u << (k & 31u);
+            if (k != 0xFFFFFFFFu && !(W[wi] & bit)) atomicOr(&W[wi], bit);
         }
     }
     __syncthreads();
-    // (a) unique keys in ascending order: thread t owns words 8t .. 8t + 7
+    // (a) unique keys in ascending order: thread t owns words q * 1024 + t (q < 8), so a
+    // store instruction's lanes write neighbouring runs of the output (a few cache lines)
+    // rather than 64 runs spread over the partition.  The per-slice prefixes of the 8
+    // popcounts (<= 32768 each) go through two scans of four packed 16-bit fields.
     {
-        uint32_t w8[8], c = 0;
+        uint32_t wq[8];
+        unsigned long long c0 = 0, c1 = 0;
 #pragma unroll
         for (int q = 0; q < 8; q++) {
-            w8[q] = W[t * 8 + q];
-            c += __popc(w8[q]);
+            wq[q] = W[q * 1024 + t];
+            const unsigned long long c = (unsigned long long)__popc(wq[q]);
+            if (q < 4) c0 |= c << (16 * q);
+            else c1 |= c << (16 * (q - 4));
         }
-        unsigned long long tot;
-        uint32_t pos = (uint32_t)scan_u64_1024(c, tmp, &tot);
+        unsigned long long tot0, tot1;
+        const unsigned long long p0 = scan_u64_1024(c0, tmp, &tot0);
+        const unsigned long long p1 = scan_u64_1024(c1, tmp, &tot1);
         uint32_t *o = skeys + (size_t)img * key_stride + start;
+        uint32_t sbase_q = 0;
 #pragma unroll
         for (int q = 0; q < 8; q++) {
-            const int word = t * 8 + q;  // = i * 2048 + (g << 3 | b >> 5)
+            const unsigned long long pk = q < 4 ? p0 : p1, tk = q < 4 ? tot0 : tot1;
+            const int sh = 16 * (q & 3);
+            uint32_t pos = sbase_q + (uint32_t)((pk >> sh) & 0xFFFFu);
+            sbase_q += (uint32_t)((tk >> sh) & 0xFFFFu);
+            const int word = q * 1024 + t;  // = i * 2048 + (g << 3 | b >> 5)
             const uint32_t kb = ((uint32_t)(4 * R + (word >> 11)) << 16) | ((uint32_t)(word & 2047) << 5);
-            for (uint32_t m = w8[q]; m; m &= m - 1) o[pos++] = kb | (uint32_t)__builtin_ctz(m);
+            for (uint32_t m = wq[q]; m; m &= m - 1) o[pos++] = kb | (uint32_t)__builtin_ctz(m);
         }
-        if (t == 0) uq[(size_t)img * NPART + R] = (uint32_t)tot;
+        if (t == 0) uq[(size_t)img * NPART + R] = sbase_q;
     }
     // (b) 4x4x4 cubes of the partition in cube-id order (see CubeEnt): thread t owns
     // cubes (G = t / 16, B = 4 (t % 16) .. + 3); bit i*16 + j*4 + bb = (4R+i, 4G+j, 4B+bb)
@@ -460,29 +534,56 @@ __global__ __launch_bounds__(GT) void k_uq_gather(const uint32_t *__restrict__ s
 
 }  // namespace
 
-hipError_t launch_uq_keys(const uint8_t *bgr, const int8_t *noise, int n, int h, int w, uint64_t seed,
-                          ImgIndex index, int64_t key_stride, uint32_t *keys, uint32_t *hist, hipStream_t s) {
+namespace {
+NoiseSrc noise_src(const int8_t *noise, int8_t *field, int64_t P, uint64_t seed) {
+    if (noise) return NoiseSrc{noise, 0, 0};
+    return NoiseSrc{field, noise_field_pixels(P), (unsigned long long)mix64(seed ^ 0x4C4C46454C4C4645ull)};
+}
+}  // namespace
+
+int64_t noise_field_pixels(int64_t P) { return (std::max<int64_t>(P, 1) + PPT - 1) / PPT * PPT; }
+
+hipError_t launch_uq_noise(const int8_t *noise, int8_t *field, int64_t P, uint64_t seed, hipStream_t s) {
+    if (noise) return hipSuccess;
+    const NoiseSrc ns = noise_src(noise, field, P, seed);
+    hipLaunchKernelGGL(k_uq_noise, dim3((unsigned)((ns.L + 255) / 256)), dim3(256), 0, s, field, ns.L, ns.stream);
+    return hipGetLastError();
+}
+
+hipError_t launch_uq_hist(const uint8_t *bgr, const int8_t *noise, const int8_t *field, int n, int h, int w,
+                          uint64_t seed, ImgIndex index, uint32_t *hist, hipStream_t s) {
     const long long P = (long long)h * w;
     const long long per_block = (long long)KB * PPT * 4;
     int bx = (int)std::min((P + per_block - 1) / per_block, 2048LL);
     if (bx < 1) bx = 1;
-    hipLaunchKernelGGL(k_uq_keys, dim3(bx, n), dim3(KB), 0, s, bgr, noise, P, (long long)key_stride,
-                       (unsigned long long)seed, index, keys, hist);
+    const NoiseSrc ns = noise_src(noise, (int8_t *)field, P, seed);
+    if (ns.L)
+        hipLaunchKernelGGL(k_uq_hist<true>, dim3(bx, n), dim3(KB), 0, s, bgr, ns, P, index, hist);
+    else
+        hipLaunchKernelGGL(k_uq_hist<false>, dim3(bx, n), dim3(KB), 0, s, bgr, ns, P, index, hist);
     return hipGetLastError();
 }
 
-hipError_t launch_uq_scatter(const uint32_t *keys, int n, int64_t P, int64_t key_stride, const uint32_t *hist,
-                             uint32_t *cursor, uint32_t *part, hipStream_t s) {
+hipError_t launch_uq_scatter(const uint8_t *bgr, const int8_t *noise, const int8_t *field, int n, int h, int w,
+                             uint64_t seed, ImgIndex index, int64_t key_stride, const uint32_t *hist, uint32_t *cursor,
+                             uint32_t *part, hipStream_t s) {
+    const int64_t P = (int64_t)h * w;
     int bx = (int)std::min((P + SK * 2 - 1) / (SK * 2), (int64_t)2048);
     if (bx < 1) bx = 1;
-    hipLaunchKernelGGL(k_uq_scatter, dim3(bx, n), dim3(KB), 0, s, keys, (long long)P, (long long)key_stride, hist,
-                       cursor, part);
+    const NoiseSrc ns = noise_src(noise, (int8_t *)field, P, seed);
+    if (ns.L)
+        hipLaunchKernelGGL(k_uq_scatter<true>, dim3(bx, n), dim3(KB), 0, s, bgr, ns, (long long)P, (long long)key_stride,
+                           index, hist, cursor, part);
+    else
+        hipLaunchKernelGGL(k_uq_scatter<false>, dim3(bx, n), dim3(KB), 0, s, bgr, ns, (long long)P,
+                           (long long)key_stride, index, hist, cursor, part);
     return hipGetLastError();
 }
 
-hipError_t launch_uq_part(const uint32_t *part, int n, int64_t key_stride, const uint32_t *hist, uint32_t *skeys,
-                          CubeEnt *seg_cubes, uint32_t *uq, uint32_t *cc, hipStream_t s) {
-    hipLaunchKernelGGL(k_uq_part, dim3(NPART, n), dim3(UT), 0, s, part, (long long)key_stride, hist, skeys,
+hipError_t launch_uq_part(const uint32_t *part, int n, int64_t key_stride, const uint32_t *hist,
+                          const uint32_t *written, uint32_t *skeys, CubeEnt *seg_cubes, uint32_t *uq, uint32_t *cc,
+                          hipStream_t s) {
+    hipLaunchKernelGGL(k_uq_part, dim3(NPART, n), dim3(UT), 0, s, part, (long long)key_stride, hist, written, skeys,
                        seg_cubes, uq, cc);
     return hipGetLastError();
 }
