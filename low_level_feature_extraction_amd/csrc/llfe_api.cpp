@@ -281,12 +281,14 @@ struct Profiler {
         (void)hipEventRecord(b, s);
         pending.push_back(Rec{kid(name), cur_slot, a, b, bytes});
     }
-    // call after the slot's (slot < 0: every) stream work has completed
+    // call after the slot's (slot == -1: every) stream work has completed
     void collect(int slot = -1) {
         size_t keep = 0;
         for (size_t i = 0; i < pending.size(); i++) {
             Rec &r = pending[i];
-            if (slot >= 0 && r.slot != slot) {
+            // slot < -1: only records whose end event has completed (the stage entry
+            // points, llfe_color_unique etc., run on the caller's stream and never wait)
+            if ((slot >= 0 && r.slot != slot) || (slot < -1 && hipEventQuery(r.b) != hipSuccess)) {
                 pending[keep++] = r;
                 continue;
             }
@@ -1064,6 +1066,7 @@ int llfe_set_concurrency(llfe_ctx *ctx, int enable) {
 
 int llfe_kernel_stats(llfe_ctx *ctx, llfe_kernel_stat *out, int32_t cap) {
     if (!ctx) return LLFE_ERR_INVALID;
+    if (!ctx->any_inflight()) ctx->prof.collect(-2);  // completed launches of the stage entry points
     int n = (int)ctx->prof.stats.size();
     for (int i = 0; i < n && i < cap && out; i++) {
         const auto &st = ctx->prof.stats[i];
