@@ -7,7 +7,7 @@
 set -u -o pipefail
 O=gpurun_out/configs_r3
 mkdir -p $O
-B="python bench.py --cpu-input both --e2e-png-steps 0 --e2e-jpeg-steps 0 --e2e-host-steps 0 --per-class-steps 0 --steps 5 --warmup 2"
+B="python bench.py --cpu-input both --e2e-png-steps 0 --e2e-jpeg-steps 0 --e2e-host-steps 0 --per-class-steps 0 --steps 20 --warmup 5"
 timeout -k 10 300 $B --batch 64 --height 512 --width 512 --features colors --cpu-images 64 > $O/c0_512_colors.json &&
 timeout -k 10 400 $B --batch 256 --features colors > $O/c1_colors_256.json &&
 timeout -k 10 400 $B --batch 256 --features colors,shapes > $O/c2_colors_shapes_256.json &&
