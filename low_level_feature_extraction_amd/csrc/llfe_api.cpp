@@ -213,7 +213,7 @@ struct Work {
     DevBuf<unsigned long long> d_shadow;
     DevBuf<int> d_order, d_parent, d_nroots, d_tlist;
     DevBuf<uint16_t> d_lab, d_roots;
-    DevBuf<uint32_t> d_raw, d_keys, d_kscratch, d_pmeta, d_tstrong;
+    DevBuf<uint32_t> d_raw, d_keys, d_kscratch, d_pmeta, d_tstrong, d_segtab;  // d_segtab: k_uq_scatter's run table
     DevBuf<CubeEnt> d_segcubes, d_cubes;
     DevBuf<int32_t> d_ncubes;
     DevBuf<int64_t> d_nuniq;
@@ -600,22 +600,21 @@ int color_stage(llfe_ctx *ctx, Work &W, const uint8_t *img, const int8_t *noise,
     HIPCHK(ctx, W.d_pmeta.ensure((size_t)n * kParts * 4));
     HIPCHK(ctx, W.d_nuniq.ensure(n));
     HIPCHK(ctx, W.d_ncubes.ensure(n));
-    uint32_t *hist = W.d_pmeta.p, *cursor = hist + (size_t)n * kParts, *uq = cursor + (size_t)n * kParts,
-             *cc = uq + (size_t)n * kParts;
-    HIPCHK(ctx, hipMemsetAsync(hist, 0, sizeof(uint32_t) * 2 * n * kParts, s));
+    // (d_pmeta: hist, a spare row, uq, cc; k-means reads uq)
+    uint32_t *hist = W.d_pmeta.p, *uq = hist + (size_t)2 * n * kParts, *cc = uq + (size_t)n * kParts;
+    HIPCHK(ctx, hipMemsetAsync(hist, 0, sizeof(uint32_t) * n * kParts, s));
+    HIPCHK(ctx, W.d_segtab.ensure((size_t)n * uq_steps(P) * kParts));
     if (!noise) {
         HIPCHK(ctx, W.d_nfield.ensure((size_t)noise_field_pixels(P)));
         HIPCHK(ctx, launch_uq_noise(noise, W.d_nfield.p, P, seed, s));
     }
-    // keys are computed twice (histogram, then scatter) instead of written and read back:
-    // the field / parity noise and BGR reads cost less than 8 B of key traffic per pixel
-    TIMED(ctx, s, "k_uq_hist", (double)n * P * (noise ? 6 : 4),
-          launch_uq_hist(img, noise, W.d_nfield.p, n, h, w, seed, index, hist, s));
+    // keys -> per-step segments sorted by partition + run table + partition totals
     TIMED(ctx, s, "k_uq_scatter", (double)n * P * (noise ? 10 : 8),
-          launch_uq_scatter(img, noise, W.d_nfield.p, n, h, w, seed, index, key_stride, hist, cursor, W.d_keys.p, s));
-    // the partitions' sorted unique keys overwrite the (dead) raw keys
+          launch_uq_scatter(img, noise, W.d_nfield.p, n, h, w, seed, index, key_stride, hist, W.d_segtab.p,
+                            W.d_keys.p, s));
+    // the partitions' sorted unique keys go to the (free) d_raw
     TIMED(ctx, s, "k_uq_part", (double)n * P * 4,
-          launch_uq_part(W.d_keys.p, n, key_stride, hist, cursor, W.d_raw.p, W.d_segcubes.p, uq, cc, s));
+          launch_uq_part(W.d_keys.p, n, key_stride, P, hist, W.d_segtab.p, W.d_raw.p, W.d_segcubes.p, uq, cc, s));
     TIMED(ctx, s, "k_uq_gather", 0,
           launch_uq_gather(W.d_raw.p, n, key_stride, hist, uq, cc, W.d_segcubes.p, W.d_keys.p, W.d_cubes.p,
                            cube_stride, W.d_nuniq.p, W.d_ncubes.p, s));

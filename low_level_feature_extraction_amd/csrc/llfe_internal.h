@@ -195,13 +195,13 @@ struct KmeansCubes {
 // (noise_field_pixels(P) bytes at `field`, written by launch_uq_noise; unique.hip)
 int64_t noise_field_pixels(int64_t P);
 hipError_t launch_uq_noise(const int8_t *noise, int8_t *field, int64_t P, uint64_t seed, hipStream_t s);
-hipError_t launch_uq_hist(const uint8_t *bgr, const int8_t *noise, const int8_t *field, int n, int h, int w,
-                          uint64_t seed, ImgIndex index, uint32_t *hist, hipStream_t s);
+// steps of 4096 pixels per image (k_uq_scatter's segments; its run table is n x steps x 64 u32)
+int64_t uq_steps(int64_t P);
 hipError_t launch_uq_scatter(const uint8_t *bgr, const int8_t *noise, const int8_t *field, int n, int h, int w,
-                             uint64_t seed, ImgIndex index, int64_t key_stride, const uint32_t *hist, uint32_t *cursor,
-                             uint32_t *part, hipStream_t s);
-hipError_t launch_uq_part(const uint32_t *part, int n, int64_t key_stride, const uint32_t *hist,
-                          const uint32_t *written, uint32_t *skeys, CubeEnt *seg_cubes, uint32_t *uq, uint32_t *cc,
+                             uint64_t seed, ImgIndex index, int64_t key_stride, uint32_t *hist, uint32_t *tab,
+                             uint32_t *seg, hipStream_t s);
+hipError_t launch_uq_part(const uint32_t *seg, int n, int64_t key_stride, int64_t P, const uint32_t *hist,
+                          const uint32_t *tab, uint32_t *skeys, CubeEnt *seg_cubes, uint32_t *uq, uint32_t *cc,
                           hipStream_t s);
 hipError_t launch_uq_gather(const uint32_t *skeys, int n, int64_t key_stride, const uint32_t *hist, const uint32_t *uq,
                             const uint32_t *cc, const CubeEnt *seg_cubes, uint32_t *keys, CubeEnt *cubes,

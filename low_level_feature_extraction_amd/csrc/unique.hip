@@ -9,12 +9,12 @@
 // partition is deduplicated in a 32 KB LDS bitmap by one workgroup.
 //
 //   k_uq_noise    the launch's noise field (no caller noise): one image's worth, hashed
-//   k_uq_hist     pixel -> key r<<16|g<<8|b -> per-image histogram of R (keys not stored)
-//   k_uq_scatter  the same keys again, counting-sorted by R (block-local LDS sort, 64
-//                 global cursors per image, coalesced runs out)
-//   k_uq_part     one 1024-thread workgroup per (image, R): LDS bitmap of the partition's
-//                 4 x 256 x 256 colours -> its sorted unique keys (written in place of the
-//                 partition) and its 4x4x4 cubes (occupancy mask + exact sums, CubeEnt)
+//   k_uq_scatter  pixel -> key r<<16|g<<8|b, each 4096-pixel step counting-sorted by R
+//                 in LDS into its own segment + run table + per-image partition totals
+//   k_uq_part     one 1024-thread workgroup per (image, R): the partition's runs over the
+//                 steps -> LDS bitmap of its 4 x 256 x 256 colours -> its sorted unique keys
+//                 (at the partition's place in key order) and its 4x4x4 cubes (occupancy
+//                 mask + exact sums, CubeEnt)
 //   k_uq_gather   per image: prefix over the partitions, contiguous sorted keys + cube
 //                 table
 #include <algorithm>
@@ -175,54 +175,6 @@ __global__ __launch_bounds__(256) void k_uq_noise(int8_t *__restrict__ field, lo
     field[q] = (int8_t)((nr + 2) * 25 + (ng + 2) * 5 + (nb + 2));
 }
 
-// grid (blocks, n): per-image histogram of the keys' red quarter R = r >> 2 (the keys
-// themselves are recomputed by k_uq_scatter rather than written and read back)
-template <bool kField>
-__global__ __launch_bounds__(KB) void k_uq_hist(const uint8_t *__restrict__ bgr, NoiseSrc ns, long long P,
-                                                ImgIndex index, uint32_t *__restrict__ hist) {
-    __shared__ uint32_t lh[NPART];
-    __shared__ uint4 wst[KB / 64][192];
-    const int img = blockIdx.y;
-    const uint8_t *src = bgr + (size_t)img * P * 3;
-    const long long off = field_offset(ns, index.at(img));
-    if (threadIdx.x < NPART) lh[threadIdx.x] = 0;
-    __syncthreads();
-    const long long nchunks = (P + PPT - 1) / PPT;
-    for (long long c = (long long)blockIdx.x * KB + threadIdx.x; c < nchunks; c += (long long)gridDim.x * KB) {
-        const long long p0 = c * PPT;
-        const int cnt = (int)min((long long)PPT, P - p0);
-        uint32_t kv[PPT];
-        const bool span = wave_span(src + p0 * 3, p0, P);
-        chunk_keys<kField>(src + p0 * 3, noise_at<kField>(ns, img, P, off, p0), cnt, span, wst[threadIdx.x >> 6], kv);
-        // neighbouring pixels usually share their red quarter, so a lane whose 16 pixels
-        // all do adds them with one LDS atomic; the others count runs
-        const uint32_t bin0 = kv[0] >> 18;
-        bool same = cnt == PPT;
-#pragma unroll
-        for (int i = 1; i < PPT; i++) same = same & ((kv[i] >> 18) == bin0);
-        if (same) {
-            atomicAdd(&lh[bin0], (uint32_t)PPT);
-        } else {
-            uint32_t run_bin = 0xFFFFFFFFu, run_len = 0;
-#pragma unroll
-            for (int i = 0; i < PPT; i++) {
-                if (i < cnt) {
-                    const uint32_t bin = kv[i] >> 18;
-                    if (bin != run_bin) {
-                        if (run_len) atomicAdd(&lh[run_bin], run_len);
-                        run_bin = bin;
-                        run_len = 0;
-                    }
-                    run_len++;
-                }
-            }
-            if (run_len) atomicAdd(&lh[run_bin], run_len);
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x < NPART && lh[threadIdx.x]) atomicAdd(hist + (size_t)img * NPART + threadIdx.x, lh[threadIdx.x]);
-}
-
 // exclusive prefix of the image's 64 partition sizes (one wave)
 __device__ __forceinline__ uint32_t part_base(const uint32_t *h, int lane, uint32_t *total) {
     uint32_t v = lane < NPART ? h[lane] : 0u, x = v;
@@ -237,22 +189,20 @@ __device__ __forceinline__ uint32_t part_base(const uint32_t *h, int lane, uint3
 
 constexpr int SK = KB * PPT;  // keys per scatter block step
 
+// Step segments: each 4096-pixel step's keys, counting-sorted by partition in LDS, go to the
+// step's own 4096-key segment (coalesced, no global cursors), with the step's 64 (offset,
+// count) run entries in `tab` and the per-image partition totals in `hist`; k_uq_part reads
+// a partition as its runs over the steps.  (No separate histogram pass over the pixels.)
 template <bool kField>
 __global__ __launch_bounds__(KB) void k_uq_scatter(const uint8_t *__restrict__ bgr, NoiseSrc ns, long long P,
-                                                   long long key_stride, ImgIndex index,
-                                                   const uint32_t *__restrict__ hist, uint32_t *__restrict__ cursor,
-                                                   uint32_t *__restrict__ part) {
-    __shared__ uint32_t base[NPART], cnt[NPART], lbase[NPART], gbase[NPART];
+                                                   long long key_stride, ImgIndex index, uint32_t *__restrict__ hist,
+                                                   uint32_t *__restrict__ tab, uint32_t *__restrict__ seg) {
+    __shared__ uint32_t cnt[NPART], lbase[NPART];
     __shared__ __attribute__((aligned(16))) uint32_t stage[SK];
     const int img = blockIdx.y, t = threadIdx.x;
     const uint8_t *src = bgr + (size_t)img * P * 3;
     const long long off = field_offset(ns, index.at(img));
-    uint32_t *out = part + (size_t)img * key_stride;
-    if (t < 64) {
-        uint32_t tot;
-        const uint32_t b = part_base(hist + (size_t)img * NPART, t, &tot);
-        base[t] = b;
-    }
+    uint32_t *out = seg + (size_t)img * key_stride;
     const long long nsteps = (P + SK - 1) / SK;
     for (long long st = blockIdx.x; st < nsteps; st += gridDim.x) {
         const long long p0 = st * SK + (long long)t * PPT;
@@ -300,7 +250,8 @@ __global__ __launch_bounds__(KB) void k_uq_scatter(const uint8_t *__restrict__ b
                 if (t >= off) x += y;
             }
             lbase[t] = x - c;
-            gbase[t] = c ? base[t] + atomicAdd(cursor + (size_t)img * NPART + t, c) : 0u;
+            tab[((size_t)img * nsteps + st) * NPART + t] = (x - c) | (c << 16);
+            if (c) atomicAdd(hist + (size_t)img * NPART + t, c);
         }
         __syncthreads();
 #pragma unroll
@@ -308,11 +259,8 @@ __global__ __launch_bounds__(KB) void k_uq_scatter(const uint8_t *__restrict__ b
             if (i < n) stage[lbase[bins[i]] + pos[i]] = kv[i];
         __syncthreads();
         const int tot = (int)min((long long)SK, P - st * SK);
-        for (int i = t; i < tot; i += KB) {
-            const uint32_t k = stage[i];
-            const uint32_t bin = k >> 18;
-            out[gbase[bin] + (uint32_t)i - lbase[bin]] = k;
-        }
+        uint32_t *o = out + st * SK;
+        for (int i = t; i < tot; i += KB) o[i] = stage[i];
         __syncthreads();
     }
 }
@@ -347,11 +295,11 @@ __device__ __forceinline__ unsigned long long scan_u64_1024(unsigned long long v
     return r;
 }
 
-// grid (64, n).  Reads the partition's keys from `part` (`written` of them: the
-// partition's hist count), writes (in place of those keys, so capacity is the partition
-// size) the sorted unique keys to `skeys`, and up to 4096 cube entries to `seg_cubes`.
-__global__ __launch_bounds__(UT) void k_uq_part(const uint32_t *__restrict__ part, long long key_stride,
-                                                const uint32_t *__restrict__ hist, const uint32_t *__restrict__ written,
+// grid (64, n).  Reads the partition's keys as its runs in the step segments (`tab`), writes
+// the sorted unique keys to `skeys` at the partition's place in key order (capacity: its
+// hist count), and up to 4096 cube entries to `seg_cubes`.
+__global__ __launch_bounds__(UT) void k_uq_part(const uint32_t *__restrict__ seg, long long key_stride, long long P,
+                                                const uint32_t *__restrict__ hist, const uint32_t *__restrict__ tab,
                                                 uint32_t *__restrict__ skeys,
                                                 CubeEnt *__restrict__ seg_cubes,
                                                 uint32_t *__restrict__ uq, uint32_t *__restrict__ cc) {
@@ -364,7 +312,7 @@ __global__ __launch_bounds__(UT) void k_uq_part(const uint32_t *__restrict__ par
         const uint32_t b = part_base(hist + (size_t)img * NPART, t, &tot);
         if (t == R) {
             sbase = b;
-            scount = written[(size_t)img * NPART + R];
+            scount = hist[(size_t)img * NPART + R];
         }
     }
     __syncthreads();
@@ -378,27 +326,52 @@ __global__ __launch_bounds__(UT) void k_uq_part(const uint32_t *__restrict__ par
     }
     for (int i = t; i < 4 * 2048 / 4; i += UT) ((uint4 *)W)[i] = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();
-    const uint32_t *in = part + (size_t)img * key_stride + start;
-    // 16 independent (coalesced) key loads in flight per thread before their LDS atomics
-    // (8: +5 % kernel time, 4: +10 %): the workgroup otherwise waits on HBM latency
-#ifndef LLFE_UQ_LOADS
-#define LLFE_UQ_LOADS 16
-#endif
-    constexpr int KB8 = LLFE_UQ_LOADS;
-    for (uint32_t base = 0; base < count; base += UT * KB8) {
-        uint32_t kk[KB8];
+    // the partition's runs: wave w takes steps w + 16 j; lane j holds run j's (offset, count)
+    // (one table load per lane for up to 64 runs), then the runs' first keys (one per lane,
+    // photo runs average ~64 keys) are loaded RG runs at a time, and the rest of the long runs
+    // (flat "ui" partitions: ~4096 keys per run) with RG loads in flight
+    const uint32_t *sg = seg + (size_t)img * key_stride;
+    const long long nsteps = (P + SK - 1) / SK;
+    const uint32_t *tb = tab + (size_t)img * nsteps * NPART + R;
+    const int lane = t & 63, wid = t >> 6;
+    constexpr int RG = 8;  // runs (and tail loads) in flight per lane (16: 97 VGPRs, one workgroup per CU)
+    auto mark = [&](uint32_t k) {
+        // flat regions put one colour in every lane: test the bit with a (broadcast) read
+        // first, so a wave does not serialise 64 atomics on one LDS word
+        const uint32_t wi = ((k >> 16) & 3u) * 2048 + ((k >> 5) & 2047u), bit = 1u << (k & 31u);
+        if (k != 0xFFFFFFFFu && !(W[wi] & bit)) atomicOr(&W[wi], bit);
+    };
+    for (long long base = 0; base < nsteps; base += (UT / 64) * 64) {
+        const long long sl = base + wid + (UT / 64) * lane;  // this lane's run
+        const uint32_t e = sl < nsteps ? tb[(size_t)sl * NPART] : 0u;
+        const unsigned long long live = __ballot(e != 0u);
+        for (int j0 = 0; j0 < 64; j0 += RG) {
+            if (!((live >> j0) & ((1ull << RG) - 1))) continue;  // (uniform)
+            uint32_t kk[RG];
 #pragma unroll
-        for (int j = 0; j < KB8; j++) {
-            const uint32_t i = base + (uint32_t)j * UT + t;
-            kk[j] = i < count ? in[i] : 0xFFFFFFFFu;
-        }
+            for (int j = 0; j < RG; j++) {
+                const uint32_t ej = __builtin_amdgcn_readlane(e, j0 + j);
+                const size_t st = (size_t)(base + wid + (UT / 64) * (j0 + j));
+                kk[j] = (uint32_t)lane < (ej >> 16) ? sg[st * SK + (ej & 0xFFFFu) + lane] : 0xFFFFFFFFu;
+            }
 #pragma unroll
-        for (int j = 0; j < KB8; j++) {
-            const uint32_t k = kk[j];
-            // flat regions put one colour in every lane: test the bit with a (broadcast)
-            // read first, so a wave does not serialise 64 atomics on one LDS word
-            const uint32_t wi = ((k >> 16) & 3u) * 2048 + ((k >> 5) & 2047u), bit = 1u << (k & 31u);
-            if (k != 0xFFFFFFFFu && !(W[wi] & bit)) atomicOr(&W[wi], bit);
+            for (int j = 0; j < RG; j++) mark(kk[j]);
+#pragma unroll
+            for (int j = 0; j < RG; j++) {
+                const uint32_t ej = __builtin_amdgcn_readlane(e, j0 + j), c = ej >> 16;
+                if (c <= 64) continue;  // (uniform)
+                const uint32_t *rp = sg + (size_t)(base + wid + (UT / 64) * (j0 + j)) * SK + (ej & 0xFFFFu);
+                for (uint32_t i0 = 64; i0 < c; i0 += 64 * RG) {
+                    uint32_t q[RG];
+#pragma unroll
+                    for (int i = 0; i < RG; i++) {
+                        const uint32_t ix = i0 + 64 * i + lane;
+                        q[i] = ix < c ? rp[ix] : 0xFFFFFFFFu;
+                    }
+#pragma unroll
+                    for (int i = 0; i < RG; i++) mark(q[i]);
+                }
+            }
         }
     }
     __syncthreads();
@@ -550,41 +523,29 @@ hipError_t launch_uq_noise(const int8_t *noise, int8_t *field, int64_t P, uint64
     return hipGetLastError();
 }
 
-hipError_t launch_uq_hist(const uint8_t *bgr, const int8_t *noise, const int8_t *field, int n, int h, int w,
-                          uint64_t seed, ImgIndex index, uint32_t *hist, hipStream_t s) {
-    const long long P = (long long)h * w;
-    const long long per_block = (long long)KB * PPT * 4;
-    int bx = (int)std::min((P + per_block - 1) / per_block, 2048LL);
-    if (bx < 1) bx = 1;
-    const NoiseSrc ns = noise_src(noise, (int8_t *)field, P, seed);
-    if (ns.L)
-        hipLaunchKernelGGL(k_uq_hist<true>, dim3(bx, n), dim3(KB), 0, s, bgr, ns, P, index, hist);
-    else
-        hipLaunchKernelGGL(k_uq_hist<false>, dim3(bx, n), dim3(KB), 0, s, bgr, ns, P, index, hist);
-    return hipGetLastError();
-}
+int64_t uq_steps(int64_t P) { return (P + SK - 1) / SK; }
 
 hipError_t launch_uq_scatter(const uint8_t *bgr, const int8_t *noise, const int8_t *field, int n, int h, int w,
-                             uint64_t seed, ImgIndex index, int64_t key_stride, const uint32_t *hist, uint32_t *cursor,
-                             uint32_t *part, hipStream_t s) {
+                             uint64_t seed, ImgIndex index, int64_t key_stride, uint32_t *hist, uint32_t *tab,
+                             uint32_t *seg, hipStream_t s) {
     const int64_t P = (int64_t)h * w;
     int bx = (int)std::min((P + SK * 2 - 1) / (SK * 2), (int64_t)2048);
     if (bx < 1) bx = 1;
     const NoiseSrc ns = noise_src(noise, (int8_t *)field, P, seed);
     if (ns.L)
         hipLaunchKernelGGL(k_uq_scatter<true>, dim3(bx, n), dim3(KB), 0, s, bgr, ns, (long long)P, (long long)key_stride,
-                           index, hist, cursor, part);
+                           index, hist, tab, seg);
     else
         hipLaunchKernelGGL(k_uq_scatter<false>, dim3(bx, n), dim3(KB), 0, s, bgr, ns, (long long)P,
-                           (long long)key_stride, index, hist, cursor, part);
+                           (long long)key_stride, index, hist, tab, seg);
     return hipGetLastError();
 }
 
-hipError_t launch_uq_part(const uint32_t *part, int n, int64_t key_stride, const uint32_t *hist,
-                          const uint32_t *written, uint32_t *skeys, CubeEnt *seg_cubes, uint32_t *uq, uint32_t *cc,
+hipError_t launch_uq_part(const uint32_t *seg, int n, int64_t key_stride, int64_t P, const uint32_t *hist,
+                          const uint32_t *tab, uint32_t *skeys, CubeEnt *seg_cubes, uint32_t *uq, uint32_t *cc,
                           hipStream_t s) {
-    hipLaunchKernelGGL(k_uq_part, dim3(NPART, n), dim3(UT), 0, s, part, (long long)key_stride, hist, written, skeys,
-                       seg_cubes, uq, cc);
+    hipLaunchKernelGGL(k_uq_part, dim3(NPART, n), dim3(UT), 0, s, seg, (long long)key_stride, (long long)P, hist, tab,
+                       skeys, seg_cubes, uq, cc);
     return hipGetLastError();
 }
 

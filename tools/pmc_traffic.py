@@ -30,14 +30,13 @@ from collections import defaultdict
 # wide coalesced streaming readers: 16 B/lane (k-means, keys, scatter) and the
 # row-streaming stencil's three coalesced dwords per lane (r2c: raw fetch 0.55 x its 3P
 # input, doubled 1.09 x 3P = its 16/256-column + 10/270-row halo)
-FETCH_X2 = {"k_kmeans", "k_uq_hist", "k_uq_scatter", "k_stencil"}
+FETCH_X2 = {"k_kmeans", "k_uq_scatter", "k_stencil"}
 
 LOGICAL = [  # (substring of the device kernel name, logical launch)
     ("k_stencil", "k_stencil"),
     ("shadow_reduce", "k_stencil"),
     ("k_ccl_", "k_hysteresis_dilate"),
     ("k_bits_dilate", "k_hysteresis_dilate"),
-    ("k_uq_hist", "k_uq_hist"),
     ("k_uq_scatter", "k_uq_scatter"),
     ("k_uq_part", "k_uq_part"),
     ("k_uq_gather", "k_uq_gather"),
