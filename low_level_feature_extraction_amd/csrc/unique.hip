@@ -55,7 +55,8 @@ __host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     return z ^ (z >> 31);
 }
 
-constexpr int KB = 256;   // threads per block (keys / scatter)
+constexpr int KB = 256;  // threads per scatter block: a step is 4096 pixels (512 / 1024: the
+                         // scatter 1.67 -> 2.19 / 2.55 ms for part 2.41 -> 2.13 / 2.04)
 constexpr int PPT = 16;   // pixels per thread per block step
 constexpr int NPART = 64;
 
