@@ -437,3 +437,21 @@ def test_backend_before_torch_in_a_fresh_process():
                          cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert out.returncode == 0, out.stderr[-2000:]
     assert out.stdout.strip().splitlines()[-1] == "1"
+
+
+def test_kernel_stats_cover_stage_entry_points(backend):
+    """Profiling records of the fine-grained entry points (here llfe_color_unique, which
+    never waits on its stream) reach llfe_kernel_stats once their launches completed."""
+    import torch
+
+    x = _batch(3, 96, 128, seed=5)
+    backend.set_profiling(True)
+    try:
+        keys, nu = backend.color_unique(x, seed=1)
+        torch.cuda.synchronize()
+        st = backend.kernel_stats()
+        for name in ("k_uq_scatter", "k_uq_part", "k_uq_gather"):
+            assert st[name]["launches"] >= 1 and st[name]["total_ms"] > 0, (name, st)
+        assert "k_uq_hist" not in st  # (no histogram pass: the scatter writes step segments)
+    finally:
+        backend.set_profiling(False)
