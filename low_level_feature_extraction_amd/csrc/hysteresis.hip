@@ -6,7 +6,7 @@
 // union-find in a fixed number of launches instead of relaunching a flood fill until it
 // stops moving (weak-pixel networks in noisy images percolate across the whole frame):
 //
-//   k_ccl_local   per 64x32 tile: LDS union-find over candidate pixels (class != 1),
+//   k_ccl_local   per 64x64 tile: LDS union-find over candidate pixels (class != 1),
 //                 local root per pixel (u16), strong flag per root, root list per tile
 //   k_ccl_border  atomicMin union of the global ids of 8-neighbour candidates that sit
 //                 in different tiles (tile right column / bottom row)
@@ -23,7 +23,11 @@
 namespace llfe {
 namespace {
 
-constexpr int TW = kTileW, TH = kTileH, TP = TW * TH;  // 2048 pixels per tile
+// 64 x 64 tiles (the GPU contour pass keeps 64 x 32: contours_gpu.hip): the 85 % of tiles
+// without a Canny candidate cost one workgroup launch each in k_ccl_local, so half as many
+// tiles: hysteresis 1.61 -> 1.34 ms per 512 x 1080p
+constexpr int TW = kTileW, TH = 64, TP = TW * TH;  // 4096 pixels per tile
+inline int htiles_y(int h) { return (h + TH - 1) / TH; }
 constexpr int NT = 256;
 static_assert(TW == 64, "k_ccl_dilate packs one 64-pixel word per tile row");
 
@@ -82,19 +86,20 @@ __global__ __launch_bounds__(NT) void k_ccl_local(const uint8_t *__restrict__ cl
                                                   int *__restrict__ tcount) {
     __shared__ int L[TP];
     __shared__ uint32_t sflag[TP / 32];
-    __shared__ __attribute__((aligned(8))) uint8_t cb[TP];
+    __shared__ __attribute__((aligned(16))) uint8_t cb[TP];
     __shared__ int cnt;
     const int tid = threadIdx.x, img = blockIdx.y, t = blockIdx.x;
     const int ntiles = ntx * nty;
     const int tx0 = (t % ntx) * TW, ty0 = (t / ntx) * TH;
     const uint8_t *c = cls + (size_t)img * H * W;
     bool any = false;
-    if ((W & 7) == 0 && tx0 + TW <= W) {  // one 8-byte load per thread, through LDS
-        const int row = tid >> 3, col = (tid & 7) * 8, y = ty0 + row;
-        const uint64_t ones = 0x0101010101010101ull;
-        const uint64_t w = y < H ? *(const uint64_t *)(c + (size_t)y * W + tx0 + col) : ones;
-        any = w != ones;
-        *(uint64_t *)&cb[row * TW + col] = w;
+    static_assert(TP == 16 * NT, "one 16-byte load per thread");
+    if ((W & 15) == 0 && tx0 + TW <= W) {  // one 16-byte load per thread, through LDS
+        const int row = tid >> 2, col = (tid & 3) * 16, y = ty0 + row;
+        const uint4 ones = make_uint4(0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u);
+        const uint4 w = y < H ? *(const uint4 *)(c + (size_t)y * W + tx0 + col) : ones;
+        any = (w.x ^ ones.x) | (w.y ^ ones.y) | (w.z ^ ones.z) | (w.w ^ ones.w);
+        *(uint4 *)&cb[row * TW + col] = w;
     } else {
         for (int k = 0; k < TP / NT; k++) {
             const int i = tid + k * NT, y = ty0 + (i >> 6), x = tx0 + (i & 63);
@@ -347,7 +352,7 @@ __global__ __launch_bounds__(NT) void k_dilate3_u8(const uint8_t *__restrict__ s
 
 // the connected-component passes up to the packed edge words wk.ebits
 hipError_t launch_ccl(const uint8_t *cls, int n, int h, int w, const HystWork &wk, hipStream_t s) {
-    const int ntx = tiles_x(w), nty = tiles_y(h), ntiles = ntx * nty;
+    const int ntx = tiles_x(w), nty = htiles_y(h), ntiles = ntx * nty;
     dim3 grid(ntiles, n);
     const size_t words = (size_t)n * h * words_per_row(w);
     hipError_t e;
@@ -369,7 +374,9 @@ hipError_t launch_ccl(const uint8_t *cls, int n, int h, int w, const HystWork &w
 
 }  // namespace
 
-size_t hysteresis_ids(int n, int h, int w) { return (size_t)n * tiles_x(w) * tiles_y(h) * TP; }
+size_t hysteresis_ids(int n, int h, int w) { return (size_t)n * tiles_x(w) * htiles_y(h) * TP; }
+size_t hysteresis_tiles(int n, int h, int w) { return (size_t)n * tiles_x(w) * htiles_y(h); }
+size_t hysteresis_tile_words() { return TP / 32; }
 
 hipError_t launch_canny_edges(const uint8_t *cls, int n, int h, int w, const HystWork &wk, uint8_t *edges_u8,
                               hipStream_t s) {

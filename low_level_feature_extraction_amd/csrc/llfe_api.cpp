@@ -515,7 +515,7 @@ int hyst_work(llfe_ctx *ctx, Work &W, int n, int h, int w, HystWork *out) {
     HIPCHK(ctx, W.d_sroot.ensure(ids));
     HIPCHK(ctx, W.d_roots.ensure(ids));
     HIPCHK(ctx, W.d_nroots.ensure(tiles));
-    HIPCHK(ctx, W.d_tstrong.ensure(tiles * (kTileW * kTileH / 32)));
+    HIPCHK(ctx, W.d_tstrong.ensure(hysteresis_tiles(n, h, w) * hysteresis_tile_words()));
     HIPCHK(ctx, W.d_ebits.ensure((size_t)n * h * words_per_row(w)));
     HIPCHK(ctx, W.d_tlist.ensure(tiles + 1));
     *out = HystWork{W.d_lab.p,     W.d_parent.p, W.d_sroot.p,       W.d_roots.p,   W.d_nroots.p,

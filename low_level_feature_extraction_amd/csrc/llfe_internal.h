@@ -57,7 +57,9 @@ struct HystWork {
     int *tlist;         // tiles with a Canny candidate (n * tiles) and their count
     int *tcount;
 };
-size_t hysteresis_ids(int n, int h, int w);
+size_t hysteresis_ids(int n, int h, int w);    // >= the GPU contour pass's ids as well
+size_t hysteresis_tiles(int n, int h, int w);  // hysteresis tiles (<= n * tiles_x * tiles_y)
+size_t hysteresis_tile_words();                // tstrong words per hysteresis tile
 hipError_t launch_hysteresis_dilate(const uint8_t *cls, int n, int h, int w, const HystWork &wk, uint64_t *bits,
                                     uint8_t *mask_u8, hipStream_t s);
 // the same connected components without the dilation: Canny's 0 / 255 edges (llfe_canny)
