@@ -26,11 +26,7 @@ namespace {
 // 64 x 64 tiles (the GPU contour pass keeps 64 x 32: contours_gpu.hip): the 85 % of tiles
 // without a Canny candidate cost one workgroup launch each in k_ccl_local, so half as many
 // tiles: hysteresis 1.61 -> 1.34 ms per 512 x 1080p
-#ifndef LLFE_HYST_TH
-#define LLFE_HYST_TH 64
-#endif
-constexpr int TW = kTileW, TH = LLFE_HYST_TH, TP = TW * TH;  // 4096 pixels per tile
-constexpr int NBT = TH + TW;  // k_ccl_border threads: the tile's right column and bottom row
+constexpr int TW = kTileW, TH = 64, TP = TW * TH;  // 4096 pixels per tile
 inline int htiles_y(int h) { return (h + TH - 1) / TH; }
 constexpr int NT = 256;
 static_assert(TW == 64, "k_ccl_dilate packs one 64-pixel word per tile row");
@@ -97,21 +93,13 @@ __global__ __launch_bounds__(NT) void k_ccl_local(const uint8_t *__restrict__ cl
     const int tx0 = (t % ntx) * TW, ty0 = (t / ntx) * TH;
     const uint8_t *c = cls + (size_t)img * H * W;
     bool any = false;
-    static_assert(TP % (16 * NT) == 0, "16-byte loads");
-    if ((W & 15) == 0 && tx0 + TW <= W) {  // 16-byte loads, through LDS
+    static_assert(TP == 16 * NT, "one 16-byte load per thread");
+    if ((W & 15) == 0 && tx0 + TW <= W) {  // one 16-byte load per thread, through LDS
+        const int row = tid >> 2, col = (tid & 3) * 16, y = ty0 + row;
         const uint4 ones = make_uint4(0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u);
-        uint4 w[TP / (16 * NT)];
-#pragma unroll
-        for (int k = 0; k < TP / (16 * NT); k++) {
-            const int q = tid + k * NT, row = q >> 2, y = ty0 + row;
-            w[k] = y < H ? *(const uint4 *)(c + (size_t)y * W + tx0 + (q & 3) * 16) : ones;
-        }
-#pragma unroll
-        for (int k = 0; k < TP / (16 * NT); k++) {
-            const int q = tid + k * NT;
-            any |= ((w[k].x ^ ones.x) | (w[k].y ^ ones.y) | (w[k].z ^ ones.z) | (w[k].w ^ ones.w)) != 0u;
-            *(uint4 *)&cb[(q >> 2) * TW + (q & 3) * 16] = w[k];
-        }
+        const uint4 w = y < H ? *(const uint4 *)(c + (size_t)y * W + tx0 + col) : ones;
+        any = (w.x ^ ones.x) | (w.y ^ ones.y) | (w.z ^ ones.z) | (w.w ^ ones.w);
+        *(uint4 *)&cb[row * TW + col] = w;
     } else {
         for (int k = 0; k < TP / NT; k++) {
             const int i = tid + k * NT, y = ty0 + (i >> 6), x = tx0 + (i & 63);
@@ -188,7 +176,7 @@ __device__ __forceinline__ int gid_of(const uint16_t *lab, int img, int H, int W
 constexpr int kListBlocks = 4096;
 
 // threads 0..31 the tile's right column (look east), 32..95 its bottom row (look south)
-__global__ __launch_bounds__(NBT) void k_ccl_border(const uint8_t *__restrict__ cls, const uint16_t *__restrict__ lab,
+__global__ __launch_bounds__(128) void k_ccl_border(const uint8_t *__restrict__ cls, const uint16_t *__restrict__ lab,
                                                     int H, int W, int ntx, int nty, const int *__restrict__ tlist,
                                                     const int *__restrict__ tcount, int *__restrict__ parent) {
     const int tid = threadIdx.x, ntiles = ntx * nty, ntl = *tcount;
@@ -373,7 +361,7 @@ hipError_t launch_ccl(const uint8_t *cls, int n, int h, int w, const HystWork &w
     hipLaunchKernelGGL(k_ccl_local, grid, dim3(NT), 0, s, cls, h, w, ntx, nty, wk.lab, wk.parent, wk.sroot, wk.roots,
                        wk.nroots, wk.tlist, wk.tcount);
     const dim3 lgrid((unsigned)std::min<int64_t>((int64_t)ntiles * n, kListBlocks));
-    hipLaunchKernelGGL(k_ccl_border, lgrid, dim3(NBT), 0, s, cls, wk.lab, h, w, ntx, nty, wk.tlist, wk.tcount,
+    hipLaunchKernelGGL(k_ccl_border, lgrid, dim3(128), 0, s, cls, wk.lab, h, w, ntx, nty, wk.tlist, wk.tcount,
                        wk.parent);
     hipLaunchKernelGGL(k_ccl_flatten, lgrid, dim3(NT), 0, s, wk.tlist, wk.tcount, wk.roots, wk.nroots, wk.parent,
                        wk.sroot);
