@@ -339,24 +339,46 @@ def main():
     def barrier():
         shard.barrier(device=local)
 
+    from concurrent.futures import ThreadPoolExecutor
+
+    from low_level_feature_extraction_amd.pipeline import assemble
+
+    asm_pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="llfe-assemble")
+    asm_log = []  # (CPU ms of one batch's assembly)
+
+    def assemble_batch(recs):
+        """The reference-shaped results of one collected batch:
+        ColorFeatures by the palette rules (color_extractor.py:231-284), the analyze_shapes
+        dict (shape pyc @L184-189) and {"shadow_level": ...} (shadow pyc @L21-31), as
+        process_feature_results receives them (utils.py:155-214)."""
+        t = time.thread_time()
+        out = [assemble(r, feats) for r in recs]
+        asm_log.append((time.thread_time() - t) * 1e3)
+        return sum(len(o["shapes"]["shapes"]) for o in out) if "shapes" in feats else 0
+
     def run_steps(k_steps, seed0, pipelined, batch=None):
-        """k_steps full passes over the batch (``imgs`` unless given).  Pipelined: a serving loop that keeps two
-        batches in flight (llfe_submit_batch / llfe_collect_batch), so batch k + 1's
-        front kernels start in the tail of batch k's k-means; every batch is still
-        computed and collected inside the caller's timed region."""
-        shapes = 0
+        """k_steps full passes over the batch (``imgs`` unless given), each ending with every
+        image's reference-shaped result objects on the host (assembled on a worker thread
+        while the GPU runs the next batches; the caller's timed region waits for them).
+        Pipelined: a serving loop that keeps two batches in flight (llfe_submit_batch /
+        llfe_collect_batch), so batch k + 1's front kernels start in the tail of batch k's
+        k-means."""
         batch = imgs if batch is None else batch
+        futs = []
         if not pipelined:
             for k in range(k_steps):
-                shapes += sum(len(r.shapes) for r in be.process(batch, feats, seed=seed0 + k, index_base=base))
-            return shapes
-        pending = []
-        for k in range(k_steps):
-            pending.append(be.submit(batch, feats, seed=seed0 + k, index_base=base))
-            if len(pending) == be.inflight:
-                shapes += sum(len(r.shapes) for r in be.collect(pending.pop(0)))
-        while pending:
-            shapes += sum(len(r.shapes) for r in be.collect(pending.pop(0)))
+                futs.append(asm_pool.submit(assemble_batch, be.process(batch, feats, seed=seed0 + k, index_base=base)))
+        else:
+            pending = []
+            for k in range(k_steps):
+                pending.append(be.submit(batch, feats, seed=seed0 + k, index_base=base))
+                if len(pending) == be.inflight:
+                    futs.append(asm_pool.submit(assemble_batch, be.collect(pending.pop(0))))
+            while pending:
+                futs.append(asm_pool.submit(assemble_batch, be.collect(pending.pop(0))))
+        t_last = time.perf_counter()
+        shapes = sum(f.result() for f in futs)
+        run_steps.tail_ms = (time.perf_counter() - t_last) * 1e3  # assembly left after the last collect
         return shapes
 
     pipelined = args.pipeline == "on"
@@ -366,11 +388,13 @@ def main():
     # overlap, so an event-timed span would include the other batch's kernels)
     be.set_profiling(not pipelined)
     be.host_contour_stats(reset=True)
+    asm_log.clear()
     t0 = time.perf_counter()
     n_shapes = run_steps(args.steps, args.seed, pipelined)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     host_ct = be.host_contour_stats(reset=True)
+    asm_ms, asm_tail = list(asm_log), run_steps.tail_ms
     barrier()
     dt = shard.max_over_ranks(t1 - t0, device=coll_dev)
     stats = be.kernel_stats()
@@ -451,6 +475,10 @@ def main():
             # PMC SQ_INSTS_VALU per launch (profiles/traffic_latest.json) over the launch's
             # VALU issue capacity (VALU_SLOTS_PER_S): how close the kernel is to its compute bound
             r["valu_busy"] = round(valu_insts[name] / (VALU_SLOTS_PER_S * avg_ms * 1e-3), 3)
+            # the limiter the counters show: VALU issue when it is > 70 % busy (frac stays
+            # the HBM fraction of the algorithmic bytes, against HBM peak)
+            if r["valu_busy"] > 0.7:
+                r["bound"] = "valu"
         return r
 
     kernels = {}
@@ -545,6 +573,12 @@ def main():
         "dominant_kernel": dominant,
         "kernels": kernels,
         "shapes_per_image": round(n_shapes / (B * args.steps), 2),
+        # rows a6 / a10 inside the timed steps: every image's ColorFeatures / shapes dict /
+        # {"shadow_level"} built on a worker thread beside the serving loop
+        "result_assembly": {"host_cpu_ms_per_step": round(sum(asm_ms) / max(len(asm_ms), 1), 3),
+                            "us_per_image": round(sum(asm_ms) / max(len(asm_ms), 1) / B * 1e3, 2),
+                            "tail_ms_after_last_collect": round(asm_tail, 3),
+                            "in_timed_region": True},
         "per_class": per_class,
         # wall share of the timed steps the host contour pool spent tracing (host mode)
         "host_contour_busy": round(host_ct["busy_ms"] / 1e3 / max(t1 - t0, 1e-9), 3),

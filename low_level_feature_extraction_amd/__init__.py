@@ -12,7 +12,7 @@ Drop-in replacements for the reference's hot-path services:
 plus batched entry points (``run_batch``, ``*_batch``).  All per-pixel work runs in
 libllfe.so (HIP kernels for gfx950, C ABI in include/llfe.h); there is no CPU fallback.
 """
-from .color_extractor import ColorExtractor
+from .color_extractor import ColorExtractor, ColorPalette
 from .font_detector import FontDetector
 from .image_processor import ImageProcessor
 from .models import ColorFeatures, FeatureType, FontFeatures
@@ -30,6 +30,7 @@ def run_batch(images, features=("colors", "shapes", "shadows"), seed=None, noise
 __all__ = [
     "ColorExtractor",
     "ColorFeatures",
+    "ColorPalette",
     "FeatureType",
     "FontDetector",
     "FontFeatures",

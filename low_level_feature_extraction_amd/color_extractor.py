@@ -54,6 +54,16 @@ def _backend():
     return Backend.get()
 
 
+class ColorPalette(ColorFeatures):
+    """Legacy palette type of the reference module (color_extractor.py:16-35), kept so
+    ``from ...color_extractor import ColorPalette`` still resolves after the import swap:
+    a ColorFeatures with a schema example and nothing else."""
+
+    model_config = {"json_schema_extra": {"example": {
+        "primary": "#1a73e8", "background": "#f8f9fa", "accent": ["#0d47a1", "#64b5f6"],
+        "metadata": {"success": True, "timestamp": 0.0, "processing_time": 0.0}}}}
+
+
 class ColorExtractor:
     # ------------------------------------------------------------ helpers (:39-71)
     @staticmethod
@@ -169,12 +179,15 @@ class ColorExtractor:
     # ------------------------------------------------------------ palette (:231-284)
     @staticmethod
     def _palette(centers: np.ndarray, counts: np.ndarray) -> ColorFeatures:
-        centers = np.asarray(centers, np.uint8).reshape(-1, 3)
-        if len(centers) > 1:
-            order = np.argsort(-np.asarray(counts), kind="stable")
-            centers = centers[order]
-        hex_colors = [ColorExtractor.rgb_to_hex(tuple(int(v) for v in c)) for c in centers]
-        hex_colors = [c for c in hex_colors if c.lower() not in ["#ffffff", "#000000"]]
+        # (plain Python lists: the serving loop assembles 512 of these per step, and
+        # per-element NumPy scalars cost ~4x the whole rule set)
+        rows = np.asarray(centers, np.uint8).reshape(-1, 3).tolist()
+        if len(rows) > 1:
+            cnt = np.asarray(counts).reshape(-1).tolist()
+            # np.argsort(-counts) (:233-234); stable, equal counts keep k-means order
+            rows = [rows[k] for k in sorted(range(len(cnt)), key=lambda k: -cnt[k])]
+        hex_colors = ["#%02x%02x%02x" % (c[0], c[1], c[2]) for c in rows]  # rgb_to_hex (:39-41)
+        hex_colors = [c for c in hex_colors if c not in ("#ffffff", "#000000")]  # (already lower case)
         md = {"success": True, "timestamp": 0.0, "processing_time": 0.0}
         if not hex_colors:
             bg = "#000000" if ColorExtractor.is_light_color((255, 255, 255)) else "#FFFFFF"

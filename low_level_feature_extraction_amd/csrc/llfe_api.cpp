@@ -244,6 +244,7 @@ struct Profiler {
         double ms = 0, bytes = 0;
     };
     bool on = false;
+    static constexpr int kStageSlot = -3;  // records of the stage entry points (caller's stream)
     int cur_slot = 0;  // slot of the work being enqueued (records are collected per slot)
     std::vector<hipEvent_t> all, free_;
     std::vector<Rec> pending;
@@ -281,14 +282,15 @@ struct Profiler {
         (void)hipEventRecord(b, s);
         pending.push_back(Rec{kid(name), cur_slot, a, b, bytes});
     }
-    // call after the slot's (slot == -1: every) stream work has completed
+    // records of slot `slot` (-1: every slot, -2: every record) whose end event has
+    // completed; a record still pending keeps its events (a recycled event still in
+    // flight would time a later launch wrongly)
     void collect(int slot = -1) {
         size_t keep = 0;
         for (size_t i = 0; i < pending.size(); i++) {
             Rec &r = pending[i];
-            // slot < -1: only records whose end event has completed (the stage entry
-            // points, llfe_color_unique etc., run on the caller's stream and never wait)
-            if ((slot >= 0 && r.slot != slot) || (slot < -1 && hipEventQuery(r.b) != hipSuccess)) {
+            const bool mine = slot == -2 || (slot == -1 ? r.slot >= 0 : r.slot == slot);
+            if (!mine || hipEventQuery(r.b) != hipSuccess) {
                 pending[keep++] = r;
                 continue;
             }
@@ -476,6 +478,17 @@ struct llfe_ctx {
     } while (0)
 
 namespace {
+
+// The stage entry points run on workspace 0, slot 0's host buffers and the caller's
+// stream: refused while submitted batches (one of which may own workspace 0) are not
+// collected.  Their profiler records carry the stage tag, so llfe_collect_batch never
+// takes them for a slot's.
+int stage_enter(llfe_ctx *ctx, const char *fn) {
+    if (ctx->any_inflight())
+        return ctx->fail(LLFE_ERR_INVALID, "%s with submitted batches not yet collected", fn);
+    ctx->prof.cur_slot = Profiler::kStageSlot;
+    return LLFE_OK;
+}
 
 int stage_input(llfe_ctx *ctx, Work &W, const llfe_batch *b, int i0, int n, const uint8_t **d_img, const int8_t **d_noise,
                 hipStream_t s) {
@@ -1065,7 +1078,7 @@ int llfe_set_concurrency(llfe_ctx *ctx, int enable) {
 
 int llfe_kernel_stats(llfe_ctx *ctx, llfe_kernel_stat *out, int32_t cap) {
     if (!ctx) return LLFE_ERR_INVALID;
-    if (!ctx->any_inflight()) ctx->prof.collect(-2);  // completed launches of the stage entry points
+    ctx->prof.collect(-2);  // every completed launch (stage entry points never wait on a slot)
     int n = (int)ctx->prof.stats.size();
     for (int i = 0; i < n && i < cap && out; i++) {
         const auto &st = ctx->prof.stats[i];
@@ -1154,6 +1167,8 @@ int llfe_process_images(llfe_ctx *ctx, const llfe_image_desc *images, int32_t n,
         return ctx->fail(LLFE_ERR_INVALID, "preprocessing mode %d", preprocessing);
     if (n_colors < 0 || n_colors > kMaxColors)
         return ctx->fail(LLFE_ERR_UNSUPPORTED, "n_colors=%d outside [1, %d]", n_colors, kMaxColors);
+    if (ctx->any_inflight())
+        return ctx->fail(LLFE_ERR_INVALID, "llfe_process_images with submitted batches not yet collected");
     struct Item {
         int oh, ow, interp;
         bool resize;
@@ -1420,6 +1435,7 @@ int llfe_text_binary(llfe_ctx *ctx, const uint8_t *img, int32_t h, int32_t w, in
 int llfe_shape_mask(llfe_ctx *ctx, const uint8_t *bgr, uint8_t *mask, int32_t n, int32_t h, int32_t w,
                     llfe_stream stream) {
     if (!ctx || !valid_dims(n, h, w) || !bgr || !mask) return LLFE_ERR_INVALID;
+    if (int rc_ = stage_enter(ctx, __func__)) return rc_;
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t s = (hipStream_t)stream;
     Work &W = ctx->ws[0];  // stage entry points run on the caller's stream, slot 0
@@ -1428,7 +1444,7 @@ int llfe_shape_mask(llfe_ctx *ctx, const uint8_t *bgr, uint8_t *mask, int32_t n,
     int rc = run_hysteresis_dilate(ctx, W, n, h, w, nullptr, mask, s);
     if (rc) return rc;
     HIPCHK(ctx, hipStreamSynchronize(s));
-    ctx->prof.collect();
+    ctx->prof.collect(-2);
     return LLFE_OK;
 }
 
@@ -1437,6 +1453,7 @@ int llfe_shape_mask(llfe_ctx *ctx, const uint8_t *bgr, uint8_t *mask, int32_t n,
 int llfe_canny(llfe_ctx *ctx, const uint8_t *bgr, uint8_t *edges, int32_t n, int32_t h, int32_t w,
                llfe_stream stream) {
     if (!ctx || !valid_dims(n, h, w) || !bgr || !edges) return LLFE_ERR_INVALID;
+    if (int rc_ = stage_enter(ctx, __func__)) return rc_;
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t s = (hipStream_t)stream;
     Work &W = ctx->ws[0];
@@ -1463,6 +1480,7 @@ int llfe_dilate3(llfe_ctx *ctx, const uint8_t *src, uint8_t *dst, int32_t n, int
 int llfe_shadow_stats(llfe_ctx *ctx, const uint8_t *bgr, uint64_t *sums, uint64_t *counts, int32_t n, int32_t h,
                       int32_t w, llfe_stream stream) {
     if (!ctx || !valid_dims(n, h, w) || !bgr || !sums || !counts) return LLFE_ERR_INVALID;
+    if (int rc_ = stage_enter(ctx, __func__)) return rc_;
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t s = (hipStream_t)stream;
     Work &W = ctx->ws[0];
@@ -1478,6 +1496,7 @@ int llfe_shadow_stats(llfe_ctx *ctx, const uint8_t *bgr, uint64_t *sums, uint64_
 int llfe_color_unique(llfe_ctx *ctx, const llfe_batch *b, uint64_t seed, uint32_t *keys, int64_t *n_unique,
                       llfe_stream stream) {
     if (!ctx || !b || !keys || !n_unique || !valid_dims(b->n, b->height, b->width)) return LLFE_ERR_INVALID;
+    if (int rc_ = stage_enter(ctx, __func__)) return rc_;
     const int cmax = chunk_for(b->height, b->width);
     if (b->n > cmax) return ctx->fail(LLFE_ERR_UNSUPPORTED, "llfe_color_unique: n > %d", cmax);
     HIPCHK(ctx, hipSetDevice(ctx->device));
@@ -1506,6 +1525,7 @@ int llfe_kmeans(llfe_ctx *ctx, const uint32_t *keys, int64_t key_stride, const i
                 int32_t n_colors, uint64_t seed, int64_t index_base, llfe_image_result *results,
                 llfe_stream stream) {
     if (!ctx || !keys || !n_points || !results || n < 0) return LLFE_ERR_INVALID;
+    if (int rc_ = stage_enter(ctx, __func__)) return rc_;
     if (key_stride % 4 || ((uintptr_t)keys & 15))
         return ctx->fail(LLFE_ERR_INVALID, "keys must be 16-byte aligned with key_stride % 4 == 0");
     if (n > kMaxKmeansBatch) return ctx->fail(LLFE_ERR_UNSUPPORTED, "llfe_kmeans: n > %d", kMaxKmeansBatch);
@@ -1774,6 +1794,7 @@ int llfe_find_contours_gpu(llfe_ctx *ctx, const uint8_t *mask, int32_t h, int32_
                            int64_t points_capacity, int32_t *offsets, int32_t offsets_capacity,
                            int64_t *needed_points) {
     if (!ctx || !mask || h <= 0 || w <= 0 || !valid_dims(1, h, w)) return LLFE_ERR_INVALID;
+    if (int rc_ = stage_enter(ctx, __func__)) return rc_;
     int rc = gpu_contours_of_masks(ctx, mask, 1, h, w);
     if (rc) return rc;
     Work &W = ctx->ws[0];
@@ -1808,6 +1829,7 @@ int llfe_shapes_from_masks_gpu(llfe_ctx *ctx, const uint8_t *masks, int32_t n, i
                                llfe_shape *shapes, int64_t capacity, int32_t *n_shapes, int32_t *n_contours,
                                int64_t *needed) {
     if (!ctx || !masks || !valid_dims(n, h, w) || n <= 0) return LLFE_ERR_INVALID;
+    if (int rc_ = stage_enter(ctx, __func__)) return rc_;
     int rc = gpu_contours_of_masks(ctx, masks, n, h, w);
     if (rc) return rc;
     const int *info = ctx->h_ct_info_s[0].p;

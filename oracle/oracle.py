@@ -296,6 +296,15 @@ def numpy_noise(n_pixels, seed):
     return rs.normal(0, 0.5, (n_pixels, 3)).astype(np.int8)
 
 
+def device_noise(n_pixels, seed, index):
+    """The product's production noise for the image with global ``index`` under batch
+    ``seed`` (no caller noise; unique.hip), restated in llfe_oracle.c
+    ``orc_device_noise``: (n_pixels, 3) int8 in RGB order, the layout of numpy_noise."""
+    out = np.empty((max(int(n_pixels), 0), 3), np.int8)
+    lib().orc_device_noise(C.c_int64(int(n_pixels)), C.c_uint64(int(seed) & MASK64), C.c_int64(int(index)), _p(out))
+    return out
+
+
 def color_unique(bgr, noise=None):
     bgr = _chk_bgr(bgr)
     h, w = bgr.shape[:2]

@@ -47,6 +47,21 @@ def test_abi_version_and_struct_sizes():
     assert C.sizeof(L.LlfeImageDesc) == 40
 
 
+def test_integration_md_ctypes_binding_matches_header():
+    """The ctypes struct a maintainer copies from INTEGRATION.md §2 has the header's layout
+    (a short struct would hand libllfe an uninitialised `indices` pointer)."""
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    m = re.search(r"^class llfe_batch\(C\.Structure\):.*?\]\)?[^\n]*\n(?=\S|\n)", text, re.M | re.S)
+    assert m, "INTEGRATION.md has no llfe_batch ctypes snippet"
+    ns = {"C": C}
+    exec(m.group(0), ns)  # (our own documentation: the struct definition only)
+    doc = ns["llfe_batch"]
+    assert C.sizeof(doc) == C.sizeof(L.LlfeBatch) == 56
+    assert [f for f, _ in doc._fields_] == [f for f, _ in L.LlfeBatch._fields_]
+    for f, _ in L.LlfeBatch._fields_:
+        assert getattr(doc, f).offset == getattr(L.LlfeBatch, f).offset, f
+
+
 def test_struct_layout_matches_header_via_compiler(tmp_path):
     """Compile a tiny C program against include/llfe.h and compare offsetof/sizeof."""
     src = tmp_path / "lay.c"

@@ -150,6 +150,21 @@ def test_three_batches_in_flight(backend):
     assert backend.inflight == 2
 
 
+def test_stage_calls_refused_while_batches_in_flight(backend, orc):
+    """Stage entry points share workspace 0 with submitted batches: while a submitted batch
+    is uncollected they are refused (no corruption of the batch), afterwards they run."""
+    x = _batch(3, 120, 200, seed=61)
+    ref = backend.process(x, ("colors", "shapes", "shadows"), seed=4, index_base=50)
+    t = backend.submit(x, ("colors", "shapes", "shadows"), seed=4, index_base=50)
+    for call in (lambda: backend.color_unique(x, seed=1), lambda: backend.shape_mask(x),
+                 lambda: backend.shadow_stats(x), lambda: backend.canny(x),
+                 lambda: backend.process_images(list(x), ("shapes",))):
+        with pytest.raises(Exception, match="not yet collected"):
+            call()
+    _same(backend.collect(t), ref)
+    assert np.array_equal(backend.shape_mask(x[:1]).cpu().numpy()[0], orc.shape_mask(x[0]))
+
+
 def test_many_shapes_capacity_retry(backend, orc):
     x = np.zeros((1, 540, 960, 3), np.uint8)
     for y in range(6, 530, 24):  # a grid of separated 12 x 12 squares -> ~880 shapes
