@@ -150,7 +150,9 @@ int llfe_set_concurrency(llfe_ctx *ctx, int enable);
 int llfe_set_contour_mode(llfe_ctx *ctx, int mode);
 int llfe_get_contour_mode(llfe_ctx *ctx); /* the current mode (or < 0) */
 /* batches llfe_submit_batch keeps in flight, each on its own workspace and streams: 2 or
- * 3 (LLFE_INFLIGHT sets a new context's depth, default 2); only with none in flight */
+ * 3 (LLFE_INFLIGHT sets a new context's depth, default 2); only with none in flight.  One
+ * device pass's workspace is sized within LLFE_WORKSPACE_GB (default 24) per slot, so the
+ * device memory held grows with the depth. */
 int llfe_set_inflight(llfe_ctx *ctx, int32_t depth);
 int llfe_get_inflight(llfe_ctx *ctx); /* the current depth (or < 0) */
 /* copies up to cap entries, returns the number of kernels with statistics */
@@ -210,7 +212,11 @@ int llfe_submit_batch(llfe_ctx *ctx, const llfe_batch *batch, uint32_t features,
 int llfe_collect_batch(llfe_ctx *ctx, int64_t ticket, llfe_image_result *results, llfe_shape *shapes,
                        int64_t shape_capacity, int64_t *shapes_needed);
 
-/* ---- stage entry points (parity tests; device in/out unless noted) ------ */
+/* ---- stage entry points (parity tests; device in/out unless noted) ------
+ * The ones that use the context's workspace (llfe_shape_mask, llfe_canny,
+ * llfe_shadow_stats, llfe_color_unique, llfe_kmeans, llfe_find_contours_gpu,
+ * llfe_shapes_from_masks_gpu) and llfe_process_images return LLFE_ERR_INVALID while a
+ * batch submitted with llfe_submit_batch is not yet collected. */
 /* gray = cvtColor(BGR2GRAY); out = GaussianBlur(gray, (5,5), 0)
  * (shape pyc @L18-21, shadow pyc @L8-9) */
 int llfe_gray_blur5(llfe_ctx *ctx, const uint8_t *bgr, uint8_t *blurred, int32_t n, int32_t h, int32_t w,

@@ -27,6 +27,21 @@
 namespace llfe {
 namespace {
 
+#ifndef LLFE_KM_EXP
+#define LLFE_KM_EXP 0
+#endif
+#ifndef LLFE_KM_PUSHV
+#define LLFE_KM_PUSHV 0
+#endif
+#ifndef LLFE_KM_LBL2
+#define LLFE_KM_LBL2 0
+#endif
+#ifndef LLFE_KM_PPCELLS
+#define LLFE_KM_PPCELLS 1
+#endif
+#ifndef LLFE_KM_CELLS
+#define LLFE_KM_CELLS 1
+#endif
 #ifndef LLFE_KM_THREADS
 #define LLFE_KM_THREADS 512
 #endif
@@ -181,8 +196,10 @@ struct KmSmem {
     unsigned long long sel_pts;          // colours the selection scans read
     unsigned long long wchunk[3][KW];    // per trial: sum of D over each wave's chunk
     uint32_t stage[KW][kStage + 64];     // per-wave ring of boundary colours (+ a dummy row)
+    int cq[KW][256];                     // per-wave list of the cubes of a chunk's failing cells
     unsigned long long qtot;             // sum of |p|^2 over all colours (exact)
     int marg[kMaxK * kMaxK + 6 * kMaxK]; // k-means++ corner margins: centre pairs, trial vs centre (+/-)
+    int margc[kMaxK * kMaxK + 6 * kMaxK];  // the same for the 4 x 8 x 8 cells
 };
 
 __device__ __forceinline__ Cent load_centres(const float (*c)[3]) {
@@ -338,7 +355,7 @@ __device__ __forceinline__ int dmin_chosen(int x, int y, int z, const ICent &ch,
 }
 
 __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, int K, uint64_t &rng,
-                         const CubeEnt *__restrict__ ctab, int C, int cb,
+                         const CubeEnt *__restrict__ ctab, int C, const CellEnt *__restrict__ ltab, int L, int cb,
                          int cend, const uint32_t *__restrict__ part_uq, unsigned long long &bytes,
                          uint32_t &pp_pts, uint32_t &pp_sel, uint64_t &t_sel) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -591,17 +608,14 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
             // and the corner margins 6 sum max(+-(a - b), 0) depend on the centres only.
             // The pairwise corner margins live in LDS (per-lane reads indexed by the lane's
             // owner k); the per-centre constants stay in scalar registers.
-            int C2[kMaxK], S3[kMaxK], T2[3];
+            int C2[kMaxK], T2[3];
             u16x2 chrb[kMaxK], trb[3];  // (B, R) of the chosen centres and the trials
     #pragma unroll
             for (int m = 0; m < kMaxK; m++) chrb[m] = u16x2{(uint16_t)ch.z[m], (uint16_t)ch.x[m]};
     #pragma unroll
             for (int j = 0; j < 3; j++) trb[j] = u16x2{(uint16_t)tz[j], (uint16_t)tx[j]};
     #pragma unroll
-            for (int m = 0; m < kMaxK; m++) {
-                C2[m] = ch.x[m] * ch.x[m] + ch.y[m] * ch.y[m] + ch.z[m] * ch.z[m];
-                S3[m] = 3 * (ch.x[m] + ch.y[m] + ch.z[m]);
-            }
+            for (int m = 0; m < kMaxK; m++) C2[m] = ch.x[m] * ch.x[m] + ch.y[m] * ch.y[m] + ch.z[m] * ch.z[m];
     #pragma unroll
             for (int j = 0; j < 3; j++) T2[j] = tx[j] * tx[j] + ty[j] * ty[j] + tz[j] * tz[j];
             // undecided cubes' colours go through the wave's LDS ring (as in the Lloyd
@@ -652,6 +666,22 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
                 for (int d = 0; d < 3; d++) acc += max(sg * (t[d] - sm.icc[k2][d]), 0);
                 sm.marg[tid] = 6 * acc;
             }
+#if LLFE_KM_PPCELLS
+            // the same corner margins for a 4 x 8 x 8 cell: 2 (3, 7, 7) . max(+-(a - b), 0)
+            if (tid >= 64 && tid < 64 + kMaxK * kMaxK) {
+                const int q = tid - 64, m = q / kMaxK, k2 = q % kMaxK;
+                sm.margc[q] = 6 * max(sm.icc[m][0] - sm.icc[k2][0], 0) + 14 * max(sm.icc[m][1] - sm.icc[k2][1], 0) +
+                              14 * max(sm.icc[m][2] - sm.icc[k2][2], 0);
+            } else if (tid >= 64 + kMaxK * kMaxK && tid < 64 + kMaxK * kMaxK + 6 * kMaxK) {
+                const int q = tid - 64 - kMaxK * kMaxK, j = (q / kMaxK) % 3, k2 = q % kMaxK;
+                const int t[3] = {j == 0 ? tx[0] : (j == 1 ? tx[1] : tx[2]), j == 0 ? ty[0] : (j == 1 ? ty[1] : ty[2]),
+                                  j == 0 ? tz[0] : (j == 1 ? tz[1] : tz[2])};
+                const int sg = q < 3 * kMaxK ? 1 : -1;
+                sm.margc[kMaxK * kMaxK + q] = 6 * max(sg * (t[0] - sm.icc[k2][0]), 0) +
+                                              14 * max(sg * (t[1] - sm.icc[k2][1]), 0) +
+                                              14 * max(sg * (t[2] - sm.icc[k2][2]), 0);
+            }
+#endif
             __syncthreads();
             const int *Mkk = sm.marg, *NA = sm.marg + kMaxK * kMaxK, *NB = sm.marg + kMaxK * kMaxK + 3 * kMaxK;
             // waves take 64-cube chunks from a shared LDS counter, read two chunks ahead
@@ -667,6 +697,218 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
                 if (lane == 0) b = atomicAdd(&sm.next_chunk, kRun);
                 return b;
             };
+            // Closed forms of a box (a cube, or a cell of up to four cubes) with origin o,
+            // count n, colour-offset sums S_u and S_u2: v_j = sum over its colours of
+            // min(D, d(., t_j)) (kk == 0: d(., t_0)), `fail` when some chosen centre or trial
+            // is not decided on the whole box.  ext: the box's offsets to its centre
+            // doubled, (3, 3, 3) for a cube, (3, 7, 7) for a cell; MK / NAx / NBx: its corner
+            // margins.
+            auto box_vals = [&](int ox, int oy, int oz, int n, int sx, int sy, int sz, int s2, const int *MK,
+                                const int *NAx, const int *NBx, int ex, int ey, int ez, uint32_t &v0, uint32_t &v1,
+                                uint32_t &v2, bool &fail) __attribute__((always_inline)) {
+                fail = false;
+                if (KK == 0) {
+                    auto bsum = [&](int cx, int cy, int cz) {
+                        const int ax = ox - cx, ay = oy - cy, az = oz - cz;
+                        const uint32_t q = (uint32_t)(__mul24(ax, ax) + __mul24(ay, ay) + __mul24(az, az));
+                        return __umul24((uint32_t)n, q) + 2u * (uint32_t)(__mul24(ax, sx) + __mul24(ay, sy) + __mul24(az, sz)) +
+                               (uint32_t)s2;
+                    };
+                    v0 = bsum(tx[0], ty[0], tz[0]);
+                    qacc += bsum(0, 0, 0);
+                    v1 = v2 = 0;
+                    return;
+                }
+                // owner candidate: nearest chosen centre to the box centre q = o + ext / 2:
+                // argmin_m |q - c_m|^2 = argmin_m (D_m(o) - ext . c_m), first minimum.
+                // Dot products of (R, B) pairs by v_dot2_u32_u16 plus the G term by a
+                // 24-bit multiply (operands <= 255 and sums <= 1792, results < 2^32: exact)
+                const u16x2 orb = u16x2{(uint16_t)oz, (uint16_t)ox};
+                const u16x2 srb = u16x2{(uint16_t)sz, (uint16_t)sx};
+                auto odot = [&](u16x2 crb, int cg) {  // o . c
+                    return (int)__builtin_amdgcn_udot2(orb, crb, __umul24((uint32_t)oy, (uint32_t)cg), false);
+                };
+                auto sdot = [&](u16x2 crb, int cg) {  // S_u . c
+                    return (int)__builtin_amdgcn_udot2(srb, crb, __umul24((uint32_t)sy, (uint32_t)cg), false);
+                };
+                int Dc[kMaxK];
+    #pragma unroll
+                for (int m = 0; m < kMaxK; m++) {  // (only the KK chosen centres are read)
+                    Dc[m] = 0;
+                    if (m < KK) Dc[m] = C2[m] - 2 * odot(chrb[m], ch.y[m]);
+                }
+                auto sq = [&](int m) { return ex * ch.x[m] + ey * ch.y[m] + ez * ch.z[m]; };
+                int k = 0, bd = Dc[0] - sq(0);
+    #pragma unroll
+                for (int m = 1; m < kMaxK; m++) {
+                    if (m >= KK) break;
+                    const int d = Dc[m] - sq(m);
+                    if (d < bd) {
+                        bd = d;
+                        k = m;
+                    }
+                }
+                // owner k's values (per-lane selects from the uniform tables)
+                int Dk = Dc[0], ky = ch.y[0];
+                u16x2 krb = chrb[0];
+    #pragma unroll
+                for (int m = 1; m < kMaxK; m++) {
+                    if (m >= KK) break;
+                    Dk = k == m ? Dc[m] : Dk;
+                    ky = k == m ? ch.y[m] : ky;
+                    krb = k == m ? chrb[m] : krb;
+                }
+                // owned: no other chosen centre is ever strictly closer on the box
+                bool owned = true;
+    #pragma unroll
+                for (int m = 0; m < kMaxK; m++) {
+                    if (m >= KK) break;
+                    if (m != k) owned = owned & (Dc[m] - Dk - MK[m * kMaxK + k] >= 0);
+                }
+                // box sums: P + n D_c(o) - 2 c.S_u, P = n |o|^2 + 2 o.S_u + S_u2
+                const int Pc = __mul24(n, odot(orb, oy)) + 2 * sdot(orb, oy) + s2;
+                const uint32_t ds = (uint32_t)(Pc + __mul24(n, Dk) - 2 * sdot(krb, ky));
+                uint32_t vv[3];
+                bool dec = owned;
+    #pragma unroll
+                for (int j = 0; j < 3; j++) {
+                    const int Dt = T2[j] - 2 * odot(trb[j], ty[j]);
+                    const int f = Dt - Dk;
+                    const bool A = f - NAx[j * kMaxK + k] >= 0;  // t_j never strictly closer than c_k
+                    const bool B = f + NBx[j * kMaxK + k] <= 0;  // t_j always at least as close
+                    dec = dec & (A | B);
+                    vv[j] = A ? ds : (uint32_t)(Pc + __mul24(n, Dt) - 2 * sdot(trb[j], ty[j]));
+                }
+                v0 = vv[0];
+                v1 = vv[1];
+                v2 = vv[2];
+                fail = !dec;
+            };
+            auto cube_vals = [&](const CubeEnt &e, uint32_t &v0, uint32_t &v1, uint32_t &v2,
+                                 bool &fail) __attribute__((always_inline)) {
+                const CubeGeo g = cube_geo(e);
+                box_vals(g.ox, g.oy, g.oz, g.n, g.sx, g.sy, g.sz, g.s2, Mkk, NA, NB, 3, 3, 3, v0, v1, v2, fail);
+            };
+            // undecided cubes among the lanes of `fm`: their colours (enumerated from the
+            // occupancy mask) packed densely into the lanes, summed 64 at a time
+            auto push_cubes = [&](unsigned long long fm, const CubeEnt &e) __attribute__((always_inline)) {
+                const uint32_t okey = cube_origin_key(e.id);  // read back per cube below
+                const uint32_t mlo = (uint32_t)e.mask, mhi = (uint32_t)(e.mask >> 32);
+                while (fm) {
+    #pragma unroll
+                    for (int u = 0; u < LLFE_KM_UNROLL; u++) {
+                        if (u > 0 && !fm) break;
+                        const int src = __builtin_ctzll(fm);
+                        fm &= fm - 1;
+                        const unsigned long long m =
+                            ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(mhi, src) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane(mlo, src);
+                        const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                        stg[lane_sel(m, ((uint32_t)head + r) & (kStage - 1), kStage + lane)] =
+                            (uint32_t)__builtin_amdgcn_readlane(okey, src) | loff;
+                        head += __popcll(m);
+                    }
+                    while (head - tail >= 64) sum_stage(64);
+                }
+            };
+            auto next_part = [&](int Pseg) __attribute__((always_inline)) {
+                if (Pseg != Pcur) {
+                    if (Pcur >= 0) {
+                        flush_pk();
+                        const unsigned long long a0 = wave_sum(acc0), a1 = wave_sum(acc1), a2 = wave_sum(acc2);
+                        if (lane == 0) {
+                            atomicAdd(&sm.psum[0][Pcur], a0);
+                            atomicAdd(&sm.psum[1][Pcur], a1);
+                            atomicAdd(&sm.psum[2][Pcur], a2);
+                        }
+                    }
+                    acc0 = acc1 = acc2 = 0;
+                    Pcur = Pseg;
+                }
+            };
+#if LLFE_KM_PPCELLS
+            // cells first: a decided cell adds its closed forms; the cubes of the undecided
+            // cells of a chunk (per partition) are listed in the wave's LDS list and go through
+            // the cube path above, 64 at a time
+            const int *MKc = sm.margc, *NAc = sm.margc + kMaxK * kMaxK, *NBc = sm.margc + kMaxK * kMaxK + 3 * kMaxK;
+            int *ql = sm.cq[wid];
+            int run = __builtin_amdgcn_readfirstlane(grab());  // the current run's first cell
+            int base = run;
+            int ahead = grab();
+            CellEnt en{0u, 0u, 0u, 0u};
+            if (base + lane < L) en = ltab[base + lane];
+            while (base < L) {
+                const bool valid = base + lane < L;
+                const CellEnt e = en;
+                int nb = base + 64;
+                if (nb >= run + kRun || nb >= L) {  // (uniform) next run
+                    run = __builtin_amdgcn_readfirstlane(ahead);
+                    nb = run;
+                    if (nb < L) ahead = grab();
+                }
+                if (nb + lane < L) en = ltab[nb + lane];
+                const int P = valid ? (int)((e.id >> 10) & 63u) : kParts;
+                uint32_t v0 = 0, v1 = 0, v2 = 0;
+                bool fail = false;
+                if (valid)
+                    box_vals((int)((e.id >> 10) & 63u) * 4, (int)((e.id >> 5) & 31u) * 8, (int)(e.id & 31u) * 8,
+                             (int)((e.id >> 18) & 511u), (int)(e.sums & 1023u), (int)((e.sums >> 10) & 2047u),
+                             (int)(e.sums >> 21), (int)e.s2, MKc, NAc, NBc, 3, 7, 7, v0, v1, v2, fail);
+                // lanes hold ascending cell ids: visit the batch's partitions in order
+                int Pseg = __shfl(P, 0);
+                for (;;) {
+                    next_part(Pseg);
+                    const bool mine = P == Pseg;
+                    if (mine && !fail) {
+                        acc0 += v0;
+                        acc1 += v1;
+                        acc2 += v2;
+                    }
+                    const bool cf = mine && fail;
+                    const uint32_t nc1 = (e.id >> 16) & 3u;
+                    const unsigned long long F = __ballot(cf), B0 = __ballot(cf && (nc1 & 1u)),
+                                             B1 = __ballot(cf && (nc1 & 2u));
+                    if (F) {
+                        auto rank = [&](unsigned long long m) {
+                            return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                        };
+                        const uint32_t pre = rank(F) + rank(B0) + 2u * rank(B1);
+                        const int total = __popcll(F) + __popcll(B0) + 2 * __popcll(B1);
+                        if (cf) {
+    #pragma unroll
+                            for (uint32_t jj = 0; jj < 4; jj++)
+                                if (jj <= nc1) ql[pre + jj] = (int)(e.first + jj);
+                        }
+                        __builtin_amdgcn_wave_barrier();
+                        for (int b = 0; b < total; b += 64) {
+                            const bool cv = b + lane < total;
+                            CubeEnt ce;
+                            ce.mask = 0;
+                            ce.id = 0;
+                            ce.sums = 0;
+                            if (cv) ce = ctab[ql[b + lane]];
+                            uint32_t c0 = 0, c1 = 0, c2 = 0;
+                            bool cfail = false;
+                            if (cv) cube_vals(ce, c0, c1, c2, cfail);
+                            if (cv && !cfail) {
+                                acc0 += c0;
+                                acc1 += c1;
+                                acc2 += c2;
+                            }
+                            const unsigned long long fm = __ballot(cv && cfail);
+                            if (fm) push_cubes(fm, ce);
+                        }
+                        __builtin_amdgcn_wave_barrier();  // (the list is rewritten next)
+                    }
+                    const unsigned long long rest = __ballot(P > Pseg && P < kParts);
+                    if (!rest) break;
+                    Pseg = __shfl(P, (int)__builtin_ctzll(rest));
+                }
+                base = nb;
+            }
+#else
             int run = __builtin_amdgcn_readfirstlane(grab());  // the current run's first cube
             int base = run;
             int ahead = grab();
@@ -676,8 +918,7 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
             en.sums = 0;
             if (base + lane < C) en = ctab[base + lane];
             while (base < C) {
-                const int cidx = base + lane;
-                const bool valid = cidx < C;
+                const bool valid = base + lane < C;
                 const CubeEnt e = en;
                 int nb = base + 64;
                 if (nb >= run + kRun || nb >= C) {  // (uniform) next run
@@ -686,133 +927,29 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
                     if (nb < C) ahead = grab();
                 }
                 if (nb + lane < C) en = ctab[nb + lane];
-                const CubeGeo g = cube_geo(e);
                 const int P = valid ? (int)((e.id >> 12) & 63u) : kParts;
                 uint32_t v0 = 0, v1 = 0, v2 = 0;
                 bool fail = false;
-                if (valid) {
-                    if (KK == 0) {
-                        v0 = cube_sum(g, tx[0], ty[0], tz[0]);
-                        qacc += cube_sum(g, 0, 0, 0);
-                    } else {
-                        // owner candidate: nearest chosen centre to the cube centre q = o + 1.5:
-                        // argmin_m |q - c_m|^2 = argmin_m (D_m(o) - 3 sum(c_m)), first minimum.
-                        // Dot products of (R, B) pairs by v_dot2_u32_u16 plus the G term by a
-                        // 24-bit multiply (all operands <= 255, sums < 2^32: exact)
-                        const u16x2 orb = u16x2{(uint16_t)g.oz, (uint16_t)g.ox};
-                        const u16x2 srb = u16x2{(uint16_t)g.sz, (uint16_t)g.sx};
-                        auto odot = [&](u16x2 crb, int cg) {  // o . c
-                            return (int)__builtin_amdgcn_udot2(orb, crb, __umul24((uint32_t)g.oy, (uint32_t)cg), false);
-                        };
-                        auto sdot = [&](u16x2 crb, int cg) {  // S_u . c
-                            return (int)__builtin_amdgcn_udot2(srb, crb, __umul24((uint32_t)g.sy, (uint32_t)cg), false);
-                        };
-                        int Dc[kMaxK];
-    #pragma unroll
-                        for (int m = 0; m < kMaxK; m++) {  // (only the KK chosen centres are read)
-                            Dc[m] = 0;
-                            if (m < KK) Dc[m] = C2[m] - 2 * odot(chrb[m], ch.y[m]);
-                        }
-                        int k = 0, bd = Dc[0] - S3[0];
-    #pragma unroll
-                        for (int m = 1; m < kMaxK; m++) {
-                            if (m >= KK) break;
-                            const int d = Dc[m] - S3[m];
-                            if (d < bd) {
-                                bd = d;
-                                k = m;
-                            }
-                        }
-                        // owner k's values (per-lane selects from the uniform tables)
-                        int Dk = Dc[0], ky = ch.y[0];
-                        u16x2 krb = chrb[0];
-    #pragma unroll
-                        for (int m = 1; m < kMaxK; m++) {
-                            if (m >= KK) break;
-                            Dk = k == m ? Dc[m] : Dk;
-                            ky = k == m ? ch.y[m] : ky;
-                            krb = k == m ? chrb[m] : krb;
-                        }
-                        auto selk = [&](const int *row) { return row[k]; };  // LDS read, per-lane k
-                        // owned: no other chosen centre is ever strictly closer on the cube
-                        bool owned = true;
-    #pragma unroll
-                        for (int m = 0; m < kMaxK; m++) {
-                            if (m >= KK) break;
-                            if (m != k) owned = owned & (Dc[m] - Dk - selk(Mkk + m * kMaxK) >= 0);
-                        }
-                        // cube sums: P + n D_c(o) - 2 c.S_u, P = n |o|^2 + 2 o.S_u + S_u2
-                        const int Pc = __mul24(g.n, odot(orb, g.oy)) + 2 * sdot(orb, g.oy) + g.s2;
-                        const uint32_t ds = (uint32_t)(Pc + __mul24(g.n, Dk) - 2 * sdot(krb, ky));
-                        uint32_t vv[3];
-                        bool dec = owned;
-    #pragma unroll
-                        for (int j = 0; j < 3; j++) {
-                            const int Dt = T2[j] - 2 * odot(trb[j], ty[j]);
-                            const int f = Dt - Dk;
-                            const bool A = f - selk(NA + j * kMaxK) >= 0;  // t_j never strictly closer than c_k
-                            const bool B = f + selk(NB + j * kMaxK) <= 0;  // t_j always at least as close
-                            dec = dec & (A | B);
-                            vv[j] = A ? ds : (uint32_t)(Pc + __mul24(g.n, Dt) - 2 * sdot(trb[j], ty[j]));
-                        }
-                        v0 = vv[0];
-                        v1 = vv[1];
-                        v2 = vv[2];
-                        fail = !dec;
-                    }
-                }
+                if (valid) cube_vals(e, v0, v1, v2, fail);
                 // lanes hold ascending cube ids: visit the batch's partitions in order
                 int Pseg = __shfl(P, 0);
                 for (;;) {
-                    if (Pseg != Pcur) {
-                        if (Pcur >= 0) {
-                            flush_pk();
-                            const unsigned long long a0 = wave_sum(acc0), a1 = wave_sum(acc1), a2 = wave_sum(acc2);
-                            if (lane == 0) {
-                                atomicAdd(&sm.psum[0][Pcur], a0);
-                                atomicAdd(&sm.psum[1][Pcur], a1);
-                                atomicAdd(&sm.psum[2][Pcur], a2);
-                            }
-                        }
-                        acc0 = acc1 = acc2 = 0;
-                        Pcur = Pseg;
-                    }
+                    next_part(Pseg);
                     const bool mine = P == Pseg;
                     if (mine && !fail) {
                         acc0 += v0;
                         acc1 += v1;
                         acc2 += v2;
                     }
-                    // undecided cubes: their colours (enumerated from the occupancy mask)
-                    // packed densely into the lanes, summed 64 at a time
-                    unsigned long long fm = __ballot(mine && fail);
-                    if (fm) {
-                        const uint32_t okey = cube_origin_key(e.id);  // read back per cube below
-                        const uint32_t mlo = (uint32_t)e.mask, mhi = (uint32_t)(e.mask >> 32);
-                        while (fm) {
-    #pragma unroll
-                            for (int u = 0; u < LLFE_KM_UNROLL; u++) {
-                                if (u > 0 && !fm) break;
-                                const int src = __builtin_ctzll(fm);
-                                fm &= fm - 1;
-                                const unsigned long long m =
-                                    ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(mhi, src) << 32) |
-                                    (uint32_t)__builtin_amdgcn_readlane(mlo, src);
-                                const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                                stg[lane_sel(m, ((uint32_t)head + r) & (kStage - 1), kStage + lane)] =
-                                    (uint32_t)__builtin_amdgcn_readlane(okey, src) | loff;
-                                head += __popcll(m);
-                            }
-                            while (head - tail >= 64) sum_stage(64);
-                        }
-                    }
+                    const unsigned long long fm = __ballot(mine && fail);
+                    if (fm) push_cubes(fm, e);
                     const unsigned long long rest = __ballot(P > Pseg && P < kParts);
                     if (!rest) break;
                     Pseg = __shfl(P, (int)__builtin_ctzll(rest));
                 }
                 base = nb;
             }
+#endif
             if (Pcur >= 0) {
                 flush_pk();
                 const unsigned long long a0 = wave_sum(acc0), a1 = wave_sum(acc1), a2 = wave_sum(acc2);
@@ -876,7 +1013,7 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
 }
 
 #ifndef LLFE_KM_MINW
-#define LLFE_KM_MINW 1
+#define LLFE_KM_MINW 4
 #endif
 // kCubes: the cube-table path (the batch pipeline); !kCubes: plain sweeps over
 // caller-supplied keys (llfe_kmeans).  Separate instantiations keep the plain path's
@@ -947,7 +1084,7 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
 
     // ------------------------------------------------ k-means++ (generateCentersPP)
     if (use_cubes) {
-        pp_cubes(sm, pts, N, K, rng, ctab, C, cb, cend, cubes.part_uq + (size_t)img * kParts, bytes, pp_pts, pp_sel, t_sel);
+        pp_cubes(sm, pts, N, K, rng, ctab, C, cubes.cells + (size_t)img * cubes.cube_stride, cubes.n_cells[img], cb, cend, cubes.part_uq + (size_t)img * kParts, bytes, pp_pts, pp_sel, t_sel);
     } else {
     int cur = 0;
     {
@@ -1239,7 +1376,11 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
             int head = 0, tail = 0;  // wave-uniform ring counters
             auto label_stage = [&](int count) {
                 __builtin_amdgcn_wave_barrier();
+#if LLFE_KM_EXP == 1
+                if (false) {
+#else
                 if (lane < count) {
+#endif
                     const uint32_t kq = stg[(tail + lane) & (kStage - 1)];
                     const int l = label5p(kq, c);
                     atomicAdd(&sm.accA[l][tid], (unsigned long long)((kq >> 16) & 255u) |
@@ -1248,7 +1389,25 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
                 }
                 tail += count;
             };
-            // Waves take 64-cube chunks from a shared LDS counter, not fixed ranges: the
+#if LLFE_KM_LBL2
+            // two full batches at once: the two LDS reads and label chains interleave
+            auto label_stage2 = [&]() {
+                __builtin_amdgcn_wave_barrier();
+                const uint32_t k0 = stg[(tail + lane) & (kStage - 1)], k1 = stg[(tail + 64 + lane) & (kStage - 1)];
+                const int l0 = label5p(k0, c), l1 = label5p(k1, c);
+                atomicAdd(&sm.accA[l0][tid], (unsigned long long)((k0 >> 16) & 255u) |
+                                                 ((unsigned long long)((k0 >> 8) & 255u) << 32));
+                atomicAdd(&sm.accB[l0][tid], (unsigned long long)(k0 & 255u) | (1ull << 32));
+                atomicAdd(&sm.accA[l1][tid], (unsigned long long)((k1 >> 16) & 255u) |
+                                                 ((unsigned long long)((k1 >> 8) & 255u) << 32));
+                atomicAdd(&sm.accB[l1][tid], (unsigned long long)(k1 & 255u) | (1ull << 32));
+                tail += 128;
+            };
+#define LABEL_FULL() while (head - tail >= 128) label_stage2()
+#else
+#define LABEL_FULL() while (head - tail >= 64) label_stage(64)
+#endif
+            // Waves take 64-entry chunks from a shared LDS counter, not fixed ranges: the
             // boundary cubes cluster, and with fixed ranges the other waves idled at the
             // iteration barrier behind the wave that drew the boundary (measured: 94 ->
             // 74 us per photo iteration; round-robin chunks 79).  The counter is read two
@@ -1258,20 +1417,7 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
                 if (lane == 0) b = atomicAdd(&sm.next_chunk, 64);
                 return b;  // (lane 0's; read with readfirstlane one chunk later)
             };
-            int base = __builtin_amdgcn_readfirstlane(grab());
-            int ahead = grab();
-            CubeEnt en;
-            en.mask = 0;
-            en.id = 0;
-            en.sums = 0;
-            if (base + lane < C) en = ctab[base + lane];
-            while (base < C) {
-                const int ci = base + lane;
-                const bool valid = ci < C;
-                const CubeEnt e = en;
-                const int nb = __builtin_amdgcn_readfirstlane(ahead);
-                if (nb + lane < C) en = ctab[nb + lane];
-                if (nb < C) ahead = grab();
+            auto cube_body = [&](const CubeEnt &e, const bool valid) __attribute__((always_inline)) {
                 bool pass = false;
                 int k = 0;
                 if (valid) {
@@ -1315,7 +1461,11 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
                 // cubes straddling a boundary: their colours (enumerated from the
                 // occupancy mask, no key loads) packed densely into the lanes and
                 // labelled 64 at a time
+#if LLFE_KM_EXP == 2
+                unsigned long long fm = 0;
+#else
                 unsigned long long fm = __ballot(valid && !pass);
+#endif
                 // per lane: the origin key of its cube (read back per failing cube with one
                 // readlane instead of rebuilding it in scalar code)
                 const uint32_t okey = cube_origin_key(e.id);
@@ -1332,6 +1482,45 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
                     stg[lane_sel(m, ((uint32_t)head + r) & (kStage - 1), kStage + lane)] = k | loff;
                     head += __popcll(m);
                 };
+#if LLFE_KM_PUSHV
+                // four failing cubes per trip as straight-line code (a dummy push with an
+                // empty mask writes only the dummy row): the readlane / mbcnt chains of the
+                // four interleave instead of running one after the other
+                while (fm) {
+                    int src[4];
+                    bool hv[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        hv[u] = fm != 0;
+                        src[u] = hv[u] ? (int)__builtin_ctzll(fm) : 0;
+                        fm &= fm - 1;
+                    }
+                    unsigned long long m[4];
+                    uint32_t kk[4], hb[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const unsigned long long mu =
+                            ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(mhi, src[u]) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane(mlo, src[u]);
+                        m[u] = hv[u] ? mu : 0ull;
+                        kk[u] = __builtin_amdgcn_readlane(okey, src[u]);
+                    }
+                    int hp = head;
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        hb[u] = (uint32_t)hp;
+                        hp += __popcll(m[u]);
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m[u] >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m[u], 0u));
+                        stg[lane_sel(m[u], (hb[u] + r) & (kStage - 1), kStage + lane)] = kk[u] | loff;
+                    }
+                    head = hp;
+                    LABEL_FULL();
+                }
+#else
                 while (fm) {
 #pragma unroll
                     for (int u = 0; u < LLFE_KM_UNROLL; u++) {
@@ -1340,11 +1529,130 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
                         fm &= fm - 1;
                         push(src);
                     }
-                    while (head - tail >= 64) label_stage(64);
+                    LABEL_FULL();
+                }
+#endif
+            };
+#if LLFE_KM_CELLS
+            // Cells first (CellEnt: the up to four cubes of a 4 x 8 x 8 box, consecutive in the
+            // cube table): a cell whose box passes the margin test at its centre
+            // q = origin + (1.5, 3.5, 3.5), with the thresholds weighted by the half extents,
+            // thrC[k][j] = 2 (1.5 |dx| + 3.5 |dy| + 3.5 |dz|) + 1, is added from its sums (the
+            // same argument as for a cube: every colour of the box is at least 1 closer to
+            // c_k); the cubes of the failing cells of a chunk are listed in the wave's LDS
+            // list and go through the cube test 64 at a time.
+            float thrC[kMaxK][kMaxK];
+#pragma unroll
+            for (int k = 0; k < kMaxK; k++)
+#pragma unroll
+                for (int j = 0; j < kMaxK; j++)
+                    thrC[k][j] = (j == k || j >= K || k >= K)
+                                     ? -__builtin_inff()
+                                     : 3.f * fabsf(cu.x[j] - cu.x[k]) + 7.f * (fabsf(cu.y[j] - cu.y[k]) +
+                                                                             fabsf(cu.z[j] - cu.z[k])) + 1.f;
+            const int L = cubes.n_cells[img];
+            const CellEnt *ltab = cubes.cells + (size_t)img * cubes.cube_stride;
+            int *ql = sm.cq[wid];
+            int base = __builtin_amdgcn_readfirstlane(grab());
+            int ahead = grab();
+            CellEnt ln{0u, 0u, 0u, 0u};
+            if (base + lane < L) ln = ltab[base + lane];
+            while (base < L) {
+                const bool lvalid = base + lane < L;
+                const CellEnt e = ln;
+                const int nb = __builtin_amdgcn_readfirstlane(ahead);
+                if (nb + lane < L) ln = ltab[nb + lane];
+                if (nb < L) ahead = grab();
+                bool pass = false;
+                int k = 0;
+                if (lvalid) {
+                    const float qx = (float)((e.id >> 10) & 63u) * 4.f + 1.5f, qy = (float)((e.id >> 5) & 31u) * 8.f + 3.5f,
+                                qz = (float)(e.id & 31u) * 8.f + 3.5f;
+                    const f2 px = f2{qx, qx}, py = f2{qy, qy}, pz = f2{qz, qz};
+                    f2 d[3];
+#pragma unroll
+                    for (int j = 0; j < 3; j++) {
+                        f2 dd = __builtin_elementwise_fma(px, lw_x[j], lc2[j]);
+                        dd = __builtin_elementwise_fma(py, lw_y[j], dd);
+                        d[j] = __builtin_elementwise_fma(pz, lw_z[j], dd);
+                    }
+                    const float dv[5] = {d[0].x, d[0].y, d[1].x, d[1].y, d[2].x};
+                    const float m1 = fminf(fminf(fminf(dv[0], dv[1]), fminf(dv[2], dv[3])), dv[4]);
+                    const bool e0 = dv[0] == m1, e1 = dv[1] == m1, e2 = dv[2] == m1, e3 = dv[3] == m1;
+                    const bool is0 = e0, is1 = !e0 & e1, is2 = !e0 & !e1 & e2, is3 = !e0 & !e1 & !e2 & e3,
+                               is4 = !(e0 | e1 | e2 | e3);
+                    const bool o01 = fabsf(dv[0] - dv[1]) > thrC[0][1], o02 = fabsf(dv[0] - dv[2]) > thrC[0][2],
+                               o03 = fabsf(dv[0] - dv[3]) > thrC[0][3], o04 = fabsf(dv[0] - dv[4]) > thrC[0][4],
+                               o12 = fabsf(dv[1] - dv[2]) > thrC[1][2], o13 = fabsf(dv[1] - dv[3]) > thrC[1][3],
+                               o14 = fabsf(dv[1] - dv[4]) > thrC[1][4], o23 = fabsf(dv[2] - dv[3]) > thrC[2][3],
+                               o24 = fabsf(dv[2] - dv[4]) > thrC[2][4], o34 = fabsf(dv[3] - dv[4]) > thrC[3][4];
+                    pass = (is0 & o01 & o02 & o03 & o04) | (is1 & o01 & o12 & o13 & o14) |
+                           (is2 & o02 & o12 & o23 & o24) | (is3 & o03 & o13 & o23 & o34) |
+                           (is4 & o04 & o14 & o24 & o34);
+                    k = is0 ? 0 : (is1 ? 1 : (is2 ? 2 : (is3 ? 3 : 4)));
+                }
+                if (pass) {
+                    // colour sums = n origin + sum u (origin (4R, 8G2, 8B2))
+                    const uint32_t n = (e.id >> 18) & 511u;
+                    const uint32_t ox = ((e.id >> 10) & 63u) * 4u, oy = ((e.id >> 5) & 31u) * 8u, oz = (e.id & 31u) * 8u;
+                    atomicAdd(&sm.accA[k][tid], (unsigned long long)(n * ox + (e.sums & 1023u)) |
+                                                    ((unsigned long long)(n * oy + ((e.sums >> 10) & 2047u)) << 32));
+                    atomicAdd(&sm.accB[k][tid], (unsigned long long)(n * oz + (e.sums >> 21)) |
+                                                    ((unsigned long long)n << 32));
+                }
+                // the failing cells' cubes: cell c's nc = 1 + (bits 16..17) cubes go to list
+                // slots [pre_c, pre_c + nc), pre_c = sum of nc over the failing lanes below
+                // (three ballots: the count and its two low bits)
+                const bool cf = lvalid && !pass;
+                const uint32_t nc1 = (e.id >> 16) & 3u;
+                const unsigned long long F = __ballot(cf), B0 = __ballot(cf && (nc1 & 1u)),
+                                         B1 = __ballot(cf && (nc1 & 2u));
+                if (F) {
+                    auto rank = [&](unsigned long long m) {
+                        return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    };
+                    const uint32_t pre = rank(F) + rank(B0) + 2u * rank(B1);
+                    const int total = __popcll(F) + __popcll(B0) + 2 * __popcll(B1);
+                    if (cf) {
+#pragma unroll
+                        for (uint32_t jj = 0; jj < 4; jj++)
+                            if (jj <= nc1) ql[pre + jj] = (int)(e.first + jj);
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    for (int b = 0; b < total; b += 64) {
+                        const bool v = b + lane < total;
+                        CubeEnt ce;
+                        ce.mask = 0;
+                        ce.id = 0;
+                        ce.sums = 0;
+                        if (v) ce = ctab[ql[b + lane]];
+                        cube_body(ce, v);
+                    }
+                    __builtin_amdgcn_wave_barrier();  // (the next chunk rewrites the list)
                 }
                 base = nb;
             }
+#else
+            int base = __builtin_amdgcn_readfirstlane(grab());
+            int ahead = grab();
+            CubeEnt en;
+            en.mask = 0;
+            en.id = 0;
+            en.sums = 0;
+            if (base + lane < C) en = ctab[base + lane];
+            while (base < C) {
+                const bool valid = base + lane < C;
+                const CubeEnt e = en;
+                const int nb = __builtin_amdgcn_readfirstlane(ahead);
+                if (nb + lane < C) en = ctab[nb + lane];
+                if (nb < C) ahead = grab();
+                cube_body(e, valid);
+                base = nb;
+            }
+#endif
+            while (head - tail >= 64) label_stage(64);
             if (head > tail) label_stage(head - tail);
+#undef LABEL_FULL
             fails = (unsigned long long)head;
             if (lane == 0 && fails) atomicAdd(&sm.fail_pts, fails);
         } else {

@@ -215,7 +215,8 @@ struct Work {
     DevBuf<uint16_t> d_lab, d_roots;
     DevBuf<uint32_t> d_raw, d_keys, d_kscratch, d_pmeta, d_tstrong, d_segtab;  // d_segtab: k_uq_scatter's run table
     DevBuf<CubeEnt> d_segcubes, d_cubes;
-    DevBuf<int32_t> d_ncubes;
+    DevBuf<CellEnt> d_segcells, d_cells;
+    DevBuf<int32_t> d_ncubes, d_ncells;
     DevBuf<int64_t> d_nuniq;
     DevBuf<KmeansAttemptOut> d_att;
     DevBuf<KmeansImageOut> d_kout;
@@ -327,12 +328,14 @@ size_t shadow_tiles(int n, int h, int w) { return stencil_parts(n, h, w); }
 // Images per device pass.  One pass per call when the workspace allows it: a bigger
 // pass amortises the k-means launch's tail (its longest attempts run 100 Lloyd
 // iterations) over more work (512 x 1080p per pass: +10 % images/s over 256).  The
-// workspace is ~16 B per pixel + the 4 MB per-image partition cube table, held within
-// LLFE_WORKSPACE_GB (default 24 GB of the 288 GB of HBM).
+// workspace is ~16 B per pixel + the 5 MB per-image partition cube and cell tables, held
+// within LLFE_WORKSPACE_GB (default 24 GB of the 288 GB of HBM) PER IN-FLIGHT SLOT: every
+// slot of llfe_set_inflight owns one such workspace, so depth 3 takes about 3x the budget.
 int chunk_for(int h, int w) {
     double gb = 24.0;
     if (const char *e = getenv("LLFE_WORKSPACE_GB"); e && atof(e) > 0) gb = atof(e);
-    const double per_image = 16.0 * (double)h * (double)w + (double)kParts * kCubesPerPart * sizeof(CubeEnt);
+    const double per_image = 16.0 * (double)h * (double)w +
+                             (double)kParts * (kCubesPerPart * sizeof(CubeEnt) + kCellsPerPart * sizeof(CellEnt));
     const double n = gb * 1e9 / per_image;
     return (int)std::max(1.0, std::min(n, (double)kMaxKmeansBatch));
 }
@@ -610,27 +613,37 @@ int color_stage(llfe_ctx *ctx, Work &W, const uint8_t *img, const int8_t *noise,
     HIPCHK(ctx, W.d_keys.ensure((size_t)n * key_stride));
     HIPCHK(ctx, W.d_segcubes.ensure((size_t)n * kParts * kCubesPerPart));
     HIPCHK(ctx, W.d_cubes.ensure((size_t)n * cube_stride));
+    HIPCHK(ctx, W.d_segcells.ensure((size_t)n * kParts * kCellsPerPart));
+    HIPCHK(ctx, W.d_cells.ensure((size_t)n * cube_stride));
+    HIPCHK(ctx, W.d_ncells.ensure(n));
     HIPCHK(ctx, W.d_pmeta.ensure((size_t)n * kParts * 4));
     HIPCHK(ctx, W.d_nuniq.ensure(n));
     HIPCHK(ctx, W.d_ncubes.ensure(n));
-    // (d_pmeta: hist, a spare row, uq, cc; k-means reads uq)
-    uint32_t *hist = W.d_pmeta.p, *uq = hist + (size_t)2 * n * kParts, *cc = uq + (size_t)n * kParts;
+    // (d_pmeta: hist, cl, uq, cc; k-means reads uq)
+    uint32_t *hist = W.d_pmeta.p, *cl = hist + (size_t)n * kParts, *uq = hist + (size_t)2 * n * kParts,
+             *cc = uq + (size_t)n * kParts;
     HIPCHK(ctx, hipMemsetAsync(hist, 0, sizeof(uint32_t) * n * kParts, s));
     HIPCHK(ctx, W.d_segtab.ensure((size_t)n * uq_steps(P) * kParts));
     if (!noise) {
         HIPCHK(ctx, W.d_nfield.ensure((size_t)noise_field_pixels(P)));
         HIPCHK(ctx, launch_uq_noise(noise, W.d_nfield.p, P, seed, s));
     }
+    // Algorithmic bytes (colour pass 3P + 4 MiB + 8U per image): the scatter
+    // is charged the input read (3P, + 3P of parity noise when given), k_uq_part the 2^24-bit
+    // presence bitmap's clear + scan (4 MiB; held in LDS here) and the unique-key write (4U),
+    // k_uq_gather the key read (4U); the step segments written and read back between the
+    // scatter and k_uq_part (4P each way) are the implementation's, not counted.
     // keys -> per-step segments sorted by partition + run table + partition totals
-    TIMED(ctx, s, "k_uq_scatter", (double)n * P * (noise ? 10 : 8),
+    TIMED(ctx, s, "k_uq_scatter", (double)n * P * (noise ? 6 : 3),
           launch_uq_scatter(img, noise, W.d_nfield.p, n, h, w, seed, index, key_stride, hist, W.d_segtab.p,
                             W.d_keys.p, s));
     // the partitions' sorted unique keys go to the (free) d_raw
-    TIMED(ctx, s, "k_uq_part", (double)n * P * 4,
-          launch_uq_part(W.d_keys.p, n, key_stride, P, hist, W.d_segtab.p, W.d_raw.p, W.d_segcubes.p, uq, cc, s));
+    TIMED(ctx, s, "k_uq_part", (double)n * 4194304.0,
+          launch_uq_part(W.d_keys.p, n, key_stride, P, hist, W.d_segtab.p, W.d_raw.p, W.d_segcubes.p,
+                         W.d_segcells.p, uq, cc, cl, s));
     TIMED(ctx, s, "k_uq_gather", 0,
-          launch_uq_gather(W.d_raw.p, n, key_stride, hist, uq, cc, W.d_segcubes.p, W.d_keys.p, W.d_cubes.p,
-                           cube_stride, W.d_nuniq.p, W.d_ncubes.p, s));
+          launch_uq_gather(W.d_raw.p, n, key_stride, hist, uq, cc, cl, W.d_segcubes.p, W.d_segcells.p, W.d_keys.p,
+                           W.d_cubes.p, W.d_cells.p, cube_stride, W.d_nuniq.p, W.d_ncubes.p, W.d_ncells.p, s));
     return LLFE_OK;
 }
 
@@ -776,7 +789,7 @@ int enqueue_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_
     }
     if (want_col) {
         const KmeansCubes cubes{W.d_cubes.p, std::min<int64_t>(key_stride, kMaxCubes), W.d_ncubes.p,
-                                W.d_pmeta.p + (size_t)2 * n * kParts};
+                                W.d_pmeta.p + (size_t)2 * n * kParts, W.d_cells.p, W.d_ncells.p};
         rc = kmeans_stage(ctx, W, W.d_keys.p, key_stride, W.d_nuniq.p, n, b->n_colors ? b->n_colors : kMaxK, seed,
                           index, cubes, col_s);
         if (rc) return rc;
@@ -929,11 +942,11 @@ int finish_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, int i0, 
             double kb = 0, ub = 0;
             for (int i = 0; i < n; i++) {
                 kb += (double)ko[i].bytes;
-                ub += 8.0 * (double)ko[i].n_unique;
+                ub += 4.0 * (double)ko[i].n_unique;
             }
             ctx->prof.add_bytes("k_kmeans", kb);
-            // unique keys written twice by k_uq_part (sorted + cube order), read and
-            // written by k_uq_gather (cube entries not counted)
+            // the unique keys: written once (k_uq_part) and read once (k_uq_gather), 8U of
+            // SURVEY.md 8d's colour pass
             ctx->prof.add_bytes("k_uq_part", ub);
             ctx->prof.add_bytes("k_uq_gather", ub);
         }
@@ -1536,7 +1549,7 @@ int llfe_kmeans(llfe_ctx *ctx, const uint32_t *keys, int64_t key_stride, const i
     Work &W = ctx->ws[0];
     HIPCHK(ctx, W.d_nuniq.ensure(n));
     HIPCHK(ctx, hipMemcpyAsync(W.d_nuniq.p, n_points, sizeof(int64_t) * n, hipMemcpyHostToDevice, s));
-    const KmeansCubes none{nullptr, 0, nullptr, nullptr};  // plain sweeps over caller-supplied keys
+    const KmeansCubes none{nullptr, 0, nullptr, nullptr, nullptr, nullptr};  // plain sweeps over caller-supplied keys
     int rc = kmeans_stage(ctx, W, keys, key_stride, W.d_nuniq.p, n, n_colors, seed, ImgIndex{index_base, nullptr}, none, s);
     if (rc) return rc;
     HIPCHK(ctx, ctx->h_kout.ensure(n));

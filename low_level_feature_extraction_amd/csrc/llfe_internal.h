@@ -179,20 +179,37 @@ struct CubeEnt {
 };
 static_assert(sizeof(CubeEnt) == 16, "CubeEnt is one 16-byte load");
 constexpr int kMaxCubes = 1 << 18;
+// 4 x 8 x 8 cells: the (up to) four cubes (R, 2 G2 + j, 2 B2 + c), j, c in {0, 1}, of one
+// partition, consecutive in the cube table (cube order within a partition is (G2, B2, j, c)).
+// The Lloyd sweeps test a cell first (one margin test for up to four cubes); only the cubes
+// of a failing cell are tested one by one.
+constexpr int kCellsPerPart = 1024;  // 32 x 32 cells per partition
+struct CellEnt {
+    uint32_t id;     // R << 10 | G2 << 5 | B2 (cell = [4R, 4R+3] x [8G2, 8G2+7] x [8B2, 8B2+7]) in bits
+                     // 0..15, (cubes - 1) in bits 16..17, colour count (<= 256) in bits 18..26
+    uint32_t first;  // index of its first cube in the image's cube table
+    uint32_t sums;   // sum over its colours u = colour - cell origin: u_r (<= 768) | u_g << 10 | u_b << 21
+                     // (each <= 1792)
+    uint32_t s2;     // sum of |u|^2 (<= 27392)
+};
+static_assert(sizeof(CellEnt) == 16, "CellEnt is one 16-byte load");
 struct KmeansCubes {
-    const CubeEnt *cubes;   // per image (cube_stride) entries in cube-id order (nullptr: no pruning)
+    const CubeEnt *cubes;   // per image (cube_stride) entries, partition by partition (nullptr: no pruning)
     int64_t cube_stride;
     const int32_t *n_cubes;
     const uint32_t *part_uq;  // per image: unique colours per red-quarter partition (kParts)
+    const CellEnt *cells;     // per image (cube_stride) cells in partition / cell order
+    const int32_t *n_cells;
 };
 // Unique colours (unique.hip), all per image with stride key_stride (u32 keys):
 //   keys:    pixels -> noised keys into `raw`, partition histogram `hist` (n x 64, zeroed)
 //   scatter: raw -> `part` grouped by partition (`cursor` n x 64, zeroed)
 //   part:    per (image, partition): sorted unique keys -> `skeys` (may alias raw),
-//            cube entries -> `seg_cubes` (n x 64 x 4096),
-//            counts -> uq, cc (n x 64)
+//            cube entries -> `seg_cubes` (n x 64 x 4096), cells -> `seg_cells` (n x 64 x 1024),
+//            counts -> uq, cc, cl (n x 64)
 //   gather:  contiguous sorted keys -> `keys` (may alias part), cube table -> `cubes`,
-//            n_unique, n_cubes
+//            cell table -> `cells` (first cube indices made image-global), n_unique, n_cubes,
+//            n_cells
 // noise: the caller's parity noise (n x P x 3 int8) or null -> the launch's noise field
 // (noise_field_pixels(P) bytes at `field`, written by launch_uq_noise; unique.hip)
 int64_t noise_field_pixels(int64_t P);
@@ -203,11 +220,13 @@ hipError_t launch_uq_scatter(const uint8_t *bgr, const int8_t *noise, const int8
                              uint64_t seed, ImgIndex index, int64_t key_stride, uint32_t *hist, uint32_t *tab,
                              uint32_t *seg, hipStream_t s);
 hipError_t launch_uq_part(const uint32_t *seg, int n, int64_t key_stride, int64_t P, const uint32_t *hist,
-                          const uint32_t *tab, uint32_t *skeys, CubeEnt *seg_cubes, uint32_t *uq, uint32_t *cc,
-                          hipStream_t s);
+                          const uint32_t *tab, uint32_t *skeys, CubeEnt *seg_cubes, CellEnt *seg_cells, uint32_t *uq,
+                          uint32_t *cc, uint32_t *cl, hipStream_t s);
 hipError_t launch_uq_gather(const uint32_t *skeys, int n, int64_t key_stride, const uint32_t *hist, const uint32_t *uq,
-                            const uint32_t *cc, const CubeEnt *seg_cubes, uint32_t *keys, CubeEnt *cubes,
-                            int64_t cube_stride, int64_t *n_unique, int32_t *n_cubes, hipStream_t s);
+                            const uint32_t *cc, const uint32_t *cl, const CubeEnt *seg_cubes,
+                            const CellEnt *seg_cells, uint32_t *keys, CubeEnt *cubes, CellEnt *cells,
+                            int64_t cube_stride, int64_t *n_unique, int32_t *n_cubes, int32_t *n_cells,
+                            hipStream_t s);
 
 // per image: K = min(n_colors, U); attempts run as separate workgroups
 // (ordered largest U first), then a finalize kernel picks the best attempt.

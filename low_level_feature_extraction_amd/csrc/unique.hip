@@ -77,6 +77,10 @@ __device__ __forceinline__ uint32_t key_of(int b, int g, int r, int nb, int ng, 
 // quarter-rate multiplies) off the per-pixel path.  A field pixel is one byte, the three
 // channel values n in [-2, 2] in base 5: (nr + 2) * 25 + (ng + 2) * 5 + (nb + 2) -- one
 // coalesced 16-B load per 16 pixels (|n| = 3 has probability 1e-9 and is not drawn).
+// Across the images of one launch the noise is NOT independent: each reads a rotation of
+// the same field, and a small image has few distinct rotations (L / 16: 256 for 64 x 64),
+// so images of a large batch can share identical noise.  Every per-image statistic (and
+// the reference's own per-call draw) only needs the within-image i.i.d. property.
 struct NoiseSrc {
     const int8_t *p;
     long long L;                // 0: parity mode
@@ -304,8 +308,9 @@ __device__ __forceinline__ unsigned long long scan_u64_wg(unsigned long long v, 
 __global__ __launch_bounds__(UT) void k_uq_part(const uint32_t *__restrict__ seg, long long key_stride, long long P,
                                                 const uint32_t *__restrict__ hist, const uint32_t *__restrict__ tab,
                                                 uint32_t *__restrict__ skeys,
-                                                CubeEnt *__restrict__ seg_cubes,
-                                                uint32_t *__restrict__ uq, uint32_t *__restrict__ cc) {
+                                                CubeEnt *__restrict__ seg_cubes, CellEnt *__restrict__ seg_cells,
+                                                uint32_t *__restrict__ uq, uint32_t *__restrict__ cc,
+                                                uint32_t *__restrict__ cl) {
     __shared__ __attribute__((aligned(16))) uint32_t W[4 * 2048];  // rows r = 4R + i, word g << 3 | b >> 5
     __shared__ unsigned long long tmp[UT / 64];
     __shared__ uint32_t sbase, scount;
@@ -324,12 +329,13 @@ __global__ __launch_bounds__(UT) void k_uq_part(const uint32_t *__restrict__ seg
         if (t == 0) {
             uq[(size_t)img * NPART + R] = 0;
             cc[(size_t)img * NPART + R] = 0;
+            cl[(size_t)img * NPART + R] = 0;
         }
         return;
     }
     for (int i = t; i < 4 * 2048 / 4; i += UT) ((uint4 *)W)[i] = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();
-    // the partition's runs: wave w takes steps w + 16 j; lane j holds run j's (offset, count)
+    // the partition's runs: wave w takes steps w + (UT / 64) j; lane j holds run j's (offset, count)
     // (one table load per lane for up to 64 runs), then the runs' first keys (one per lane,
     // photo runs average ~64 keys) are loaded RG runs at a time, and the rest of the long runs
     // (flat "ui" partitions: ~4096 keys per run) with RG loads in flight
@@ -409,41 +415,47 @@ __global__ __launch_bounds__(UT) void k_uq_part(const uint32_t *__restrict__ seg
         }
         if (t == 0) uq[(size_t)img * NPART + R] = sbase_q;
     }
-    // (b) 4x4x4 cubes of the partition in cube-id order (see CubeEnt): in pass h thread t
-    // owns cubes (G = t / 16 + h UT / 16, B = 4 (t % 16) .. + 3); bit i*16 + j*4 + bb =
-    // (4R+i, 4G+j, 4B+bb)
-    uint32_t cbase = 0;
+    // (b) the partition's 4x4x4 cubes and 4x8x8 cells.  In pass h thread t owns cell
+    // (G2, B2) = (c >> 5, c & 31), c = h UT + t, and its four cubes (G, B) = (2 G2 + j,
+    // 2 B2 + cc), written in cell order and within a cell in (j, cc) order, so a cell's cubes
+    // are consecutive; bit i*16 + jj*4 + bb of a cube = colour (4R + i, 4G + jj, 4B + bb).
+    // The cell's colours are the bytes (B2 & 3) of the 32 words W[i][8 G2 + g][B2 >> 2].
+    uint32_t cbase = 0, lbase = 0;
     CubeEnt *ce = seg_cubes + ((size_t)img * NPART + R) * 4096;
+    CellEnt *le = seg_cells + ((size_t)img * NPART + R) * kCellsPerPart;
+#pragma unroll 1
+    for (int h = 0; h < kCellsPerPart / UT; h++) {
+        const int cell = h * UT + t, G2 = cell >> 5, B2 = cell & 31;
+        const int wsel = (G2 << 6) | (B2 >> 2), sh0 = (B2 & 3) * 8;
+        unsigned long long mask[4];  // cube (j, c) = mask[2 j + c]
 #pragma unroll
-    for (int h = 0; h < 1024 / UT; h++) {
-        const int G = (t >> 4) + h * (UT / 16), B0 = (t & 15) * 4;
-        const int wsel = (G << 5) | ((t & 15) >> 1);
-        const int sh0 = (t & 1) * 16;
-        uint32_t w[4][4];
+        for (int q = 0; q < 4; q++) mask[q] = 0;
 #pragma unroll
         for (int i = 0; i < 4; i++)
 #pragma unroll
-            for (int j = 0; j < 4; j++) w[i][j] = W[i * 2048 + wsel + (j << 3)];
-        unsigned long long mask[4], mine = 0;
+            for (int g = 0; g < 8; g++) {
+                const uint32_t byte = (W[i * 2048 + wsel + (g << 3)] >> sh0) & 255u;
+                const int j = g >> 2, jj = g & 3;
+                mask[2 * j] |= (unsigned long long)(byte & 15u) << (i * 16 + jj * 4);
+                mask[2 * j + 1] |= (unsigned long long)(byte >> 4) << (i * 16 + jj * 4);
+            }
+        unsigned long long mine = 0;
 #pragma unroll
-        for (int c = 0; c < 4; c++) {
-            unsigned long long m = 0;
-#pragma unroll
-            for (int i = 0; i < 4; i++)
-#pragma unroll
-                for (int j = 0; j < 4; j++)
-                    m |= (unsigned long long)((w[i][j] >> (sh0 + 4 * c)) & 15u) << (i * 16 + j * 4);
-            mask[c] = m;
-            mine += m ? 1ull : 0ull;
-        }
+        for (int q = 0; q < 4; q++) mine += mask[q] ? 1ull : 0ull;
+        if (mine) mine |= 1ull << 32;  // one cell
         unsigned long long tot;
-        uint32_t ci = cbase + (uint32_t)scan_u64_wg(mine, tmp, &tot);
+        const unsigned long long pos = scan_u64_wg(mine, tmp, &tot);
+        uint32_t ci = cbase + (uint32_t)pos;
+        const uint32_t li = lbase + (uint32_t)(pos >> 32), first = ci;
         cbase += (uint32_t)tot;
+        lbase += (uint32_t)(tot >> 32);
+        uint32_t ln = 0, lr = 0, lg = 0, lb = 0, l2 = 0;  // the cell's sums
 #pragma unroll
-        for (int c = 0; c < 4; c++) {
-            const unsigned long long m = mask[c];
+        for (int q = 0; q < 4; q++) {
+            const unsigned long long m = mask[q];
             if (!m) continue;
-            const int B = B0 + c;
+            const int j = q >> 1, c4 = (q & 1) * 4, j4 = j * 4;
+            const int G = 2 * G2 + j, B = 2 * B2 + (q & 1);
             const uint32_t n = (uint32_t)__popcll(m);
             uint32_t sr = 0, sg = 0, sb = 0, su2 = 0;  // over u = colour - cube origin
 #pragma unroll
@@ -453,10 +465,10 @@ __global__ __launch_bounds__(UT) void k_uq_part(const uint32_t *__restrict__ seg
                 su2 += i * i * c;
             }
 #pragma unroll
-            for (int j = 1; j < 4; j++) {
-                const uint32_t c = (uint32_t)__popcll(m & (0x000F000F000F000Full << (4 * j)));
-                sg += j * c;
-                su2 += j * j * c;
+            for (int jj = 1; jj < 4; jj++) {
+                const uint32_t c = (uint32_t)__popcll(m & (0x000F000F000F000Full << (4 * jj)));
+                sg += jj * c;
+                su2 += jj * jj * c;
             }
 #pragma unroll
             for (int bb = 1; bb < 4; bb++) {
@@ -469,47 +481,78 @@ __global__ __launch_bounds__(UT) void k_uq_part(const uint32_t *__restrict__ seg
             e.id = ((uint32_t)R << 12) | ((uint32_t)G << 6) | (uint32_t)B | (su2 << 18);
             e.sums = n | (sr << 7) | (sg << 15) | (sb << 23);
             ce[ci++] = e;
+            // relative to the cell origin the cube sits at (0, 4 j, 4 c)
+            ln += n;
+            lr += sr;
+            lg += sg + j4 * n;
+            lb += sb + c4 * n;
+            l2 += su2 + 2u * (j4 * sg + c4 * sb) + n * (uint32_t)(j4 * j4 + c4 * c4);
+        }
+        if (ln) {
+            CellEnt e;
+            e.id = ((uint32_t)R << 10) | ((uint32_t)G2 << 5) | (uint32_t)B2 | ((ci - first - 1u) << 16) | (ln << 18);
+            e.first = first;
+            e.sums = lr | (lg << 10) | (lb << 21);
+            e.s2 = l2;
+            le[li] = e;
         }
     }
-    if (t == 0) cc[(size_t)img * NPART + R] = cbase;
+    if (t == 0) {
+        cc[(size_t)img * NPART + R] = cbase;
+        cl[(size_t)img * NPART + R] = lbase;
+    }
 }
 
 // grid (64, n): one workgroup per (partition, image) copies the partition's sorted
-// unique keys and cube entries to their place in the contiguous per-image arrays
+// unique keys, cube entries and cells to their place in the contiguous per-image arrays
+// (a cell's first cube index becomes image-global)
 constexpr int GT = 256;
 __global__ __launch_bounds__(GT) void k_uq_gather(const uint32_t *__restrict__ skeys, long long key_stride,
                                                   const uint32_t *__restrict__ hist, const uint32_t *__restrict__ uq,
-                                                  const uint32_t *__restrict__ cc,
-                                                  const CubeEnt *__restrict__ seg_cubes, uint32_t *__restrict__ keys,
-                                                  CubeEnt *__restrict__ cubes, long long cube_stride,
-                                                  long long *__restrict__ n_unique, int *__restrict__ n_cubes) {
-    __shared__ uint32_t sp, su, sc, nu, nc;
+                                                  const uint32_t *__restrict__ cc, const uint32_t *__restrict__ cl,
+                                                  const CubeEnt *__restrict__ seg_cubes,
+                                                  const CellEnt *__restrict__ seg_cells, uint32_t *__restrict__ keys,
+                                                  CubeEnt *__restrict__ cubes, CellEnt *__restrict__ cells,
+                                                  long long cube_stride, long long *__restrict__ n_unique,
+                                                  int *__restrict__ n_cubes, int *__restrict__ n_cells) {
+    __shared__ uint32_t sp, su, sc, sl, nu, nc, nl;
     const int R = blockIdx.x, img = blockIdx.y, t = threadIdx.x;
     if (t < 64) {
-        uint32_t tot, ut, ct;
+        uint32_t tot, ut, ct, lt;
         const uint32_t ps = part_base(hist + (size_t)img * NPART, t, &tot);
         const uint32_t ub = part_base(uq + (size_t)img * NPART, t, &ut);
         const uint32_t cb = part_base(cc + (size_t)img * NPART, t, &ct);
+        const uint32_t lb = part_base(cl + (size_t)img * NPART, t, &lt);
         if (t == R) {
             sp = ps;
             su = ub;
             sc = cb;
+            sl = lb;
             nu = uq[(size_t)img * NPART + R];
             nc = cc[(size_t)img * NPART + R];
+            nl = cl[(size_t)img * NPART + R];
         }
         if (t == 0 && R == 0) {
             n_unique[img] = ut;
             n_cubes[img] = (int)ct;
+            n_cells[img] = (int)lt;
         }
     }
     __syncthreads();
-    const uint32_t U = nu, C = nc;
+    const uint32_t U = nu, C = nc, L = nl, cbase = sc;
     const uint32_t *sk = skeys + (size_t)img * key_stride + sp;
     uint32_t *ok = keys + (size_t)img * key_stride + su;
     for (uint32_t i = t; i < U; i += GT) ok[i] = sk[i];
     const CubeEnt *scp = seg_cubes + ((size_t)img * NPART + R) * 4096;
     CubeEnt *oc = cubes + (size_t)img * cube_stride + sc;
     for (uint32_t i = t; i < C; i += GT) oc[i] = scp[i];
+    const CellEnt *slp = seg_cells + ((size_t)img * NPART + R) * kCellsPerPart;
+    CellEnt *ol = cells + (size_t)img * cube_stride + sl;
+    for (uint32_t i = t; i < L; i += GT) {
+        CellEnt e = slp[i];
+        e.first += cbase;
+        ol[i] = e;
+    }
 }
 
 }  // namespace
@@ -549,18 +592,21 @@ hipError_t launch_uq_scatter(const uint8_t *bgr, const int8_t *noise, const int8
 }
 
 hipError_t launch_uq_part(const uint32_t *seg, int n, int64_t key_stride, int64_t P, const uint32_t *hist,
-                          const uint32_t *tab, uint32_t *skeys, CubeEnt *seg_cubes, uint32_t *uq, uint32_t *cc,
-                          hipStream_t s) {
+                          const uint32_t *tab, uint32_t *skeys, CubeEnt *seg_cubes, CellEnt *seg_cells, uint32_t *uq,
+                          uint32_t *cc, uint32_t *cl, hipStream_t s) {
     hipLaunchKernelGGL(k_uq_part, dim3(NPART, n), dim3(UT), 0, s, seg, (long long)key_stride, (long long)P, hist, tab,
-                       skeys, seg_cubes, uq, cc);
+                       skeys, seg_cubes, seg_cells, uq, cc, cl);
     return hipGetLastError();
 }
 
 hipError_t launch_uq_gather(const uint32_t *skeys, int n, int64_t key_stride, const uint32_t *hist, const uint32_t *uq,
-                            const uint32_t *cc, const CubeEnt *seg_cubes, uint32_t *keys, CubeEnt *cubes,
-                            int64_t cube_stride, int64_t *n_unique, int32_t *n_cubes, hipStream_t s) {
-    hipLaunchKernelGGL(k_uq_gather, dim3(NPART, n), dim3(GT), 0, s, skeys, (long long)key_stride, hist, uq, cc, seg_cubes,
-                       keys, cubes, (long long)cube_stride, (long long *)n_unique, (int *)n_cubes);
+                            const uint32_t *cc, const uint32_t *cl, const CubeEnt *seg_cubes,
+                            const CellEnt *seg_cells, uint32_t *keys, CubeEnt *cubes, CellEnt *cells,
+                            int64_t cube_stride, int64_t *n_unique, int32_t *n_cubes, int32_t *n_cells,
+                            hipStream_t s) {
+    hipLaunchKernelGGL(k_uq_gather, dim3(NPART, n), dim3(GT), 0, s, skeys, (long long)key_stride, hist, uq, cc, cl,
+                       seg_cubes, seg_cells, keys, cubes, cells, (long long)cube_stride, (long long *)n_unique,
+                       (int *)n_cubes, (int *)n_cells);
     return hipGetLastError();
 }
 

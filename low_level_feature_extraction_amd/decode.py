@@ -79,10 +79,34 @@ def _image_size(b):
 
 
 
-def _raise_pillow_limit(Image) -> None:
-    lim = Image.MAX_IMAGE_PIXELS
-    if lim is not None and lim < MAX_PIXELS:
-        Image.MAX_IMAGE_PIXELS = MAX_PIXELS  # our own MAX_PIXELS check below still applies
+_PIL_LIMIT_LOCK = None
+
+
+def _pillow_open(Image, image_bytes: bytes):
+    """Image.open under cv2.imdecode's size limit (MAX_PIXELS) instead of Pillow's
+    decompression-bomb guard (2 x MAX_IMAGE_PIXELS, ~179 MP by default), without changing
+    that process-global guard for other Pillow users: the warning between the two Pillow
+    limits is suppressed locally, and only an image Pillow refuses outright is opened again
+    with the limit raised for that one call (under a lock, restored afterwards)."""
+    import threading
+    import warnings
+
+    global _PIL_LIMIT_LOCK
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", Image.DecompressionBombWarning)
+        try:
+            return Image.open(io.BytesIO(image_bytes))
+        except Image.DecompressionBombError:
+            pass
+        if _PIL_LIMIT_LOCK is None:
+            _PIL_LIMIT_LOCK = threading.Lock()
+        with _PIL_LIMIT_LOCK:
+            old = Image.MAX_IMAGE_PIXELS
+            Image.MAX_IMAGE_PIXELS = MAX_PIXELS  # (the MAX_PIXELS check of the caller still applies)
+            try:
+                return Image.open(io.BytesIO(image_bytes))
+            finally:
+                Image.MAX_IMAGE_PIXELS = old
 
 
 def decode_bgr(image_bytes: bytes) -> np.ndarray:
@@ -98,9 +122,8 @@ def decode_bgr(image_bytes: bytes) -> np.ndarray:
             return out[0]
     # cv2.imdecode accepts up to CV_IO_MAX_IMAGE_PIXELS; Pillow's decompression-bomb
     # check would refuse images above 2 * MAX_IMAGE_PIXELS (~179 MP by default) at open
-    _raise_pillow_limit(Image)
     try:
-        im = Image.open(io.BytesIO(image_bytes))
+        im = _pillow_open(Image, image_bytes)
         if im.width * im.height > MAX_PIXELS:
             raise DecodeError(f"Failed to decode image: {im.width}x{im.height} exceeds {MAX_PIXELS} pixels")
         im.load()

@@ -122,7 +122,8 @@ def test_batcher_on_gpu_matches_run_batch():
 def test_decode_ignores_pillow_bomb_limit(monkeypatch):
     """Pillow-decoded formats follow cv2.imdecode's CV_IO_MAX_IMAGE_PIXELS (2^30), not
     Pillow's decompression-bomb limit: a GIF above a lowered
-    PIL.Image.MAX_IMAGE_PIXELS still decodes."""
+    PIL.Image.MAX_IMAGE_PIXELS still decodes -- and the process-global Pillow limit is left
+    as it was for other Pillow users."""
     import io
 
     from PIL import Image
@@ -135,4 +136,12 @@ def test_decode_ignores_pillow_bomb_limit(monkeypatch):
     monkeypatch.setattr(Image, "MAX_IMAGE_PIXELS", 1000)  # 2 * 1000 < 60 * 70: a bomb to Pillow
     out = decode.decode_bgr(buf.getvalue())
     assert out.shape == (60, 70, 3)
-    assert Image.MAX_IMAGE_PIXELS == decode.MAX_PIXELS
+    assert Image.MAX_IMAGE_PIXELS == 1000
+    # between Pillow's warning and error thresholds: decodes, and no warning escapes
+    import warnings
+
+    monkeypatch.setattr(Image, "MAX_IMAGE_PIXELS", 3000)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        assert decode.decode_bgr(buf.getvalue()).shape == (60, 70, 3)
+    assert Image.MAX_IMAGE_PIXELS == 3000
