@@ -27,21 +27,7 @@
 namespace llfe {
 namespace {
 
-#ifndef LLFE_KM_EXP
-#define LLFE_KM_EXP 0
-#endif
-#ifndef LLFE_KM_PUSHV
-#define LLFE_KM_PUSHV 0
-#endif
-#ifndef LLFE_KM_LBL2
-#define LLFE_KM_LBL2 0
-#endif
-#ifndef LLFE_KM_PPCELLS
-#define LLFE_KM_PPCELLS 1
-#endif
-#ifndef LLFE_KM_CELLS
-#define LLFE_KM_CELLS 1
-#endif
+constexpr int kCellMinCubes = 8192;  // the sweeps test cells before cubes from this cube count on
 #ifndef LLFE_KM_THREADS
 #define LLFE_KM_THREADS 512
 #endif
@@ -666,7 +652,6 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
                 for (int d = 0; d < 3; d++) acc += max(sg * (t[d] - sm.icc[k2][d]), 0);
                 sm.marg[tid] = 6 * acc;
             }
-#if LLFE_KM_PPCELLS
             // the same corner margins for a 4 x 8 x 8 cell: 2 (3, 7, 7) . max(+-(a - b), 0)
             if (tid >= 64 && tid < 64 + kMaxK * kMaxK) {
                 const int q = tid - 64, m = q / kMaxK, k2 = q % kMaxK;
@@ -681,7 +666,6 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
                                               14 * max(sg * (t[1] - sm.icc[k2][1]), 0) +
                                               14 * max(sg * (t[2] - sm.icc[k2][2]), 0);
             }
-#endif
             __syncthreads();
             const int *Mkk = sm.marg, *NA = sm.marg + kMaxK * kMaxK, *NB = sm.marg + kMaxK * kMaxK + 3 * kMaxK;
             // waves take 64-cube chunks from a shared LDS counter, read two chunks ahead
@@ -827,129 +811,132 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
                     Pcur = Pseg;
                 }
             };
-#if LLFE_KM_PPCELLS
-            // cells first: a decided cell adds its closed forms; the cubes of the undecided
-            // cells of a chunk (per partition) are listed in the wave's LDS list and go through
-            // the cube path above, 64 at a time
-            const int *MKc = sm.margc, *NAc = sm.margc + kMaxK * kMaxK, *NBc = sm.margc + kMaxK * kMaxK + 3 * kMaxK;
-            int *ql = sm.cq[wid];
-            int run = __builtin_amdgcn_readfirstlane(grab());  // the current run's first cell
-            int base = run;
-            int ahead = grab();
-            CellEnt en{0u, 0u, 0u, 0u};
-            if (base + lane < L) en = ltab[base + lane];
-            while (base < L) {
-                const bool valid = base + lane < L;
-                const CellEnt e = en;
-                int nb = base + 64;
-                if (nb >= run + kRun || nb >= L) {  // (uniform) next run
-                    run = __builtin_amdgcn_readfirstlane(ahead);
-                    nb = run;
-                    if (nb < L) ahead = grab();
-                }
-                if (nb + lane < L) en = ltab[nb + lane];
-                const int P = valid ? (int)((e.id >> 10) & 63u) : kParts;
-                uint32_t v0 = 0, v1 = 0, v2 = 0;
-                bool fail = false;
-                if (valid)
-                    box_vals((int)((e.id >> 10) & 63u) * 4, (int)((e.id >> 5) & 31u) * 8, (int)(e.id & 31u) * 8,
-                             (int)((e.id >> 18) & 511u), (int)(e.sums & 1023u), (int)((e.sums >> 10) & 2047u),
-                             (int)(e.sums >> 21), (int)e.s2, MKc, NAc, NBc, 3, 7, 7, v0, v1, v2, fail);
-                // lanes hold ascending cell ids: visit the batch's partitions in order
-                int Pseg = __shfl(P, 0);
-                for (;;) {
-                    next_part(Pseg);
-                    const bool mine = P == Pseg;
-                    if (mine && !fail) {
-                        acc0 += v0;
-                        acc1 += v1;
-                        acc2 += v2;
+            // Cells pay off on large cube tables (photo-like images: k-means++ 0.99 -> 0.86 ms
+            // per attempt, r4b); on small ones (ui: 3k cubes) the extra level cost more than it
+            // saved (0.18 -> 0.24 ms), so the choice is per image (uniform).
+            if (C >= kCellMinCubes) {
+                // cells first: a decided cell adds its closed forms; the cubes of the undecided
+                // cells of a chunk (per partition) are listed in the wave's LDS list and go through
+                // the cube path above, 64 at a time
+                const int *MKc = sm.margc, *NAc = sm.margc + kMaxK * kMaxK, *NBc = sm.margc + kMaxK * kMaxK + 3 * kMaxK;
+                int *ql = sm.cq[wid];
+                int run = __builtin_amdgcn_readfirstlane(grab());  // the current run's first cell
+                int base = run;
+                int ahead = grab();
+                CellEnt en{0u, 0u, 0u, 0u};
+                if (base + lane < L) en = ltab[base + lane];
+                while (base < L) {
+                    const bool valid = base + lane < L;
+                    const CellEnt e = en;
+                    int nb = base + 64;
+                    if (nb >= run + kRun || nb >= L) {  // (uniform) next run
+                        run = __builtin_amdgcn_readfirstlane(ahead);
+                        nb = run;
+                        if (nb < L) ahead = grab();
                     }
-                    const bool cf = mine && fail;
-                    const uint32_t nc1 = (e.id >> 16) & 3u;
-                    const unsigned long long F = __ballot(cf), B0 = __ballot(cf && (nc1 & 1u)),
-                                             B1 = __ballot(cf && (nc1 & 2u));
-                    if (F) {
-                        auto rank = [&](unsigned long long m) {
-                            return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                        };
-                        const uint32_t pre = rank(F) + rank(B0) + 2u * rank(B1);
-                        const int total = __popcll(F) + __popcll(B0) + 2 * __popcll(B1);
-                        if (cf) {
-    #pragma unroll
-                            for (uint32_t jj = 0; jj < 4; jj++)
-                                if (jj <= nc1) ql[pre + jj] = (int)(e.first + jj);
+                    if (nb + lane < L) en = ltab[nb + lane];
+                    const int P = valid ? (int)((e.id >> 10) & 63u) : kParts;
+                    uint32_t v0 = 0, v1 = 0, v2 = 0;
+                    bool fail = false;
+                    if (valid)
+                        box_vals((int)((e.id >> 10) & 63u) * 4, (int)((e.id >> 5) & 31u) * 8, (int)(e.id & 31u) * 8,
+                                 (int)((e.id >> 18) & 511u), (int)(e.sums & 1023u), (int)((e.sums >> 10) & 2047u),
+                                 (int)(e.sums >> 21), (int)e.s2, MKc, NAc, NBc, 3, 7, 7, v0, v1, v2, fail);
+                    // lanes hold ascending cell ids: visit the batch's partitions in order
+                    int Pseg = __shfl(P, 0);
+                    for (;;) {
+                        next_part(Pseg);
+                        const bool mine = P == Pseg;
+                        if (mine && !fail) {
+                            acc0 += v0;
+                            acc1 += v1;
+                            acc2 += v2;
                         }
-                        __builtin_amdgcn_wave_barrier();
-                        for (int b = 0; b < total; b += 64) {
-                            const bool cv = b + lane < total;
-                            CubeEnt ce;
-                            ce.mask = 0;
-                            ce.id = 0;
-                            ce.sums = 0;
-                            if (cv) ce = ctab[ql[b + lane]];
-                            uint32_t c0 = 0, c1 = 0, c2 = 0;
-                            bool cfail = false;
-                            if (cv) cube_vals(ce, c0, c1, c2, cfail);
-                            if (cv && !cfail) {
-                                acc0 += c0;
-                                acc1 += c1;
-                                acc2 += c2;
+                        const bool cf = mine && fail;
+                        const uint32_t nc1 = (e.id >> 16) & 3u;
+                        const unsigned long long F = __ballot(cf), B0 = __ballot(cf && (nc1 & 1u)),
+                                                 B1 = __ballot(cf && (nc1 & 2u));
+                        if (F) {
+                            auto rank = [&](unsigned long long m) {
+                                return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                            };
+                            const uint32_t pre = rank(F) + rank(B0) + 2u * rank(B1);
+                            const int total = __popcll(F) + __popcll(B0) + 2 * __popcll(B1);
+                            if (cf) {
+        #pragma unroll
+                                for (uint32_t jj = 0; jj < 4; jj++)
+                                    if (jj <= nc1) ql[pre + jj] = (int)(e.first + jj);
                             }
-                            const unsigned long long fm = __ballot(cv && cfail);
-                            if (fm) push_cubes(fm, ce);
+                            __builtin_amdgcn_wave_barrier();
+                            for (int b = 0; b < total; b += 64) {
+                                const bool cv = b + lane < total;
+                                CubeEnt ce;
+                                ce.mask = 0;
+                                ce.id = 0;
+                                ce.sums = 0;
+                                if (cv) ce = ctab[ql[b + lane]];
+                                uint32_t c0 = 0, c1 = 0, c2 = 0;
+                                bool cfail = false;
+                                if (cv) cube_vals(ce, c0, c1, c2, cfail);
+                                if (cv && !cfail) {
+                                    acc0 += c0;
+                                    acc1 += c1;
+                                    acc2 += c2;
+                                }
+                                const unsigned long long fm = __ballot(cv && cfail);
+                                if (fm) push_cubes(fm, ce);
+                            }
+                            __builtin_amdgcn_wave_barrier();  // (the list is rewritten next)
                         }
-                        __builtin_amdgcn_wave_barrier();  // (the list is rewritten next)
+                        const unsigned long long rest = __ballot(P > Pseg && P < kParts);
+                        if (!rest) break;
+                        Pseg = __shfl(P, (int)__builtin_ctzll(rest));
                     }
-                    const unsigned long long rest = __ballot(P > Pseg && P < kParts);
-                    if (!rest) break;
-                    Pseg = __shfl(P, (int)__builtin_ctzll(rest));
+                    base = nb;
                 }
-                base = nb;
-            }
-#else
-            int run = __builtin_amdgcn_readfirstlane(grab());  // the current run's first cube
-            int base = run;
-            int ahead = grab();
-            CubeEnt en;
-            en.mask = 0;
-            en.id = 0;
-            en.sums = 0;
-            if (base + lane < C) en = ctab[base + lane];
-            while (base < C) {
-                const bool valid = base + lane < C;
-                const CubeEnt e = en;
-                int nb = base + 64;
-                if (nb >= run + kRun || nb >= C) {  // (uniform) next run
-                    run = __builtin_amdgcn_readfirstlane(ahead);
-                    nb = run;
-                    if (nb < C) ahead = grab();
-                }
-                if (nb + lane < C) en = ctab[nb + lane];
-                const int P = valid ? (int)((e.id >> 12) & 63u) : kParts;
-                uint32_t v0 = 0, v1 = 0, v2 = 0;
-                bool fail = false;
-                if (valid) cube_vals(e, v0, v1, v2, fail);
-                // lanes hold ascending cube ids: visit the batch's partitions in order
-                int Pseg = __shfl(P, 0);
-                for (;;) {
-                    next_part(Pseg);
-                    const bool mine = P == Pseg;
-                    if (mine && !fail) {
-                        acc0 += v0;
-                        acc1 += v1;
-                        acc2 += v2;
+            } else {
+                int run = __builtin_amdgcn_readfirstlane(grab());  // the current run's first cube
+                int base = run;
+                int ahead = grab();
+                CubeEnt en;
+                en.mask = 0;
+                en.id = 0;
+                en.sums = 0;
+                if (base + lane < C) en = ctab[base + lane];
+                while (base < C) {
+                    const bool valid = base + lane < C;
+                    const CubeEnt e = en;
+                    int nb = base + 64;
+                    if (nb >= run + kRun || nb >= C) {  // (uniform) next run
+                        run = __builtin_amdgcn_readfirstlane(ahead);
+                        nb = run;
+                        if (nb < C) ahead = grab();
                     }
-                    const unsigned long long fm = __ballot(mine && fail);
-                    if (fm) push_cubes(fm, e);
-                    const unsigned long long rest = __ballot(P > Pseg && P < kParts);
-                    if (!rest) break;
-                    Pseg = __shfl(P, (int)__builtin_ctzll(rest));
-                }
-                base = nb;
+                    if (nb + lane < C) en = ctab[nb + lane];
+                    const int P = valid ? (int)((e.id >> 12) & 63u) : kParts;
+                    uint32_t v0 = 0, v1 = 0, v2 = 0;
+                    bool fail = false;
+                    if (valid) cube_vals(e, v0, v1, v2, fail);
+                    // lanes hold ascending cube ids: visit the batch's partitions in order
+                    int Pseg = __shfl(P, 0);
+                    for (;;) {
+                        next_part(Pseg);
+                        const bool mine = P == Pseg;
+                        if (mine && !fail) {
+                            acc0 += v0;
+                            acc1 += v1;
+                            acc2 += v2;
+                        }
+                        const unsigned long long fm = __ballot(mine && fail);
+                        if (fm) push_cubes(fm, e);
+                        const unsigned long long rest = __ballot(P > Pseg && P < kParts);
+                        if (!rest) break;
+                        Pseg = __shfl(P, (int)__builtin_ctzll(rest));
+                    }
+                    base = nb;
             }
-#endif
+            }
             if (Pcur >= 0) {
                 flush_pk();
                 const unsigned long long a0 = wave_sum(acc0), a1 = wave_sum(acc1), a2 = wave_sum(acc2);
@@ -1376,11 +1363,7 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
             int head = 0, tail = 0;  // wave-uniform ring counters
             auto label_stage = [&](int count) {
                 __builtin_amdgcn_wave_barrier();
-#if LLFE_KM_EXP == 1
-                if (false) {
-#else
                 if (lane < count) {
-#endif
                     const uint32_t kq = stg[(tail + lane) & (kStage - 1)];
                     const int l = label5p(kq, c);
                     atomicAdd(&sm.accA[l][tid], (unsigned long long)((kq >> 16) & 255u) |
@@ -1389,7 +1372,6 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
                 }
                 tail += count;
             };
-#if LLFE_KM_LBL2
             // two full batches at once: the two LDS reads and label chains interleave
             auto label_stage2 = [&]() {
                 __builtin_amdgcn_wave_barrier();
@@ -1404,9 +1386,6 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
                 tail += 128;
             };
 #define LABEL_FULL() while (head - tail >= 128) label_stage2()
-#else
-#define LABEL_FULL() while (head - tail >= 64) label_stage(64)
-#endif
             // Waves take 64-entry chunks from a shared LDS counter, not fixed ranges: the
             // boundary cubes cluster, and with fixed ranges the other waves idled at the
             // iteration barrier behind the wave that drew the boundary (measured: 94 ->
@@ -1461,11 +1440,7 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
                 // cubes straddling a boundary: their colours (enumerated from the
                 // occupancy mask, no key loads) packed densely into the lanes and
                 // labelled 64 at a time
-#if LLFE_KM_EXP == 2
-                unsigned long long fm = 0;
-#else
                 unsigned long long fm = __ballot(valid && !pass);
-#endif
                 // per lane: the origin key of its cube (read back per failing cube with one
                 // readlane instead of rebuilding it in scalar code)
                 const uint32_t okey = cube_origin_key(e.id);
@@ -1482,45 +1457,6 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
                     stg[lane_sel(m, ((uint32_t)head + r) & (kStage - 1), kStage + lane)] = k | loff;
                     head += __popcll(m);
                 };
-#if LLFE_KM_PUSHV
-                // four failing cubes per trip as straight-line code (a dummy push with an
-                // empty mask writes only the dummy row): the readlane / mbcnt chains of the
-                // four interleave instead of running one after the other
-                while (fm) {
-                    int src[4];
-                    bool hv[4];
-#pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        hv[u] = fm != 0;
-                        src[u] = hv[u] ? (int)__builtin_ctzll(fm) : 0;
-                        fm &= fm - 1;
-                    }
-                    unsigned long long m[4];
-                    uint32_t kk[4], hb[4];
-#pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        const unsigned long long mu =
-                            ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(mhi, src[u]) << 32) |
-                            (uint32_t)__builtin_amdgcn_readlane(mlo, src[u]);
-                        m[u] = hv[u] ? mu : 0ull;
-                        kk[u] = __builtin_amdgcn_readlane(okey, src[u]);
-                    }
-                    int hp = head;
-#pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        hb[u] = (uint32_t)hp;
-                        hp += __popcll(m[u]);
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m[u] >> 32),
-                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m[u], 0u));
-                        stg[lane_sel(m[u], (hb[u] + r) & (kStage - 1), kStage + lane)] = kk[u] | loff;
-                    }
-                    head = hp;
-                    LABEL_FULL();
-                }
-#else
                 while (fm) {
 #pragma unroll
                     for (int u = 0; u < LLFE_KM_UNROLL; u++) {
@@ -1531,9 +1467,7 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
                     }
                     LABEL_FULL();
                 }
-#endif
             };
-#if LLFE_KM_CELLS
             // Cells first (CellEnt: the up to four cubes of a 4 x 8 x 8 box, consecutive in the
             // cube table): a cell whose box passes the margin test at its centre
             // q = origin + (1.5, 3.5, 3.5), with the thresholds weighted by the half extents,
@@ -1550,106 +1484,109 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
                                      ? -__builtin_inff()
                                      : 3.f * fabsf(cu.x[j] - cu.x[k]) + 7.f * (fabsf(cu.y[j] - cu.y[k]) +
                                                                              fabsf(cu.z[j] - cu.z[k])) + 1.f;
-            const int L = cubes.n_cells[img];
-            const CellEnt *ltab = cubes.cells + (size_t)img * cubes.cube_stride;
-            int *ql = sm.cq[wid];
-            int base = __builtin_amdgcn_readfirstlane(grab());
-            int ahead = grab();
-            CellEnt ln{0u, 0u, 0u, 0u};
-            if (base + lane < L) ln = ltab[base + lane];
-            while (base < L) {
-                const bool lvalid = base + lane < L;
-                const CellEnt e = ln;
-                const int nb = __builtin_amdgcn_readfirstlane(ahead);
-                if (nb + lane < L) ln = ltab[nb + lane];
-                if (nb < L) ahead = grab();
-                bool pass = false;
-                int k = 0;
-                if (lvalid) {
-                    const float qx = (float)((e.id >> 10) & 63u) * 4.f + 1.5f, qy = (float)((e.id >> 5) & 31u) * 8.f + 3.5f,
-                                qz = (float)(e.id & 31u) * 8.f + 3.5f;
-                    const f2 px = f2{qx, qx}, py = f2{qy, qy}, pz = f2{qz, qz};
-                    f2 d[3];
+            // (per image, as in k-means++: cells pay off on large cube tables -- a photo's
+            // Lloyd iteration 74.5 -> 69.8 us, r4b -- not on a ui image's ~3k cubes)
+            if (C >= kCellMinCubes) {
+                const int L = cubes.n_cells[img];
+                const CellEnt *ltab = cubes.cells + (size_t)img * cubes.cube_stride;
+                int *ql = sm.cq[wid];
+                int base = __builtin_amdgcn_readfirstlane(grab());
+                int ahead = grab();
+                CellEnt ln{0u, 0u, 0u, 0u};
+                if (base + lane < L) ln = ltab[base + lane];
+                while (base < L) {
+                    const bool lvalid = base + lane < L;
+                    const CellEnt e = ln;
+                    const int nb = __builtin_amdgcn_readfirstlane(ahead);
+                    if (nb + lane < L) ln = ltab[nb + lane];
+                    if (nb < L) ahead = grab();
+                    bool pass = false;
+                    int k = 0;
+                    if (lvalid) {
+                        const float qx = (float)((e.id >> 10) & 63u) * 4.f + 1.5f, qy = (float)((e.id >> 5) & 31u) * 8.f + 3.5f,
+                                    qz = (float)(e.id & 31u) * 8.f + 3.5f;
+                        const f2 px = f2{qx, qx}, py = f2{qy, qy}, pz = f2{qz, qz};
+                        f2 d[3];
 #pragma unroll
-                    for (int j = 0; j < 3; j++) {
-                        f2 dd = __builtin_elementwise_fma(px, lw_x[j], lc2[j]);
-                        dd = __builtin_elementwise_fma(py, lw_y[j], dd);
-                        d[j] = __builtin_elementwise_fma(pz, lw_z[j], dd);
+                        for (int j = 0; j < 3; j++) {
+                            f2 dd = __builtin_elementwise_fma(px, lw_x[j], lc2[j]);
+                            dd = __builtin_elementwise_fma(py, lw_y[j], dd);
+                            d[j] = __builtin_elementwise_fma(pz, lw_z[j], dd);
+                        }
+                        const float dv[5] = {d[0].x, d[0].y, d[1].x, d[1].y, d[2].x};
+                        const float m1 = fminf(fminf(fminf(dv[0], dv[1]), fminf(dv[2], dv[3])), dv[4]);
+                        const bool e0 = dv[0] == m1, e1 = dv[1] == m1, e2 = dv[2] == m1, e3 = dv[3] == m1;
+                        const bool is0 = e0, is1 = !e0 & e1, is2 = !e0 & !e1 & e2, is3 = !e0 & !e1 & !e2 & e3,
+                                   is4 = !(e0 | e1 | e2 | e3);
+                        const bool o01 = fabsf(dv[0] - dv[1]) > thrC[0][1], o02 = fabsf(dv[0] - dv[2]) > thrC[0][2],
+                                   o03 = fabsf(dv[0] - dv[3]) > thrC[0][3], o04 = fabsf(dv[0] - dv[4]) > thrC[0][4],
+                                   o12 = fabsf(dv[1] - dv[2]) > thrC[1][2], o13 = fabsf(dv[1] - dv[3]) > thrC[1][3],
+                                   o14 = fabsf(dv[1] - dv[4]) > thrC[1][4], o23 = fabsf(dv[2] - dv[3]) > thrC[2][3],
+                                   o24 = fabsf(dv[2] - dv[4]) > thrC[2][4], o34 = fabsf(dv[3] - dv[4]) > thrC[3][4];
+                        pass = (is0 & o01 & o02 & o03 & o04) | (is1 & o01 & o12 & o13 & o14) |
+                               (is2 & o02 & o12 & o23 & o24) | (is3 & o03 & o13 & o23 & o34) |
+                               (is4 & o04 & o14 & o24 & o34);
+                        k = is0 ? 0 : (is1 ? 1 : (is2 ? 2 : (is3 ? 3 : 4)));
                     }
-                    const float dv[5] = {d[0].x, d[0].y, d[1].x, d[1].y, d[2].x};
-                    const float m1 = fminf(fminf(fminf(dv[0], dv[1]), fminf(dv[2], dv[3])), dv[4]);
-                    const bool e0 = dv[0] == m1, e1 = dv[1] == m1, e2 = dv[2] == m1, e3 = dv[3] == m1;
-                    const bool is0 = e0, is1 = !e0 & e1, is2 = !e0 & !e1 & e2, is3 = !e0 & !e1 & !e2 & e3,
-                               is4 = !(e0 | e1 | e2 | e3);
-                    const bool o01 = fabsf(dv[0] - dv[1]) > thrC[0][1], o02 = fabsf(dv[0] - dv[2]) > thrC[0][2],
-                               o03 = fabsf(dv[0] - dv[3]) > thrC[0][3], o04 = fabsf(dv[0] - dv[4]) > thrC[0][4],
-                               o12 = fabsf(dv[1] - dv[2]) > thrC[1][2], o13 = fabsf(dv[1] - dv[3]) > thrC[1][3],
-                               o14 = fabsf(dv[1] - dv[4]) > thrC[1][4], o23 = fabsf(dv[2] - dv[3]) > thrC[2][3],
-                               o24 = fabsf(dv[2] - dv[4]) > thrC[2][4], o34 = fabsf(dv[3] - dv[4]) > thrC[3][4];
-                    pass = (is0 & o01 & o02 & o03 & o04) | (is1 & o01 & o12 & o13 & o14) |
-                           (is2 & o02 & o12 & o23 & o24) | (is3 & o03 & o13 & o23 & o34) |
-                           (is4 & o04 & o14 & o24 & o34);
-                    k = is0 ? 0 : (is1 ? 1 : (is2 ? 2 : (is3 ? 3 : 4)));
-                }
-                if (pass) {
-                    // colour sums = n origin + sum u (origin (4R, 8G2, 8B2))
-                    const uint32_t n = (e.id >> 18) & 511u;
-                    const uint32_t ox = ((e.id >> 10) & 63u) * 4u, oy = ((e.id >> 5) & 31u) * 8u, oz = (e.id & 31u) * 8u;
-                    atomicAdd(&sm.accA[k][tid], (unsigned long long)(n * ox + (e.sums & 1023u)) |
-                                                    ((unsigned long long)(n * oy + ((e.sums >> 10) & 2047u)) << 32));
-                    atomicAdd(&sm.accB[k][tid], (unsigned long long)(n * oz + (e.sums >> 21)) |
-                                                    ((unsigned long long)n << 32));
-                }
-                // the failing cells' cubes: cell c's nc = 1 + (bits 16..17) cubes go to list
-                // slots [pre_c, pre_c + nc), pre_c = sum of nc over the failing lanes below
-                // (three ballots: the count and its two low bits)
-                const bool cf = lvalid && !pass;
-                const uint32_t nc1 = (e.id >> 16) & 3u;
-                const unsigned long long F = __ballot(cf), B0 = __ballot(cf && (nc1 & 1u)),
-                                         B1 = __ballot(cf && (nc1 & 2u));
-                if (F) {
-                    auto rank = [&](unsigned long long m) {
-                        return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                    };
-                    const uint32_t pre = rank(F) + rank(B0) + 2u * rank(B1);
-                    const int total = __popcll(F) + __popcll(B0) + 2 * __popcll(B1);
-                    if (cf) {
+                    if (pass) {
+                        // colour sums = n origin + sum u (origin (4R, 8G2, 8B2))
+                        const uint32_t n = (e.id >> 18) & 511u;
+                        const uint32_t ox = ((e.id >> 10) & 63u) * 4u, oy = ((e.id >> 5) & 31u) * 8u, oz = (e.id & 31u) * 8u;
+                        atomicAdd(&sm.accA[k][tid], (unsigned long long)(n * ox + (e.sums & 1023u)) |
+                                                        ((unsigned long long)(n * oy + ((e.sums >> 10) & 2047u)) << 32));
+                        atomicAdd(&sm.accB[k][tid], (unsigned long long)(n * oz + (e.sums >> 21)) |
+                                                        ((unsigned long long)n << 32));
+                    }
+                    // the failing cells' cubes: cell c's nc = 1 + (bits 16..17) cubes go to list
+                    // slots [pre_c, pre_c + nc), pre_c = sum of nc over the failing lanes below
+                    // (three ballots: the count and its two low bits)
+                    const bool cf = lvalid && !pass;
+                    const uint32_t nc1 = (e.id >> 16) & 3u;
+                    const unsigned long long F = __ballot(cf), B0 = __ballot(cf && (nc1 & 1u)),
+                                             B1 = __ballot(cf && (nc1 & 2u));
+                    if (F) {
+                        auto rank = [&](unsigned long long m) {
+                            return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                        };
+                        const uint32_t pre = rank(F) + rank(B0) + 2u * rank(B1);
+                        const int total = __popcll(F) + __popcll(B0) + 2 * __popcll(B1);
+                        if (cf) {
 #pragma unroll
-                        for (uint32_t jj = 0; jj < 4; jj++)
-                            if (jj <= nc1) ql[pre + jj] = (int)(e.first + jj);
+                            for (uint32_t jj = 0; jj < 4; jj++)
+                                if (jj <= nc1) ql[pre + jj] = (int)(e.first + jj);
+                        }
+                        __builtin_amdgcn_wave_barrier();
+                        for (int b = 0; b < total; b += 64) {
+                            const bool v = b + lane < total;
+                            CubeEnt ce;
+                            ce.mask = 0;
+                            ce.id = 0;
+                            ce.sums = 0;
+                            if (v) ce = ctab[ql[b + lane]];
+                            cube_body(ce, v);
+                        }
+                        __builtin_amdgcn_wave_barrier();  // (the next chunk rewrites the list)
                     }
-                    __builtin_amdgcn_wave_barrier();
-                    for (int b = 0; b < total; b += 64) {
-                        const bool v = b + lane < total;
-                        CubeEnt ce;
-                        ce.mask = 0;
-                        ce.id = 0;
-                        ce.sums = 0;
-                        if (v) ce = ctab[ql[b + lane]];
-                        cube_body(ce, v);
-                    }
-                    __builtin_amdgcn_wave_barrier();  // (the next chunk rewrites the list)
+                    base = nb;
                 }
-                base = nb;
+            } else {
+                int base = __builtin_amdgcn_readfirstlane(grab());
+                int ahead = grab();
+                CubeEnt en;
+                en.mask = 0;
+                en.id = 0;
+                en.sums = 0;
+                if (base + lane < C) en = ctab[base + lane];
+                while (base < C) {
+                    const bool valid = base + lane < C;
+                    const CubeEnt e = en;
+                    const int nb = __builtin_amdgcn_readfirstlane(ahead);
+                    if (nb + lane < C) en = ctab[nb + lane];
+                    if (nb < C) ahead = grab();
+                    cube_body(e, valid);
+                    base = nb;
+                }
             }
-#else
-            int base = __builtin_amdgcn_readfirstlane(grab());
-            int ahead = grab();
-            CubeEnt en;
-            en.mask = 0;
-            en.id = 0;
-            en.sums = 0;
-            if (base + lane < C) en = ctab[base + lane];
-            while (base < C) {
-                const bool valid = base + lane < C;
-                const CubeEnt e = en;
-                const int nb = __builtin_amdgcn_readfirstlane(ahead);
-                if (nb + lane < C) en = ctab[nb + lane];
-                if (nb < C) ahead = grab();
-                cube_body(e, valid);
-                base = nb;
-            }
-#endif
             while (head - tail >= 64) label_stage(64);
             if (head > tail) label_stage(head - tail);
 #undef LABEL_FULL
