@@ -372,6 +372,115 @@ void row_to_bgr(const Png &png, const uint8_t *s, uint8_t *o) {
     }
 }
 
+// 8-bit RGB rows unfiltered straight into the BGR output: every PNG filter is per channel
+// (Sub / Avg / Paeth take the same channel of the left, upper and upper-left pixels), so it
+// commutes with the R <-> B swap, and the swapped rows can be unfiltered against the previous
+// BGR output row.  One pass over the row instead of unfilter + convert (round 4: the two
+// were 11 % of a 1080p decode, inflate the rest).  No store passes the row's last byte: the
+// row after it may be another image, decoded by another thread.
+inline uint32_t rgb_bgr32(uint32_t x) { return __builtin_bswap32(x) >> 8; }  // R G B . -> B G R 0
+inline void st24(uint8_t *p, uint32_t v) {
+    p[0] = (uint8_t)v;
+    p[1] = (uint8_t)(v >> 8);
+    p[2] = (uint8_t)(v >> 16);
+}
+
+__attribute__((target("ssse3"))) size_t up_bgr_ssse3(const uint8_t *s, const uint8_t *prior, uint8_t *o, size_t w) {
+    const __m128i m00 = _mm_setr_epi8(2, 1, 0, 5, 4, 3, 8, 7, 6, 11, 10, 9, 14, 13, 12, -1);
+    const __m128i m01 = _mm_setr_epi8(-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, 1);
+    const __m128i m10 = _mm_setr_epi8(-1, 15, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1);
+    const __m128i m11 = _mm_setr_epi8(0, -1, 4, 3, 2, 7, 6, 5, 10, 9, 8, 13, 12, 11, -1, 15);
+    const __m128i m12 = _mm_setr_epi8(-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, 0, -1);
+    const __m128i m21 = _mm_setr_epi8(14, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1);
+    const __m128i m22 = _mm_setr_epi8(-1, 3, 2, 1, 6, 5, 4, 9, 8, 7, 12, 11, 10, 15, 14, 13);
+    size_t x = 0;
+    const bool up = prior != nullptr;
+    for (; x + 16 <= w; x += 16, s += 48, o += 48, prior += up ? 48 : 0) {
+        const __m128i a = _mm_loadu_si128((const __m128i *)s), b = _mm_loadu_si128((const __m128i *)(s + 16)),
+                      c = _mm_loadu_si128((const __m128i *)(s + 32));
+        const __m128i o0 = _mm_or_si128(_mm_shuffle_epi8(a, m00), _mm_shuffle_epi8(b, m01));
+        const __m128i o1 = _mm_or_si128(_mm_or_si128(_mm_shuffle_epi8(a, m10), _mm_shuffle_epi8(b, m11)),
+                                        _mm_shuffle_epi8(c, m12));
+        const __m128i o2 = _mm_or_si128(_mm_shuffle_epi8(b, m21), _mm_shuffle_epi8(c, m22));
+        if (up) {
+            _mm_storeu_si128((__m128i *)o, _mm_add_epi8(o0, _mm_loadu_si128((const __m128i *)prior)));
+            _mm_storeu_si128((__m128i *)(o + 16), _mm_add_epi8(o1, _mm_loadu_si128((const __m128i *)(prior + 16))));
+            _mm_storeu_si128((__m128i *)(o + 32), _mm_add_epi8(o2, _mm_loadu_si128((const __m128i *)(prior + 32))));
+        } else {
+            _mm_storeu_si128((__m128i *)o, o0);
+            _mm_storeu_si128((__m128i *)(o + 16), o1);
+            _mm_storeu_si128((__m128i *)(o + 32), o2);
+        }
+    }
+    return x;
+}
+
+// src: the filtered RGB row (inflated buffer, readable 4 bytes past its end), dst: the BGR
+// output row, prior: the previous BGR output row (nullptr for row 0); w >= 1 pixels
+bool unfilter_rgb_to_bgr(int f, uint8_t *__restrict dst, const uint8_t *__restrict src, const uint8_t *prior,
+                         size_t w) {
+    if (f < 0 || f > 4) return false;
+    size_t x = 0;
+    if (f == 0 || f == 2) {  // None, Up: no left dependency, 16 pixels per step
+        const uint8_t *pr = f == 2 ? prior : nullptr;
+        if (have_ssse3()) x = up_bgr_ssse3(src, pr, dst, w);
+        for (; x < w; x++) {
+            const size_t i = 3 * x;
+            for (int c = 0; c < 3; c++) dst[i + c] = (uint8_t)(src[i + 2 - c] + (pr ? pr[i + c] : 0));
+        }
+        return true;
+    }
+    if (f == 1) {  // Sub: per-byte adds without carries (SWAR)
+        uint32_t a = 0;
+        for (; x < w; x++) {
+            const uint32_t v = rgb_bgr32(ld32(src + 3 * x));
+            a = ((v & 0x7f7f7f7fu) + (a & 0x7f7f7f7fu)) ^ ((v ^ a) & 0x80808080u);
+            if (x + 1 < w) st32(dst + 3 * x, a);
+            else st24(dst + 3 * x, a);
+            a &= 0x00ffffffu;
+        }
+        return true;
+    }
+    const __m128i z = _mm_setzero_si128();
+    auto ldp = [&](size_t i) {  // the previous row's pixel (4-byte load inside the image:
+        // prior's row is followed by dst's)
+        return prior ? _mm_unpacklo_epi8(_mm_cvtsi32_si128((int)ld32(prior + i)), z) : z;
+    };
+    auto put = [&](size_t xx, __m128i v) {
+        const uint32_t u = (uint32_t)_mm_cvtsi128_si32(v);
+        if (xx + 1 < w) st32(dst + 3 * xx, u);
+        else st24(dst + 3 * xx, u);
+    };
+    __m128i a = z, c = z;
+    if (f == 3) {
+        for (; x < w; x++) {
+            const __m128i b = ldp(3 * x);
+            const __m128i avg = _mm_srli_epi16(_mm_add_epi16(_mm_unpacklo_epi8(a, z), b), 1);
+            a = _mm_add_epi8(_mm_cvtsi32_si128((int)rgb_bgr32(ld32(src + 3 * x))), _mm_packus_epi16(avg, avg));
+            put(x, a);
+        }
+    } else {  // Paeth
+        for (; x < w; x++) {
+            const __m128i b = ldp(3 * x);
+            const __m128i a16 = _mm_unpacklo_epi8(a, z);
+            const __m128i bc = _mm_sub_epi16(b, c), ac = _mm_sub_epi16(a16, c);
+            const __m128i pa = _mm_max_epi16(bc, _mm_sub_epi16(z, bc));
+            const __m128i pb = _mm_max_epi16(ac, _mm_sub_epi16(z, ac));
+            const __m128i sm = _mm_add_epi16(bc, ac);
+            const __m128i pc = _mm_max_epi16(sm, _mm_sub_epi16(z, sm));
+            const __m128i use_a = _mm_andnot_si128(_mm_or_si128(_mm_cmpgt_epi16(pa, pb), _mm_cmpgt_epi16(pa, pc)),
+                                                   _mm_set1_epi16(-1));
+            const __m128i use_b = _mm_andnot_si128(_mm_cmpgt_epi16(pb, pc), _mm_set1_epi16(-1));
+            const __m128i bc_sel = _mm_or_si128(_mm_and_si128(use_b, b), _mm_andnot_si128(use_b, c));
+            const __m128i pred = _mm_or_si128(_mm_and_si128(use_a, a16), _mm_andnot_si128(use_a, bc_sel));
+            a = _mm_add_epi8(_mm_cvtsi32_si128((int)rgb_bgr32(ld32(src + 3 * x))), _mm_packus_epi16(pred, pred));
+            put(x, a);
+            c = b;
+        }
+    }
+    return true;
+}
+
 // cv2.imdecode refuses images above CV_IO_MAX_IMAGE_PIXELS (default 2^30 pixels,
 // OPENCV_IO_MAX_IMAGE_PIXELS overrides): here LLFE_MAX_PIXELS, checked from the header
 // before anything is allocated
@@ -405,7 +514,13 @@ int decode_one(const uint8_t *data, size_t size, int32_t h, int32_t w, uint8_t *
     raw.resize(raw_n + 16);       // (4-byte pixel loads read one byte past a row)
     rows.resize(2 * (rowb + 16));  // two unfiltered rows, ping-pong (this row, prior), padded
     rc = inflate_idat(png, raw.data(), raw_n, cat) ? LLFE_OK : LLFE_ERR_INVALID;
-    for (uint32_t y = 0; rc == LLFE_OK && y < png.h; y++) {
+    const bool fused = png.ctype == 2 && png.depth == 8;  // RGB8: unfilter into BGR in one pass
+    for (uint32_t y = 0; fused && rc == LLFE_OK && y < png.h; y++) {
+        const uint8_t *r = raw.data() + y * stride;
+        uint8_t *o = out + (size_t)y * png.w * 3;
+        if (!unfilter_rgb_to_bgr(r[0], o, r + 1, y ? o - (size_t)png.w * 3 : nullptr, png.w)) rc = LLFE_ERR_INVALID;
+    }
+    for (uint32_t y = 0; !fused && rc == LLFE_OK && y < png.h; y++) {
         const uint8_t *r = raw.data() + y * stride;
         uint8_t *cur = rows.data() + (y & 1) * (rowb + 16);
         const uint8_t *prior = y ? rows.data() + ((y - 1) & 1) * (rowb + 16) : nullptr;

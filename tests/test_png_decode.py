@@ -165,3 +165,20 @@ def test_decode_batch_mixed_png_and_jpeg():
     np.testing.assert_array_equal(out[1], _pillow_ref(j.getvalue()))
     out2 = decode.decode_batch([j.getvalue(), p.getvalue()], workers=2)
     np.testing.assert_array_equal(out2[1], a[:, :, ::-1])
+
+
+@pytest.mark.parametrize("w", [37, 32, 1])
+@pytest.mark.parametrize("f", [0, 1, 2, 3, 4])
+def test_rgb8_rows_stay_inside_the_image(w, f):
+    """RGB8 rows are unfiltered straight into the BGR output with 4-byte pixel stores: the
+    byte after an image (the next image of a batch, decoded by another thread) is never
+    written."""
+    rng = np.random.default_rng(w * 10 + f)
+    h = 5
+    raw = rng.integers(0, 256, (h, w * 3), dtype=np.uint8)
+    b = _png_bytes(raw, w, h, 8, 2, [f])
+    backing = np.full((2, h, w, 3), 0xA5, np.uint8)
+    st = decode._native([b], h, w, backing[:1], 1)
+    assert st[0] == 0
+    np.testing.assert_array_equal(backing[0], raw.reshape(h, w, 3)[:, :, ::-1])
+    assert (backing[1] == 0xA5).all()

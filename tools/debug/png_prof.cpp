@@ -18,7 +18,7 @@ int main(int argc, char **argv) {
     std::vector<uint8_t> raw(raw_n + 16), cat, out((size_t)png.w * png.h * 3), un(raw_n + 16);
     int hist[5] = {0};
     double tf[5] = {0};
-    double t_inf = 0, t_unf = 0, t_cvt = 0, t_all = 0;
+    double t_inf = 0, t_unf = 0, t_cvt = 0, t_all = 0, t_fus = 0;
     using C = std::chrono::steady_clock;
     for (int r = 0; r < reps; r++) {
         auto a = C::now();
@@ -36,6 +36,12 @@ int main(int argc, char **argv) {
         auto e = C::now();
         decode_one(d.data(), d.size(), png.h, png.w, out.data());
         auto g = C::now();
+        if (png.ctype == 2 && png.depth == 8)
+            for (uint32_t y = 0; y < png.h; y++) {
+                uint8_t *o = out.data() + (size_t)y * png.w * 3;
+                unfilter_rgb_to_bgr(raw[y * stride], o, raw.data() + y * stride + 1, y ? o - (size_t)png.w * 3 : nullptr, png.w);
+            }
+        t_fus += std::chrono::duration<double, std::milli>(C::now() - g).count();
         t_inf += std::chrono::duration<double, std::milli>(b - a).count();
         t_unf += std::chrono::duration<double, std::milli>(c - b).count();
         t_cvt += std::chrono::duration<double, std::milli>(e - c).count();
@@ -44,5 +50,6 @@ int main(int argc, char **argv) {
     printf("%s %ux%u ctype %d bytes %zu libdeflate %d | inflate %.2f ms unfilter %.2f ms convert %.2f ms | decode_one %.2f ms | filters none/sub/up/avg/paeth %d/%d/%d/%d/%d\n",
            argv[1], png.w, png.h, png.ctype, d.size(), (int)deflate().ok, t_inf / reps, t_unf / reps, t_cvt / reps,
            t_all / reps, hist[0], hist[1], hist[2], hist[3], hist[4]);
+    printf("  fused unfilter + convert (RGB8) %.2f ms\n", t_fus / reps);
     printf("  per filter ms: none %.2f sub %.2f up %.2f avg %.2f paeth %.2f\n", tf[0] / reps, tf[1] / reps, tf[2] / reps, tf[3] / reps, tf[4] / reps);
 }
