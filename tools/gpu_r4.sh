@@ -14,3 +14,4 @@ head -c 1200 gpurun_out/bench_$TAG.json; echo
 tail -3 gpurun_out/bench_$TAG.err
 if [ $brc -ne 0 ]; then echo "bench exit $brc: stopping"; exit $brc; fi
 bash tools/profile.sh $TAG
+bash tools/png_split.sh || { echo "png split failed"; exit 1; }
