@@ -4,7 +4,7 @@ bash tools/debug/identity.sh 2>&1 | grep -v "^$" || exit 1
 bash tools/debug/run_variants.sh || exit 1
 L=low_level_feature_extraction_amd/libllfe.so
 cp $L /tmp/keep.so
-cp tools/debug/variants/libllfe_q_kstage.so $L
+cp tools/debug/variants/libllfe_s_lut_kstage.so $L
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py -k "unique or kmeans" tests/test_gpu_served.py -k "unique or production_keys" > gpurun_out/kstage_tests.log 2>&1; rc=$?
 cp /tmp/keep.so $L
 tail -3 gpurun_out/kstage_tests.log
