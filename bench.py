@@ -220,11 +220,12 @@ def e2e_png(be, B, H, W, feats, steps, distinct, seed, fmt="PNG", decode_steps=2
         pending = []
         for k in range(steps):
             batch = fut.result()
-            pending.append(be.submit(batch, feats, seed=seed + k))
-            # decode batch k + 1 while batch k - 1 is collected (its contours on the host
-            # pool): buffer (k + 1) % 3 last held batch k - 2, collected one step earlier
+            # decode batch k + 1 (started before batch k is submitted, so the decode threads
+            # never wait on the submission) while batch k - 1 is collected: buffer
+            # (k + 1) % 3 last held batch k - 2, collected one step earlier
             if k + 1 < steps:
                 fut = prod.submit(decode.decode_batch, blobs, bufs[(k + 1) % 3], threads)
+            pending.append(be.submit(batch, feats, seed=seed + k))
             if len(pending) == 2:
                 be.collect(pending.pop(0))
         while pending:
@@ -276,7 +277,7 @@ def main():
                          "it does not resize this size: BASELINE configs [3] auto at 1080p, [4] high_quality at 4K)")
     ap.add_argument("--e2e-host-steps", type=int, default=8, help="0 disables the decoded-host-array line")
     ap.add_argument("--seed", type=int, default=2025)
-    ap.add_argument("--e2e-png-steps", type=int, default=4, help="0 disables the PNG end-to-end line")
+    ap.add_argument("--e2e-png-steps", type=int, default=6, help="0 disables the PNG end-to-end line")
     ap.add_argument("--e2e-jpeg-steps", type=int, default=6, help="0 disables the JPEG end-to-end line")
     ap.add_argument("--e2e-at-scale", action="store_true",
                     help="also run the e2e lines when WORLD_SIZE > 1 (off by default: every rank would pin "
