@@ -294,6 +294,11 @@ def main():
                          "llfe_collect_batch: batch k+1's front kernels fill the tail of batch k's k-means; "
                          "kernel timings then come from the same steps run one batch at a time); "
                          "off: one llfe_process_batch per step")
+    ap.add_argument("--inflight", choices=["auto", "2", "3"], default="auto",
+                    help="batches the pipelined loop keeps in flight: auto = 3 for steps of at most "
+                         "256 x 1080p pixels (short steps, where host jitter between collect and the next "
+                         "submit would otherwise idle the GPU: configs[1]/[2] measured +10-25 %%, "
+                         "profiles/r4/inflight/), else 2 (the headline: no difference, one workspace less)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -323,6 +328,10 @@ def main():
     from low_level_feature_extraction_amd.backend import Backend
 
     be = Backend.get(local)
+    depth = (3 if args.batch * args.height * args.width <= 256 * 1080 * 1920 else 2) if args.inflight == "auto" \
+        else int(args.inflight)
+    if args.pipeline == "on":
+        be.inflight = depth
     if args.contours != "auto":
         be.set_contour_mode(args.contours)
     feats = tuple(f for f in args.features.split(",") if f)
@@ -361,7 +370,7 @@ def main():
         """k_steps full passes over the batch (``imgs`` unless given), each ending with every
         image's reference-shaped result objects on the host (assembled on a worker thread
         while the GPU runs the next batches; the caller's timed region waits for them).
-        Pipelined: a serving loop that keeps two batches in flight (llfe_submit_batch /
+        Pipelined: a serving loop that keeps be.inflight batches in flight (llfe_submit_batch /
         llfe_collect_batch), so batch k + 1's front kernels start in the tail of batch k's
         k-means."""
         batch = imgs if batch is None else batch
@@ -550,6 +559,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(dt / args.steps * 1e3, 3),
         "pipelined": pipelined,
+        "inflight": be.inflight if pipelined else 1,
         "value_one_batch_at_a_time": round(total_images / dt_sync, 2) if dt_sync else None,
         "higher_is_better": True,
         "scaling": "weak",
