@@ -196,11 +196,21 @@ def test_headline_512_two_in_flight(backend, orc, served1080):
 
 @pytest.mark.parametrize("feats", [("colors",), ("colors", "shapes")], ids=["configs1", "configs2"])
 def test_256_configs(backend, orc, served1080, feats):
-    """configs[1] / configs[2] per GPU: 256 x 1080p.  Results equal the 512 launch's for the
-    same seed and global index (seeds follow the image, not the batch), and the oracle."""
+    """configs[1] / configs[2] per GPU: 256 x 1080p, three batches in flight as bench.py
+    keeps them at this size (--inflight auto), four submissions so the first slot is reused.
+    Results equal the 512 launch's for the same seed and global index (seeds follow the
+    image, not the batch), and the oracle."""
     sub = served1080.dev[:256]
-    seeds = [SEED, SEED + 7]
-    runs = _serve(backend, sub, feats, seeds)
+    seeds = [SEED, SEED + 7, SEED + 3, SEED]
+    assert backend.inflight == 2
+    backend.inflight = 3
+    try:
+        runs = _serve(backend, sub, feats, seeds)
+    finally:
+        backend.inflight = 2
+    for a, b in zip(runs[0], runs[3]):  # slot 0 reused by the fourth batch, same seed
+        assert np.array_equal(a.centers_rgb, b.centers_rgb) and np.array_equal(a.counts, b.counts)
+        assert a.n_unique == b.n_unique and a.shapes == b.shapes
     every = list(range(256))
     _check_n_unique(orc, served1080, runs[0], seeds[0], every)
     ref = getattr(served1080, "runs512", None)
