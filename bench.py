@@ -11,6 +11,10 @@ host.  Per-GPU batch is fixed (weak scaling): BASELINE.json config 4 is 4096 ima
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
+--gpus is authoritative: without a launcher (no WORLD_SIZE) and N > 1 the script starts N
+ranks itself under torch.distributed.run (child processes, before any GPU call); under a
+launcher WORLD_SIZE must equal N.
+
 Rank 0 prints ONE JSON line.  Kernel durations come from hipEvents recorded by
 libllfe on the launch stream during the timed steps (llfe_set_profiling); the
 `cpu_baseline` leg runs the CPU oracle (C restatement of the reference's
@@ -258,6 +262,34 @@ def _config_name(B, H, W, feats, pre):
     return "custom"
 
 
+def launch_ranks(n: int, argv: list[str]) -> list[str]:
+    """The command that runs this script as `n` ranks of one node (one process per GPU,
+    Dockerfile:26's process-per-worker model): torch.distributed.run on 127.0.0.1 with a
+    free port, the same arguments."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+
+
+def check_world(gpus: int, env=os.environ) -> str:
+    """--gpus is authoritative.  'launch': no launcher ran us and N > 1, so start N ranks
+    (before anything touches the GPU); 'run': this process is one rank of the N asked for
+    (or the single rank of N = 1).  A launcher whose WORLD_SIZE disagrees with --gpus is
+    an error: the line would report a GPU count that did not run."""
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1, got {gpus}")
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return "launch" if gpus > 1 else "run"
+    if int(ws) != gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={ws} from the launcher but --gpus {gpus}; they must agree")
+    return "run"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -288,7 +320,7 @@ def main():
     ap.add_argument("--contours", choices=["auto", "host", "gpu"], default="auto",
                     help="where findContours + the shape loop run: the host pool from the copied-back mask "
                          "(overlaps k-means), the GPU (contours_gpu.hip), or auto (the library's choice: "
-                         "host unless the rank has < 8 host cores)")
+                         "host unless the rank has < 4 host cores)")
     ap.add_argument("--pipeline", choices=["on", "off"], default="on",
                     help="on: a serving loop with two batches in flight (llfe_submit_batch / "
                          "llfe_collect_batch: batch k+1's front kernels fill the tail of batch k's k-means; "
@@ -299,7 +331,23 @@ def main():
                          "256 x 1080p pixels (short steps, where host jitter between collect and the next "
                          "submit would otherwise idle the GPU: configs[1]/[2] measured +10-25 %%, "
                          "profiles/r4/inflight/), else 2 (the headline: no difference, one workspace less)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch the ranks, initialise the process group and run the control-plane collectives "
+                         "(barrier, MAX over ranks), print the line's identity fields with value null; no workload")
     args = ap.parse_args()
+
+    if check_world(args.gpus) == "launch":
+        # no GPU call has happened in this process: the ranks are children, and this
+        # process only waits for them and exits with their status
+        import subprocess
+
+        if os.environ.get("LLFE_BENCH_SHARE_GPU") != "1":
+            import torch  # device_count() does not initialise the GPU
+
+            have = torch.cuda.device_count()
+            if have < args.gpus:
+                raise SystemExit(f"bench.py: --gpus {args.gpus} but {have} GPUs are visible")
+        sys.exit(subprocess.call(launch_ranks(args.gpus, sys.argv[1:])))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1 and not args.e2e_at_scale:
@@ -314,7 +362,12 @@ def main():
 
     import torch
 
-    torch.cuda.set_device(local)
+    # --dry-run on a host without a GPU: the rank / collective plumbing only (CPU tests)
+    no_gpu = args.dry_run and not torch.cuda.is_available()
+    if no_gpu:
+        share_gpu = True
+    else:
+        torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -323,6 +376,20 @@ def main():
             dist.init_process_group("gloo")  # (host tensors for its collectives: coll_dev)
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if args.dry_run:
+        from low_level_feature_extraction_amd import shard
+
+        base, stop = shard.shard_bounds(args.batch * world, rank, world)
+        shard.barrier(device=None if no_gpu else local)
+        t = shard.max_over_ranks(float(rank), device=None if share_gpu else f"cuda:{local}")
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "dry_run": True, "n_gpus": world,
+                              "max_over_ranks_probe": t,
+                              "config": {"global_batch": args.batch * world, "batch_per_gpu": args.batch,
+                                         "parallelism": f"replicas x{world} (host-side shard, no collective)"}}))
+        if dist is not None:
+            dist.destroy_process_group()
+        return
 
     from low_level_feature_extraction_amd import shard, synth
     from low_level_feature_extraction_amd.backend import Backend
