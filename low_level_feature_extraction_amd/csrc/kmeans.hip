@@ -27,7 +27,10 @@
 namespace llfe {
 namespace {
 
-constexpr int kCellMinCubes = 8192;  // the sweeps test cells before cubes from this cube count on
+constexpr int kCellMinCubes = 8192;
+#ifndef LLFE_KM_LLOYD_QUEUE
+#define LLFE_KM_LLOYD_QUEUE 0  // Lloyd as a work queue too (1) or one workgroup per attempt (0)
+#endif  // the sweeps test cells before cubes from this cube count on
 #ifndef LLFE_KM_THREADS
 #define LLFE_KM_THREADS 512
 #endif
@@ -132,8 +135,12 @@ constexpr int SEL_U = 4;
 #define LLFE_KM_PPRUN 4
 #endif
 constexpr int kPPRun = LLFE_KM_PPRUN;  // 64-cube chunks per k-means++ work grab
-// per-wave LDS ring of boundary colours awaiting labelling (>= 64 + 64 x unroll)
-constexpr int kStage = LLFE_KM_UNROLL <= 2 ? 256 : 512;
+// per-wave LDS ring of boundary colours awaiting labelling: the Lloyd sweep drains it
+// once 128 colours are pending, so it holds <= 127 pending + LLFE_KM_UNROLL x 64 pushed
+// (k-means++ drains at 64); a power of two (ring indices are masked)
+constexpr int ring_size(int need) { return need <= 256 ? 256 : (need <= 512 ? 512 : 1024); }
+constexpr int kStage = ring_size(127 + 64 * LLFE_KM_UNROLL);
+static_assert(kStage >= 127 + 64 * LLFE_KM_UNROLL && (kStage & (kStage - 1)) == 0, "boundary-colour ring too small");
 
 // the 4 keys of lane `lane` in 256-point step `s` (zeros past the full steps)
 __device__ __forceinline__ uint4 load_step(const uint32_t *pts, int s, int se_full, int lane) {
@@ -169,6 +176,7 @@ struct KmSmem {
     unsigned long long found_excl[3];
     int ci[3];
     int flag;
+    int task;                            // work-queue item of the workgroup (persistent launches)
     int next_chunk;                      // next 64-cube chunk to hand out (cube sweeps)
     unsigned long long fail_pts;  // keys read point by point in this Lloyd sweep
     // cube-based k-means++ (pp_cubes)
@@ -340,9 +348,17 @@ __device__ __forceinline__ int dmin_chosen(int x, int y, int z, const ICent &ch,
     return d;
 }
 
-__device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, int K, uint64_t &rng,
-                         const CubeEnt *__restrict__ ctab, int C, const CellEnt *__restrict__ ltab, int L, int cb,
-                         int cend, const uint32_t *__restrict__ part_uq, unsigned long long &bytes,
+// Inlined into the k-means++ kernel (its only caller): 105 VGPRs and no scratch; as a
+// call the kernel needed 128 VGPRs with 2 spilled (LLFE_KM_PP_CALL=1 keeps the call for
+// measurements).
+#if LLFE_KM_PP_CALL
+__device__
+#else
+__device__ __forceinline__
+#endif
+void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, int K, uint64_t &rng,
+                         const CubeEnt *__restrict__ ctab, int C, const CellEnt *__restrict__ ltab, int L,
+                         const uint32_t *__restrict__ part_uq, unsigned long long &bytes,
                          uint32_t &pp_pts, uint32_t &pp_sel, uint64_t &t_sel) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     if (wid == 0) {
@@ -1002,31 +1018,59 @@ __device__ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, in
 #ifndef LLFE_KM_MINW
 #define LLFE_KM_MINW 4
 #endif
-// kCubes: the cube-table path (the batch pipeline); !kCubes: plain sweeps over
-// caller-supplied keys (llfe_kmeans).  Separate instantiations keep the plain path's
-// register-heavy prefetch out of the hot kernel.
-template <bool kCubes>
+// k-means attempts, one workgroup per (image, attempt) task; tasks are numbered in LPT
+// order (task t = attempt t % 10 of image order[t / 10]).  kPhase: 3 = k-means++ and Lloyd
+// (the plain path, one launch); 1 = k-means++ only (the cube path's first launch: the
+// chosen centres, Sum |p|^2 and the k-means++ counters go to the attempt record); 2 =
+// Lloyd only (the cube path's second launch, starting from that record).  kQueue: one
+// workgroup per resident slot takes tasks from the global counter `queue` until they run
+// out (else task = blockIdx.x).  kCubes: the cube-table path (the batch pipeline);
+// !kCubes: plain sweeps over caller-supplied keys (llfe_kmeans).  Separate instantiations
+// keep the plain path's register-heavy prefetch out of the hot kernels.  (The body stays
+// in the kernel: as an inlined device function the Lloyd sweep lost its register budget
+// and spilled 20 VGPRs.)
+template <bool kCubes, int kPhase, bool kQueue>
 __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__restrict__ keys, long long key_stride,
-                                               const long long *__restrict__ n_unique, int n_colors,
-                                               unsigned long long seed, ImgIndex index,
-                                               const int *__restrict__ order,
-                                               uint32_t *__restrict__ scratch, long long scratch_stride,
-                                               KmeansAttemptOut *__restrict__ out, const KmeansCubes cubes) {
+                                                   const long long *__restrict__ n_unique, int n_colors,
+                                                   unsigned long long seed, ImgIndex index,
+                                                   const int *__restrict__ order, int n_tasks,
+                                                   int *__restrict__ queue, uint32_t *__restrict__ scratch,
+                                                   long long scratch_stride, KmeansAttemptOut *__restrict__ out,
+                                                   const KmeansCubes cubes) {
+    static_assert(kPhase == 3 || kCubes, "the plain path runs both phases in one workgroup");
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     KmSmem &sm = *reinterpret_cast<KmSmem *>(smem_raw);
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int img = order[blockIdx.x / kAttempts];
-    const int att = blockIdx.x % kAttempts;
+    int task = blockIdx.x;
+    if (kQueue) {
+        if (tid == 0) sm.task = atomicAdd(queue, 1);
+        __syncthreads();
+        task = sm.task;
+        __syncthreads();
+    }
+    while (task < n_tasks) {  // (every workgroup of a queue launch leaves once the counter passes n_tasks)
+    {
+    const int img = order[task / kAttempts];
+    const int att = task % kAttempts;
     const int N = (int)n_unique[img];
     const int K = min(n_colors, N);
     KmeansAttemptOut *o = out + (size_t)img * kAttempts + att;
+    if (kPhase == 1 && K <= 1) goto next_task;  // (no k-means: the Lloyd launch writes the record)
     if (tid == 0) {
         unsigned hw, xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        o->t_start = wall_clock64();
-        o->hw_id = hw;
-        o->xcc_id = xcc;
+        const uint64_t t = wall_clock64();
+        if (kPhase & 1) {
+            o->t_start = t;
+            o->hw_id = hw;
+            o->xcc_id = xcc;
+        }
+        if (kPhase & 2) {
+            o->t_lstart = t;
+            o->hw_id2 = hw;
+            o->xcc_id2 = xcc;
+        }
     }
     if (K <= 1) {
         if (tid == 0) {
@@ -1039,9 +1083,15 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
             o->ll_pts = 0;
             o->t_sw = 0;
             o->drift_hist = 0;
+            o->pad = 0;
             o->t_end = wall_clock64();
+            if (kPhase == 2) {  // (the k-means++ launch skipped the attempt)
+                o->t_start = o->t_pp = o->t_lstart;
+                o->hw_id = o->hw_id2;
+                o->xcc_id = o->xcc_id2;
+            }
         }
-        return;
+        goto next_task;
     }
     const uint32_t *pts = keys + (size_t)img * key_stride;
     const int M = (N + STEP - 1) / STEP;         // steps
@@ -1056,8 +1106,6 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
     constexpr bool use_cubes = kCubes;
     const int C = use_cubes ? cubes.n_cubes[img] : 0;
     const CubeEnt *ctab = use_cubes ? cubes.cubes + (size_t)img * cubes.cube_stride : nullptr;
-    const int Cw = (C + KW - 1) / KW;
-    const int cb = min(C, wid * Cw), cend = min(C, cb + Cw);
     uint32_t pp_pts = 0, pp_sel = 0;
     uint64_t t_sel = 0, ll_pts = 0;
     // plain path: k-means++ + compactness passes; the cube path adds what its passes read
@@ -1065,13 +1113,14 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
     if (tid == 0) sm.fail_pts = 0;
 #define SSLOT(slot) (ss + (size_t)(slot) * (size_t)M)
 
+    if (kPhase & 1) {
     uint64_t rng = splitmix64(seed + (unsigned long long)index.at(img));
     if (rng == 0) rng = 0xFFFFFFFFull;  // cv::RNG(0) takes the default state
     for (int q = 0, skip = att * (1 + 6 * (K - 1)); q < skip; q++) cvrng_next(rng);
 
     // ------------------------------------------------ k-means++ (generateCentersPP)
     if (use_cubes) {
-        pp_cubes(sm, pts, N, K, rng, ctab, C, cubes.cells + (size_t)img * cubes.cube_stride, cubes.n_cells[img], cb, cend, cubes.part_uq + (size_t)img * kParts, bytes, pp_pts, pp_sel, t_sel);
+        pp_cubes(sm, pts, N, K, rng, ctab, C, cubes.cells + (size_t)img * cubes.cube_stride, cubes.n_cells[img], cubes.part_uq + (size_t)img * kParts, bytes, pp_pts, pp_sel, t_sel);
     } else {
     int cur = 0;
     {
@@ -1287,6 +1336,28 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
 
     }  // k-means++
     if (tid == 0) o->t_pp = wall_clock64();
+    }  // kPhase & 1
+    if (kPhase == 1) {
+        // hand the attempt to the Lloyd launch: chosen centres, Sum |p|^2, counters
+        if (tid < kMaxK * 3) (&o->centers[0][0])[(tid / 3) * 3 + tid % 3] = sm.cc[tid / 3][tid % 3];
+        if (tid == 0) {
+            o->qtot = sm.qtot;
+            o->bytes = bytes;
+            o->pp_pts = pp_pts;
+            o->pad = (int32_t)pp_sel;
+            o->t_sel = t_sel;
+        }
+        goto next_task;
+    }
+    if (kPhase == 2) {
+        if (tid < kMaxK * 3) {
+            const int k = tid / 3, j = tid % 3;
+            sm.cc[k][j] = k < K ? o->centers[k][j] : kFar;
+        }
+        if (tid == 0) sm.qtot = o->qtot;
+        bytes = o->bytes;
+        __syncthreads();
+    }
     // ------------------------------------------------ Lloyd iterations
     if (tid < kMaxK * 3) {
         int k = tid / 3, j = tid % 3;
@@ -1446,7 +1517,7 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
                 const uint32_t okey = cube_origin_key(e.id);
                 const uint32_t mlo = (uint32_t)e.mask, mhi = (uint32_t)(e.mask >> 32);
                 // LLFE_KM_UNROLL failing cubes per trip: independent readlane / mbcnt chains
-                // interleave; the ring (kStage) holds <= 63 pending + UNROLL x 64 new colours
+                // interleave; the ring (kStage) holds <= 127 pending + UNROLL x 64 new colours
                 auto push = [&](int src) {
                     const unsigned long long m =
                         ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(mhi, src) << 32) |
@@ -1827,9 +1898,11 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
             o->compactness = compactness;
             o->iters = iter;
             o->bytes = bytes;
-            o->pp_pts = pp_pts;
-            o->pad = (int32_t)pp_sel;
-            o->t_sel = t_sel;
+            if (kPhase & 1) {
+                o->pp_pts = pp_pts;
+                o->pad = (int32_t)pp_sel;
+                o->t_sel = t_sel;
+            }
             o->ll_pts = ll_pts;
             o->t_sw = t_sw;
             o->n_cubes = (uint32_t)C;
@@ -1841,7 +1914,27 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
             }
         }
     }
+    }  // (the task's scope)
+    next_task:
+    if (!kQueue) break;
+    __syncthreads();  // (the task's last LDS reads before thread 0 rewrites sm.task)
+    if (tid == 0) sm.task = atomicAdd(queue, 1);
+    __syncthreads();
+    task = sm.task;
+    __syncthreads();
+    }
 }
+
+// The cube path runs in two launches.  Attempt durations vary 1-8x (k-means++ on ~3k-cube
+// ui tables vs ~35k-cube photos; Lloyd 12-97 iterations), and the dispatcher places
+// workgroup i on XCD i mod 8 in order, so with one workgroup per attempt a slot freed on
+// one XCD waits while the next workgroup's XCD is full: ~15 % of the slots idled between
+// attempts (profiles/r4/dispatch_gap/).  A work queue removes that -- one
+// workgroup per resident slot takes the next task from a global counter -- but the task
+// loop around the whole attempt spilled registers (round 4).  Split, each phase is its own
+// kernel with its own register allocation: k-means++ as a work queue (<true, 1, true>),
+// then Lloyd from its centres (<true, 2, LLFE_KM_LLOYD_QUEUE>).  The counters sit after the
+// LPT order (order[n], order[n + 1]), zeroed by k_kmeans_order.
 
 // LPT order: images sorted by U descending, index ascending on ties (n <= 4096): each
 // image's rank is the number of images before it in that order (LDS broadcast reads;
@@ -1862,6 +1955,7 @@ __global__ __launch_bounds__(OT) void k_kmeans_order(const long long *__restrict
         }
         order[r] = i;
     }
+    if (threadIdx.x < 2) order[n + threadIdx.x] = 0;  // the work-queue counters
 }
 
 __global__ void k_kmeans_finalize(const uint32_t *__restrict__ keys, long long key_stride,
@@ -1923,21 +2017,37 @@ hipError_t launch_kmeans(const uint32_t *keys, int64_t key_stride, const int64_t
     if (n > OMAX) return hipErrorInvalidValue;
     if (n == 0) return hipSuccess;
     // the dynamic-LDS attribute is per device: set once per device id, under a lock (one
-    // context per GPU per host thread, so several threads / devices can get here at once)
+    // context per GPU per host thread, so several threads / devices can get here at once);
+    // with it the resident workgroup slots of the work-queue kernels (CUs x workgroups
+    // per CU at this LDS / register use)
     static std::mutex attr_mu;
     static uint64_t attr_set = 0;  // bit d: set on device d
+    static int slots_pp[64], slots_ll[64];
     const size_t smem = sizeof(KmSmem);
+    constexpr bool kLloydQueue = LLFE_KM_LLOYD_QUEUE;
+    const void *plain = (const void *)k_kmeans<false, 3, false>, *pp = (const void *)k_kmeans<true, 1, true>,
+               *lloyd = (const void *)k_kmeans<true, 2, kLloydQueue>;
+    int dev = 0;
     {
-        int dev = 0;
         hipError_t e = hipGetDevice(&dev);
         if (e != hipSuccess) return e;
+        if (dev >= 64) return hipErrorInvalidDevice;
         std::lock_guard<std::mutex> lk(attr_mu);
-        const uint64_t bit = dev < 64 ? 1ull << dev : 0;
-        if (!bit || !(attr_set & bit)) {
-            e = hipFuncSetAttribute((const void *)k_kmeans<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        const uint64_t bit = 1ull << dev;
+        if (!(attr_set & bit)) {
+            for (const void *f : {plain, pp, lloyd}) {
+                e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+                if (e != hipSuccess) return e;
+            }
+            int cus = 0, per_pp = 0, per_ll = 0;
+            e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
             if (e != hipSuccess) return e;
-            e = hipFuncSetAttribute((const void *)k_kmeans<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_pp, pp, KT, smem);
             if (e != hipSuccess) return e;
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_ll, lloyd, KT, smem);
+            if (e != hipSuccess) return e;
+            slots_pp[dev] = std::max(1, cus * per_pp);
+            slots_ll[dev] = std::max(1, cus * per_ll);
             attr_set |= bit;
         }
     }
@@ -1946,10 +2056,19 @@ hipError_t launch_kmeans(const uint32_t *keys, int64_t key_stride, const int64_t
         const hipError_t e = launch_kmeans_big(keys, key_stride, n_unique, n, n_colors, seed, index, order,
                                                scratch, scratch_stride, attempts, s);
         if (e != hipSuccess) return e;
-    } else {
-        hipLaunchKernelGGL(cubes.cubes ? k_kmeans<true> : k_kmeans<false>, dim3(n * kAttempts), dim3(KT), smem, s, keys,
+    } else if (!cubes.cubes) {
+        hipLaunchKernelGGL((k_kmeans<false, 3, false>), dim3(n * kAttempts), dim3(KT), smem, s, keys,
                            (long long)key_stride, (const long long *)n_unique, n_colors, (unsigned long long)seed,
-                           index, order, scratch, (long long)scratch_stride, attempts, cubes);
+                           index, order, n * kAttempts, nullptr, scratch, (long long)scratch_stride, attempts, cubes);
+    } else {
+        const int tasks = n * kAttempts;
+        hipLaunchKernelGGL((k_kmeans<true, 1, true>), dim3(std::min(tasks, slots_pp[dev])), dim3(KT), smem, s, keys,
+                           (long long)key_stride, (const long long *)n_unique, n_colors, (unsigned long long)seed,
+                           index, order, tasks, order + n, nullptr, 0LL, attempts, cubes);
+        hipLaunchKernelGGL((k_kmeans<true, 2, kLloydQueue>), dim3(kLloydQueue ? std::min(tasks, slots_ll[dev]) : tasks),
+                           dim3(KT), smem, s, keys, (long long)key_stride, (const long long *)n_unique, n_colors,
+                           (unsigned long long)seed, index, order, tasks, order + n + 1, nullptr, 0LL, attempts,
+                           cubes);
     }
     hipLaunchKernelGGL(k_kmeans_finalize, dim3((n + 255) / 256), dim3(256), 0, s, keys, (long long)key_stride,
                        (const long long *)n_unique, n, n_colors, attempts, out);

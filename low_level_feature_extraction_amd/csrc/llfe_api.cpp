@@ -544,7 +544,11 @@ int run_hysteresis_dilate(llfe_ctx *ctx, Work &W, int n, int h, int w, uint64_t 
     HystWork wk;
     const int rc = hyst_work(ctx, W, n, h, w, &wk);
     if (rc) return rc;
-    TIMED(ctx, s, "k_hysteresis_dilate", (double)n * h * w * (1 + 2 + 1 + 2 + 3 * 0.125),
+    // algorithmic bytes (which folds hysteresis into the fused 4P stencil
+    // front): what any implementation of this stage must move -- the class map read (P) and
+    // the bit-packed dilated mask written (P/8).  The CC labels and tile bitmaps it also
+    // reads and writes are the implementation's (PMC saw ~2.4 P per image, round 4).
+    TIMED(ctx, s, "k_hysteresis_dilate", (double)n * h * w * (1 + 0.125),
           launch_hysteresis_dilate(W.d_cls.p, n, h, w, wk, bits, mask_u8, s));
     return LLFE_OK;
 }
@@ -652,7 +656,7 @@ int kmeans_stage(llfe_ctx *ctx, Work &W, const uint32_t *keys, int64_t key_strid
     if (n_colors < 1 || n_colors > kMaxColors)
         return ctx->fail(LLFE_ERR_UNSUPPORTED, "n_colors must be in [1, LLFE_MAX_COLORS]");
     const int64_t sstride = kmeans_scratch_stride(key_stride);
-    HIPCHK(ctx, W.d_order.ensure(n));
+    HIPCHK(ctx, W.d_order.ensure((size_t)n + 2));  // LPT order + the two work-queue counters
     HIPCHK(ctx, W.d_kscratch.ensure((size_t)n * kAttempts * sstride));
     HIPCHK(ctx, W.d_att.ensure((size_t)n * kAttempts));
     HIPCHK(ctx, W.d_kout.ensure(n));
@@ -671,10 +675,11 @@ int kmeans_stage(llfe_ctx *ctx, Work &W, const uint32_t *keys, int64_t key_strid
             for (int i = 0; i < n; i++)
                 for (int a = 0; a < kAttempts; a++) {
                     const KmeansAttemptOut &o = att[(size_t)i * kAttempts + a];
-                    fprintf(f, "%d %d %lld %d %llu %llu %u %u %llu %llu %llu %u %u %d %llu %llu %llu 0 0 %llu\n", i, a, (long long)nu[i], o.iters,
+                    fprintf(f, "%d %d %lld %d %llu %llu %u %u %llu %llu %llu %u %u %d %llu %llu %llu 0 0 %llu %llu %u %u\n", i, a, (long long)nu[i], o.iters,
                             (unsigned long long)o.t_start, (unsigned long long)o.t_end, o.hw_id, o.xcc_id,
                             (unsigned long long)o.t_pp, (unsigned long long)o.t_lloyd, (unsigned long long)o.bytes, o.pp_pts, o.n_cubes, o.pad, (unsigned long long)o.t_sel,
-                            (unsigned long long)o.ll_pts, (unsigned long long)o.t_sw, (unsigned long long)o.drift_hist);
+                            (unsigned long long)o.ll_pts, (unsigned long long)o.t_sw, (unsigned long long)o.drift_hist,
+                            (unsigned long long)o.t_lstart, o.hw_id2, o.xcc_id2);
                 }
             fclose(f);
         }

@@ -155,6 +155,9 @@ struct KmeansAttemptOut {
     uint64_t ll_pts;           // colours Lloyd labelled one by one (all sweeps)
     uint64_t t_sw;             // Lloyd time in the labelling sweeps (ticks)
     uint64_t drift_hist;       // Lloyd iterations by largest centre move (8 x u8 bins)
+    uint64_t qtot;             // sum of |p|^2 over the image's colours (k-means++ -> Lloyd launch)
+    uint64_t t_lstart;         // Lloyd launch: start of the attempt's workgroup
+    uint32_t hw_id2, xcc_id2;  // ... and its placement
 };
 
 struct KmeansImageOut {
@@ -231,6 +234,7 @@ hipError_t launch_uq_gather(const uint32_t *skeys, int n, int64_t key_stride, co
 // per image: K = min(n_colors, U); attempts run as separate workgroups
 // (ordered largest U first), then a finalize kernel picks the best attempt.
 // cv::RNG state of image i = splitmix64(seed + index.at(i)), 0 -> 0xffffffff
+// order: n + 2 ints (the LPT order, then the work-queue counters of the cube path)
 hipError_t launch_kmeans(const uint32_t *keys, int64_t key_stride, const int64_t *n_unique, int n, int n_colors,
                          uint64_t seed, ImgIndex index, int32_t *order, uint32_t *scratch, int64_t scratch_stride,
                          KmeansAttemptOut *attempts, KmeansImageOut *out, const KmeansCubes &cubes,

@@ -416,8 +416,10 @@ __attribute__((target("ssse3"))) size_t up_bgr_ssse3(const uint8_t *s, const uin
 }
 
 // src: the filtered RGB row (inflated buffer, readable 4 bytes past its end), dst: the BGR
-// output row, prior: the previous BGR output row (nullptr for row 0); w >= 1 pixels
-bool unfilter_rgb_to_bgr(int f, uint8_t *__restrict dst, const uint8_t *__restrict src, const uint8_t *prior,
+// output row, prior: the previous BGR output row (nullptr for row 0); w >= 1 pixels.  dst is
+// not __restrict: prior is the row before it in the same buffer, and the last pixel's
+// 4-byte load of prior reaches dst[0] (a discarded lane, but the memory is shared).
+bool unfilter_rgb_to_bgr(int f, uint8_t *dst, const uint8_t *__restrict src, const uint8_t *prior,
                          size_t w) {
     if (f < 0 || f > 4) return false;
     size_t x = 0;

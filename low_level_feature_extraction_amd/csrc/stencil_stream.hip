@@ -35,10 +35,23 @@
 namespace llfe {
 namespace {
 
+// (analysis builds only, -DLLFE_ST_MARK: stage markers in the ISA for the per-stage
+// instruction table of tools/stencil_isa.py)
+// ST_PIN(x) materialises a stage's result before the next marker, so code motion cannot
+// sink the stage's instructions into a later one
+#if LLFE_ST_MARK
+#define ST_MARK(name) do { __builtin_amdgcn_sched_barrier(0); asm volatile(";@st " #name); __builtin_amdgcn_sched_barrier(0); } while (0)
+#define ST_PIN(x) asm volatile("" : "+v"(x))
+#define ST_RARE() asm volatile(";@rare")
+#else
+#define ST_RARE()
+#define ST_MARK(name)
+#define ST_PIN(x)
+#endif
+
 constexpr int kLanesOut = 60;               // lanes 2 .. 61 produce output
 constexpr int kStripW = 4 * kLanesOut;      // 240 output columns per wave
 constexpr int kHalo = 8;                    // columns left of the strip's first output
-constexpr int kRing = 11;
 constexpr int kWavesPerBlock = 4;
 
 typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
@@ -118,6 +131,15 @@ __device__ __forceinline__ uint32_t gray4(Raw r) {
     return y0 | (y1 << 8) | (y2 << 16) | (y3 << 24);
 }
 
+// {1, 1} the optimiser cannot see: min(sub_sat(a, b), 1) with a visible 1 is folded into
+// a per-half compare (a > b), which gfx950 has only for one u16 at a time -- two v_cmp, two
+// v_cndmask and a v_perm instead of one v_pk_min_u16 per pair (ISA, tools/stencil_isa.py)
+__device__ __forceinline__ uint32_t opaque_ones() {
+    uint32_t v;
+    asm("s_mov_b32 %0, 0x10001" : "=s"(v));
+    return v;
+}
+
 __device__ __forceinline__ uint32_t lo2(uint32_t g) { return __builtin_amdgcn_perm(0u, g, 0x0c010c00u); }  // bytes 0,1 -> u16x2
 __device__ __forceinline__ uint32_t hi2(uint32_t g) { return __builtin_amdgcn_perm(0u, g, 0x0c030c02u); }  // bytes 2,3 -> u16x2
 
@@ -165,6 +187,7 @@ __device__ __forceinline__ bool sobel4(uint32_t b0, uint32_t b1, uint32_t b2, ui
     const bool need = (int)m_lo.x > LOW || (int)m_lo.y > LOW || (int)m_hi.x > LOW || (int)m_hi.y > LOW;
     const bool wave_need = __ballot(need) != 0;
     if (wave_need) {
+        ST_MARK(direction);
         const int gxs[4] = {gx_lo.x, gx_lo.y, gx_hi.x, gx_hi.y};
         const int gys[4] = {gy_lo.x, gy_lo.y, gy_hi.x, gy_hi.y};
         const int axs[4] = {ax_lo.x, ax_lo.y, ax_hi.x, ax_hi.y};
@@ -181,6 +204,7 @@ __device__ __forceinline__ bool sobel4(uint32_t b0, uint32_t b1, uint32_t b2, ui
         }
         lo |= (d[0] << 12) | (d[1] << 28);
         hi |= (d[2] << 12) | (d[3] << 28);
+        ST_MARK(direction_end);
     }
     mlo = lo;
     mhi = hi;
@@ -206,7 +230,7 @@ __device__ __forceinline__ uint32_t nms4(uint32_t alo, uint32_t ahi, uint32_t ml
     // the neighbour lanes' dwords: cols (c-2, c-1) from the left, (c+4, c+5) from the right
     const uint32_t Ap = from_left(A1), An = from_right(A0), Mp = from_left(M1), Mn = from_right(M0),
                    Bp = from_left(B1), Bn = from_right(B0);
-    const u16x2 one = {1, 1}, low1 = {51, 51}, high1 = {151, 151};
+    const u16x2 one = {1, 1}, low1 = {51, 51}, high1 = {151, 151}, one_o = U(opaque_ones());
     auto cls2 = [&](uint32_t Ac, uint32_t AL, uint32_t AR, uint32_t Mc, uint32_t ML, uint32_t MR, uint32_t Bc,
                     uint32_t BL, uint32_t BR, uint32_t mraw) {
         const u16x2 t0 = __builtin_elementwise_max(U(ML) + one, U(MR));
@@ -218,8 +242,8 @@ __device__ __forceinline__ uint32_t nms4(uint32_t alo, uint32_t ahi, uint32_t ml
         const uint32_t m1 = W32(z - U((mraw >> 13) & 0x00010001u));  // dir bit 1
         const uint32_t T = bsel(m1, bsel(m0, W32(t3), W32(t2)), bsel(m0, W32(t1), W32(t0)));
         const u16x2 Tm = __builtin_elementwise_max(U(T), low1);
-        const u16x2 nk = __builtin_elementwise_min(__builtin_elementwise_sub_sat(Tm, U(Mc)), one);    // 1: suppressed
-        const u16x2 ns = __builtin_elementwise_min(__builtin_elementwise_sub_sat(high1, U(Mc)), one); // 1: not strong
+        const u16x2 nk = __builtin_elementwise_min(__builtin_elementwise_sub_sat(Tm, U(Mc)), one_o);    // 1: suppressed
+        const u16x2 ns = __builtin_elementwise_min(__builtin_elementwise_sub_sat(high1, U(Mc)), one_o); // 1: not strong
         const uint32_t k2 = (W32(nk) | W32(ns)) ^ 0x00010001u;  // kept and strong
         return W32(nk) | (k2 + k2);                             // 1 suppressed, 2 strong, 0 weak
     };
@@ -274,6 +298,8 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, LLFE_ST_MINW) void k_stencil_s
     const int img_i = rest / segs;
     const uint8_t *img = bgr + (size_t)img_i * H * W * 3;
     uint8_t *cimg = CLS ? cls + (size_t)img_i * H * W : nullptr;
+    // the image's class map as a buffer (H * W < 2^31 bytes: valid_dims)
+    const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(cimg, (short)0, CLS ? H * W : 0, 0x00020000);
     const int ya = seg * seg_rows, yb = min(H, ya + seg_rows);
     const int x = strip * kStripW - kHalo + 4 * lane;  // the lane's first column
     const bool out_lane = lane >= 2 && lane < 2 + kLanesOut && x < W;
@@ -309,93 +335,135 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, LLFE_ST_MINW) void k_stencil_s
 #pragma unroll
     for (int k = 0; k < 11; k++) k11[k] = prm.k11[k];
 
-    const int t0 = ya - 5, t_end = yb + 5;
-    auto crow = [&](int t) { return clampi(t, 0, H - 1); };
-    auto loadrow = [&](int t) { return reflect101(crow(t) + 2, H); };
-    // gray ring: rows reflect101(c - 2 .. c + 1) of the blur row c = crow(t) entering next
-    const int c0 = crow(t0);
-    uint32_t g0 = gray4(load_px(img, reflect101(c0 - 2, H), W, x, fast, coff));
-    uint32_t g1 = gray4(load_px(img, reflect101(c0 - 1, H), W, x, fast, coff));
-    uint32_t g2 = gray4(load_px(img, reflect101(c0, H), W, x, fast, coff));
-    uint32_t g3 = gray4(load_px(img, reflect101(c0 + 1, H), W, x, fast, coff));
-    Raw q0 = load_px(img, loadrow(t0), W, x, fast, coff);
-    Raw q1 = load_px(img, loadrow(t0 + 1), W, x, fast, coff);
-
-    uint32_t bring[kRing];
-    // magnitude rows t-3 (a), t-2 (m) and whether row m has a candidate in this wave
-    uint32_t a_lo = 0, a_hi = 0, m_lo = 0, m_hi = 0;
-    bool m_cand = false;
-    f32x2 ra[kRing], rb[kRing];
+    // Row steps t (one blurred row enters per step; the loop is unrolled kU = 12 times and
+    // every ring's length divides 12, so each ring slot is a fixed register and no step
+    // moves ring data -- round 4's 11-row unroll shifted its gray / input / magnitude rings
+    // by register moves every step):
+    //   input rows  Q[3]   virtual row v = t + 4 issued at step t, consumed at step t + 2
+    //                      (two loads in flight), slot v % 3
+    //   gray rows   G[6]   virtual row v = t + 2 converted at step t, slot v % 6 (gray row
+    //                      reflect101(v): blur row t reads virtual rows t - 2 .. t + 2)
+    //   blurred     bring[6]: row t, slot t % 6 (read back to row t - 5); CV_32F row pass
+//               ra / rb[12]: row t, slot t % 12 (the column pass reads rows t - 10 .. t)
+    //   magnitude   Mlo / Mhi / Mc[3]: row t - 1 (computed at step t), slot t % 3
+    // Steps t0 - 6, t0 - 5 only issue loads, t0 - 4 .. t0 - 1 also convert gray rows; from
+    // max(t0, 0) on a step computes its blurred row.  REPLICATE of the blurred image: rows
+    // t >= H copy row t - 1; rows -5 .. -1 (the first segment) are filled with row 0 when it
+    // is computed, at step 0, before anything reads them.
+    constexpr int kU = 12;
+    const int t0 = ya - 5, t_end = yb + 5, ts = t0 - 6, tf = max(t0, 0);
+    const int tb0 = ts >= 0 ? ts - ts % kU : -(((-ts) + kU - 1) / kU) * kU;  // floor to a multiple of kU
+    Raw Q[3];
+    uint32_t G[6], bring[6], Mlo[3], Mhi[3];
+    bool Mc[3];
+    f32x2 ra[kU], rb[kU];
 #pragma unroll
-    for (int k = 0; k < kRing; k++) {
-        bring[k] = 0;
-        ra[k] = rb[k] = f32x2{0.0f, 0.0f};
+    for (int k = 0; k < kU; k++) ra[k] = rb[k] = f32x2{0.0f, 0.0f};
+#pragma unroll
+    for (int k = 0; k < 6; k++) G[k] = bring[k] = 0;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        Q[k] = Raw{0u, 0u, 0u};
+        Mlo[k] = Mhi[k] = 0;
+        Mc[k] = false;
     }
     uint32_t lsum = 0, lcnt = 0;
 
-    for (int tb = t0; tb < t_end; tb += kRing) {
+    for (int tb = tb0; tb < t_end; tb += kU) {
 #pragma unroll
-        for (int k = 0; k < kRing; k++) {
+        for (int k = 0; k < kU; k++) {
             const int t = tb + k;
-            if (t < t_end) {  // (no break: the loop must unroll so ring slots are registers)
-            // ---- blur row crow(t) enters
-            const Raw raw = q0;
-            q0 = q1;
-            q1 = load_px(img, loadrow(t + 2), W, x, fast, coff);
-            const uint32_t g4 = gray4(raw);
-            uint32_t B = blur4(g0, g1, g2, g3, g4);
-            if (crow(t + 1) != crow(t)) {
-                g0 = g1;
-                g1 = g2;
-                g2 = g3;
-                g3 = g4;
+            if (t >= ts && t < t_end) {  // (no break: the loop must unroll so ring slots are registers)
+            ST_MARK(load);
+            if (t + 2 < t_end) Q[(k + 2) % 3] = load_px(img, reflect101(t + 4, H), W, x, fast, coff);
+            if (t >= ts + 2) {
+                ST_MARK(gray);
+                uint32_t g = gray4(Q[k % 3]);
+                ST_PIN(g);
+                G[(k + 2) % 6] = g;
             }
+            if (t >= tf) {
+            // ---- blurred row t: computed (0 <= t < H) or REPLICATE'd (t >= H)
+            ST_MARK(blur5);
+            uint32_t B = blur4(G[(k + 4) % 6], G[(k + 5) % 6], G[k % 6], G[(k + 1) % 6], G[(k + 2) % 6]);
+            ST_PIN(B);
+            ST_MARK(edge);
             if (edge) {  // REPLICATE the blurred image beyond columns 0 / W-1
+                ST_RARE();
                 const uint32_t bl = byte_of(__builtin_amdgcn_readlane(B, max(lane0, 0) & 63), 0) * 0x01010101u;
                 const uint32_t br = byte_of(__builtin_amdgcn_readlane(B, min(laneW, 63) & 63), (W - 1 - xw0) & 3) * 0x01010101u;
                 B = (B & ~(rep_l | rep_r)) | (bl & rep_l) | (br & rep_r);
             }
-            bring[k] = B;
-            if (SHD) rowpass4(B, k11, ra[k], rb[k]);
-            if (CLS) {
+            if (t >= H) {  // (t >= 0 here)
+                ST_RARE();
+                B = bring[(k + 5) % 6];
+            }
+            bring[k % 6] = B;
+            if (t == 0 && t0 < 0) {  // rows -5 .. -1 of the first segment
+                ST_RARE();
+#pragma unroll
+                for (int j = 1; j <= 5; j++) bring[(k + 6 - j) % 6] = B;
+            }
+            ST_MARK(gauss_row);
+            if (SHD) {
+                rowpass4(B, k11, ra[k], rb[k]);  // (of the copied row past H: the same values)
+                ST_PIN(ra[k]);
+                ST_PIN(rb[k]);
+                if (t == 0 && t0 < 0) {
+                    ST_RARE();
+#pragma unroll
+                    for (int j = 1; j <= 5; j++) {
+                        ra[(k + kU - j) % kU] = ra[k];
+                        rb[(k + kU - j) % kU] = rb[k];
+                    }
+                }
+            }
+            if (CLS && t >= ya) {
                 // ---- magnitude row t-1 from blurred rows t-2, t-1, t
+                ST_MARK(sobel);
                 uint32_t lo, hi;
-                const bool cand = sobel4(bring[(k + kRing - 2) % kRing], bring[(k + kRing - 1) % kRing], B, lo, hi);
+                const bool cand = sobel4(bring[(k + 4) % 6], bring[(k + 5) % 6], B, lo, hi);
+                ST_PIN(lo);
+                ST_PIN(hi);
                 const bool row_in = (unsigned)(t - 1) < (unsigned)H;
-                const uint32_t b_lo = row_in ? (lo & in_lo) : 0u, b_hi = row_in ? (hi & in_hi) : 0u;
+                Mlo[k % 3] = row_in ? (lo & in_lo) : 0u;
+                Mhi[k % 3] = row_in ? (hi & in_hi) : 0u;
+                Mc[k % 3] = cand && row_in;
                 // ---- NMS of row t-2 from magnitude rows t-3, t-2, t-1 (class 1 for the
                 // whole row when no pixel of the wave's row is a candidate)
                 const int yn = t - 2;
+                ST_MARK(nms);
                 if (yn >= ya && yn < yb) {
+                    const int ia = (k + 1) % 3, im = (k + 2) % 3, ib = k % 3;
                     uint32_t o = 0x01010101u;
-                    if (m_cand) o = nms4(a_lo, a_hi, m_lo, m_hi, b_lo, b_hi);
-                    uint8_t *dst = cimg + ((size_t)yn * W + x);
+                    if (Mc[im]) o = nms4(Mlo[ia], Mhi[ia], Mlo[im], Mhi[im], Mlo[ib], Mhi[ib]);
+                    ST_PIN(o);
+                    ST_MARK(store);
                     if (out_fast) {
-                        __builtin_nontemporal_store(o, (uint32_t *)dst);
+                        // buffer store: row offset yn * W in an SGPR, the lane's column x in a
+                        // VGPR that never changes -- no per-lane 64-bit address per step
+                        __builtin_amdgcn_raw_buffer_store_b32(o, crs, (uint32_t)x, yn * W, 2 /* nt */);
                     } else if (out_lane) {
+                        uint8_t *const dst = cimg + ((size_t)yn * W + x);
 #pragma unroll
                         for (int j = 0; j < 4; j++)
                             if (x + j < W) dst[j] = (uint8_t)(o >> (8 * j));
                     }
                 }
-                a_lo = m_lo;
-                a_hi = m_hi;
-                m_lo = b_lo;
-                m_hi = b_hi;
-                m_cand = cand && row_in;
             }
+            ST_MARK(gauss_col);
             if (SHD) {
                 // ---- Gauss11 column pass of row t-5, mean, mask, masked sum / count
                 const int yg = t - 5;
                 if (yg >= ya && yg < yb) {
-                    const int kc = (k + kRing - 5) % kRing;
+                    const int kc = (k + kU - 5) % kU;
                     const f32x2 w5 = {k11[5], k11[5]};
                     // (the symmetric pairs summed first: the packed adds then never feed the
                     // next instruction, which on gfx950 costs an s_nop)
                     f32x2 pa[5], pb[5];
 #pragma unroll
                     for (int d = 1; d <= 5; d++) {
-                        const int kp = (kc + d) % kRing, kq = (kc + kRing - d) % kRing;
+                        const int kp = (kc + d) % kU, kq = (kc + kU - d) % kU;
                         pa[d - 1] = ra[kp] + ra[kq];
                         pb[d - 1] = rb[kp] + rb[kq];
                     }
@@ -411,20 +479,25 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, LLFE_ST_MINW) void k_stencil_s
                     // [2^23, 2^24)), so the low 16 bits of the sum are the mean; then two
                     // pixels per u16 pair: mask = min(sat(mean - (b + 1)), 1) (b + 2 <= mean),
                     // sum += b . mask and count += 1 . mask by v_dot2_u32_u16
+                    ST_PIN(s01);
+                    ST_PIN(s23);
+                    ST_MARK(mean_mask_sum);
                     const f32x2 two23 = {8388608.0f, 8388608.0f};
                     // (ring pairs, and so s01 / s23 here, hold columns (c0, c2) and (c1, c3))
                     const f32x2 q01 = s01 + two23, q23 = s23 + two23;
                     const uint32_t mean01 = __builtin_amdgcn_perm(__float_as_uint(q01.y), __float_as_uint(q01.x), 0x05040100u);
                     const uint32_t mean23 = __builtin_amdgcn_perm(__float_as_uint(q23.y), __float_as_uint(q23.x), 0x05040100u);
-                    const uint32_t bw = bring[kc];
+                    const uint32_t bw = bring[(k + 1) % 6];  // row t - 5
                     const u16x2 one = {1, 1};
                     const u16x2 b01 = U(__builtin_amdgcn_perm(0u, bw, 0x0c020c00u));  // bytes 0, 2
                     const u16x2 b23 = U(__builtin_amdgcn_perm(0u, bw, 0x0c030c01u));  // bytes 1, 3
-                    uint32_t m01 = W32(__builtin_elementwise_min(__builtin_elementwise_sub_sat(U(mean01), b01 + one), one));
-                    uint32_t m23 = W32(__builtin_elementwise_min(__builtin_elementwise_sub_sat(U(mean23), b23 + one), one));
+                    const u16x2 one_o = U(opaque_ones());
+                    uint32_t m01 = W32(__builtin_elementwise_min(__builtin_elementwise_sub_sat(U(mean01), b01 + one), one_o));
+                    uint32_t m23 = W32(__builtin_elementwise_min(__builtin_elementwise_sub_sat(U(mean23), b23 + one), one_o));
                     // halo lanes are dropped after the loop; only border waves have output
                     // lanes with columns past W
                     if (edge) {
+                        ST_RARE();
                         m01 &= in_02;
                         m23 &= in_13;
                     }
@@ -434,6 +507,8 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, LLFE_ST_MINW) void k_stencil_s
                     lcnt = __builtin_amdgcn_udot2(U(m23), one, lcnt, false);
                 }
             }
+            }  // t >= tf
+            ST_MARK(step_end);
             }
         }
     }

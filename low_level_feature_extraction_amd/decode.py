@@ -14,6 +14,7 @@ above ``MAX_PIXELS`` (cv2's CV_IO_MAX_IMAGE_PIXELS, 2^30) fail like cv2.imdecode
 from __future__ import annotations
 
 import io
+import threading as _threading
 
 import numpy as np
 
@@ -78,35 +79,34 @@ def _image_size(b):
     return h.value, w.value
 
 
-
-_PIL_LIMIT_LOCK = None
+# Serialises _pillow_open: warnings.catch_warnings saves / restores the process-global
+# filter list and the retry below swaps Image.MAX_IMAGE_PIXELS, so two decode threads
+# inside it at once could leave either changed.  Image.open only parses the header.
+_PIL_OPEN_LOCK = _threading.Lock()
 
 
 def _pillow_open(Image, image_bytes: bytes):
     """Image.open under cv2.imdecode's size limit (MAX_PIXELS) instead of Pillow's
-    decompression-bomb guard (2 x MAX_IMAGE_PIXELS, ~179 MP by default), without changing
-    that process-global guard for other Pillow users: the warning between the two Pillow
-    limits is suppressed locally, and only an image Pillow refuses outright is opened again
-    with the limit raised for that one call (under a lock, restored afterwards)."""
-    import threading
+    decompression-bomb guard (2 x MAX_IMAGE_PIXELS, ~179 MP by default), leaving that
+    process-global guard and the warning filters as they were: the warning between the
+    two Pillow limits is suppressed locally, and only an image Pillow refuses outright is
+    opened again with the limit raised for that one call.  All of it under one lock, so
+    concurrent decode threads neither interleave the filter save / restore nor see each
+    other's raised limit."""
     import warnings
 
-    global _PIL_LIMIT_LOCK
-    with warnings.catch_warnings():
+    with _PIL_OPEN_LOCK, warnings.catch_warnings():
         warnings.simplefilter("ignore", Image.DecompressionBombWarning)
         try:
             return Image.open(io.BytesIO(image_bytes))
         except Image.DecompressionBombError:
             pass
-        if _PIL_LIMIT_LOCK is None:
-            _PIL_LIMIT_LOCK = threading.Lock()
-        with _PIL_LIMIT_LOCK:
-            old = Image.MAX_IMAGE_PIXELS
-            Image.MAX_IMAGE_PIXELS = MAX_PIXELS  # (the MAX_PIXELS check of the caller still applies)
-            try:
-                return Image.open(io.BytesIO(image_bytes))
-            finally:
-                Image.MAX_IMAGE_PIXELS = old
+        old = Image.MAX_IMAGE_PIXELS
+        Image.MAX_IMAGE_PIXELS = MAX_PIXELS  # (the MAX_PIXELS check of the caller still applies)
+        try:
+            return Image.open(io.BytesIO(image_bytes))
+        finally:
+            Image.MAX_IMAGE_PIXELS = old
 
 
 def decode_bgr(image_bytes: bytes) -> np.ndarray:
@@ -160,7 +160,7 @@ def decode_bgr(image_bytes: bytes) -> np.ndarray:
 # the end-to-end bound, so decoding fans out over a thread pool (Pillow's codecs release
 # the GIL) and writes straight into the NHWC batch that goes to the device.
 _POOL = None
-_POOL_LOCK = None
+_POOL_LOCK = _threading.Lock()
 
 
 def usable_cores() -> int:
@@ -194,12 +194,9 @@ def default_decode_threads() -> int:
 
 
 def _pool(workers=None):
-    global _POOL, _POOL_LOCK
-    import threading
+    global _POOL
     from concurrent.futures import ThreadPoolExecutor
 
-    if _POOL_LOCK is None:
-        _POOL_LOCK = threading.Lock()
     with _POOL_LOCK:
         want = workers or default_decode_threads()
         if _POOL is None or _POOL._max_workers != want:

@@ -145,3 +145,28 @@ def test_decode_ignores_pillow_bomb_limit(monkeypatch):
         warnings.simplefilter("error")
         assert decode.decode_bgr(buf.getvalue()).shape == (60, 70, 3)
     assert Image.MAX_IMAGE_PIXELS == 3000
+
+
+def test_pillow_bomb_guard_untouched_by_concurrent_decodes():
+    """decode_many over bomb-sized images (Pillow fallback path: GIF headers of
+    100 MP, between Pillow's warning and error limits, and 225 MP, above its error limit but
+    below cv2's 2^30) on the decode pool leaves Image.MAX_IMAGE_PIXELS and the process's
+    warning filters exactly as they were."""
+    import struct
+    import warnings
+
+    from PIL import Image
+
+    from low_level_feature_extraction_amd import decode
+
+    def gif(w, h):  # header + one truncated frame: open() parses it, load() fails
+        b = b"GIF89a" + struct.pack("<HHBBB", w, h, 0x80, 0, 0) + b"\x00\x00\x00\xff\xff\xff"
+        return b + b"," + struct.pack("<HHHHB", 0, 0, w, h, 0) + b"\x02\x02\x44\x01\x00;"
+
+    filters0 = list(warnings.filters)
+    limit0 = Image.MAX_IMAGE_PIXELS
+    blobs = [gif(10000, 10000), gif(15000, 15000)] * 4
+    out = decode.decode_many(blobs, workers=4)
+    assert all(isinstance(o, decode.DecodeError) for o in out)  # truncated frames
+    assert Image.MAX_IMAGE_PIXELS == limit0
+    assert warnings.filters == filters0

@@ -186,6 +186,25 @@ def test_n_colors_parameter(backend, orc):
             assert delta_e_matched(r.centers_rgb, centers) <= 2.5
 
 
+def test_n_colors_below_five_on_cell_tables(backend, orc):
+    """K in {1, 2, 3, 4} on a photo-class 1080p image: its cube table has >= 8192 cubes, so
+    both k-means++ and Lloyd take the 4 x 8 x 8 cell path with unused centres (the -inf
+    margins / +inf forms of centres k >= K), compared with the oracle on the k-means bar
+    (the served tests only reach the cell path at K = 5)."""
+    x = synth.synth_numpy(1, 1080, 1920, seed=91, kind="photo")[None]
+    noise = orc.numpy_noise(1080 * 1920, 7)[None]
+    for k in (1, 2, 3, 4):
+        r = backend.process(x, ("colors",), seed=3, noise=noise, n_colors=k)[0]
+        centers, counts, nu, comp = orc.dominant_colors(x[0], noise[0], k, orc.image_rng_state(3, 0))
+        assert nu > 300_000  # photo class: ~34k occupied 4 x 4 x 4 cubes, >= the cell path's 8192
+        assert r.n_unique == nu and len(r.centers_rgb) == len(centers) == k
+        if k == 1:  # no k-means (color_extractor.py:185-186): the first unique colour
+            assert np.array_equal(np.asarray(r.centers_rgb), np.asarray(centers))
+            continue
+        assert int(np.sum(r.counts)) == nu
+        kmeans_bar.check(r.centers_rgb, r.counts, r.compactness, centers, counts, comp, nu, tag=f"cells-K{k}")
+
+
 @pytest.mark.parametrize("k", [6, 8, 12, 32])
 def test_n_colors_above_five_vs_oracle(backend, orc, k):
     """K = min(n_colors, U) > 5 runs the general-K kernel (kmeans_big.hip): same attempts

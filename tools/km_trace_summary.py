@@ -28,7 +28,8 @@ def main():
     dh = a.T[19].astype(np.uint64) if a.shape[1] >= 20 else z.astype(np.uint64)
     ok = it > 1
     pp = (tpp - t0) / 100.0
-    ll = (tll - tpp) / 100.0
+    tl0 = a.T[20] if a.shape[1] >= 23 and (a.T[20] > 0).any() else tpp  # Lloyd start (split launches)
+    ll = (tll - tl0) / 100.0
     cp = (t1 - tll) / 100.0
     ph = U > 300000
     for name, m in [("photo", ph & ok), ("ui", ~ph & ok)]:
@@ -45,6 +46,35 @@ def main():
             bins = np.stack([((dh[m] >> np.uint64(8 * b)) & np.uint64(255)).astype(np.int64) for b in range(8)], 1)
             print("      iterations by largest centre move [<.25 <.5 <1 <2 <4 <8 <16 >=16]:",
                   np.round(bins.mean(0), 2).tolist(), f"; iters max {it[m].max()}")
+    # slot gaps per phase: one interval per attempt and CU; the gap after an attempt ends
+    # is the wait until the next attempt starts on the same CU (two workgroup slots per
+    # CU), and the idle share is the slot time not covered by attempts over the phase's span
+    def cu_of(h, x):
+        return x * 1000 + ((h >> 13) & 7) * 100 + ((h >> 12) & 1) * 16 + ((h >> 8) & 15)
+
+    split = a.shape[1] >= 23 and (a.T[20] > 0).any()
+    phases = [("k-means++", t0, tpp, cu_of(hw, xcc))]
+    if split:
+        tls, hw2, xcc2 = a.T[20], a.T[21], a.T[22]
+        phases.append(("Lloyd", tls, t1, cu_of(hw2, xcc2)))
+    else:
+        phases = [("attempt", t0, t1, cu_of(hw, xcc))]
+    for name, s0, s1, cus in phases:
+        m = it > 1 if name != "attempt" else np.ones_like(it, bool)
+        gaps = []
+        for c in np.unique(cus[m]):
+            sel = m & (cus == c)
+            st, en = np.sort(s0[sel]), s1[sel]
+            for e in en:
+                k = np.searchsorted(st, e)
+                if k < len(st):
+                    gaps.append((st[k] - e) / 100.0)
+        span = (s1[m].max() - s0[m].min()) / 100.0
+        slots = 2 * len(np.unique(cus[m]))
+        idle = 1 - ((s1[m] - s0[m]) / 100.0).sum() / (slots * span)
+        g = np.array(gaps) if gaps else np.zeros(1)
+        print(f"{name:9s} span {span / 1e3:.2f} ms over {slots} slots: idle share {idle:.3f}; gap after an attempt"
+              f" median {np.median(g):.1f} us, mean {g.mean():.1f}, p90 {np.percentile(g, 90):.1f}")
     dur = (t1 - t0) / 100.0
     cu = xcc * 1000 + ((hw >> 13) & 7) * 100 + ((hw >> 12) & 1) * 16 + ((hw >> 8) & 15)
     busy = {}
