@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define LLFE_ABI_VERSION 2
+#define LLFE_ABI_VERSION 3
 /* most k-means centres per image (extract_colors(n_colors=...) accepts 1 .. LLFE_MAX_COLORS) */
 #define LLFE_MAX_COLORS 32
 
@@ -98,6 +98,16 @@ typedef struct {
     int64_t shape_offset;
     int32_t n_shapes;
     int32_t n_contours;        /* external contours before the area >= 100 filter */
+    /* the reference-shaped summaries, made on the host half of the call in C (no Python):
+     * extract_colors' palette rules on the centres / counts above (color_extractor.py:
+     * 231-284: most frequent first, '#rrggbb', '#ffffff' / '#000000' dropped, primary, three
+     * accents, background by the primary's luminance, is_light_color :67-71) and
+     * analyze_shadow_level's level (shadow pyc @L21-31) */
+    char primary[8];           /* NUL-terminated; "" when colors were not requested */
+    char background[8];        /* "#FFFFFF" or "#000000" (the reference's upper case) */
+    char accent[3][8];
+    int32_t shadow_level;      /* 0 Low, 1 Moderate, 2 High; -1 when shadows were not requested */
+    int32_t pad2_;
 } llfe_image_result;
 
 typedef struct {
@@ -116,6 +126,17 @@ typedef struct {
     double total_ms;
     double bytes;  /* algorithmic HBM bytes attributed to those launches */
 } llfe_kernel_stat;
+
+/* one k-means attempt of the last llfe_process_batch (diagnostics, llfe_kmeans_attempts):
+ * cv2.kmeans' attempt a (color_extractor.py:192-196) -- its k-means++ centres, the centres
+ * and cluster sizes after Lloyd, the Lloyd iterations and the compactness */
+typedef struct {
+    float pp_centers[5][3];
+    float centers[5][3];
+    int32_t counts[5];
+    int32_t iters;
+    double compactness;
+} llfe_kmeans_attempt;
 
 /* ---- context ---------------------------------------------------------- */
 int llfe_init(int device, llfe_ctx **out);
@@ -263,6 +284,15 @@ int llfe_color_unique(llfe_ctx *ctx, const llfe_batch *batch, uint64_t seed, uin
 int llfe_kmeans(llfe_ctx *ctx, const uint32_t *keys, int64_t key_stride, const int64_t *n_points, int32_t n,
                 int32_t n_colors, uint64_t seed, int64_t index_base, llfe_image_result *results,
                 llfe_stream stream);
+/* extract_colors' palette rules alone (color_extractor.py:231-284; host, no context):
+ * k centres (RGB u8) and counts in k-means order -> r's primary / background / accent, as
+ * llfe_process_batch fills them (the other fields of r are left as they are). */
+int llfe_palette_rules(const uint8_t *centers_rgb, const int32_t *counts, int32_t k, llfe_image_result *r);
+/* Diagnostics: the 10 attempt records (llfe_kmeans_attempt) of each of the first n images
+ * of the last chunk of the last llfe_process_batch on this context (n <= its size), for
+ * n_colors <= 5 (the cube-table k-means), into out[n * 10] (host).  Replaces nothing in the
+ * reference: cv2.kmeans only returns the best attempt (color_extractor.py:194). */
+int llfe_kmeans_attempts(llfe_ctx *ctx, int32_t n, llfe_kmeans_attempt *out);
 /* Pillow Image.resize(size, LANCZOS, box) on u8 HWC (image_processor.py:221-224).
  * box may be NULL (whole image). src/dst device. */
 int llfe_resize_lanczos_pil(llfe_ctx *ctx, const uint8_t *src, int32_t h, int32_t w, int32_t ch, uint8_t *dst,

@@ -65,6 +65,11 @@ class LlfeImageResult(C.Structure):
         ("shape_offset", C.c_int64),
         ("n_shapes", C.c_int32),
         ("n_contours", C.c_int32),
+        ("primary", C.c_char * 8),
+        ("background", C.c_char * 8),
+        ("accent", (C.c_char * 8) * 3),
+        ("shadow_level", C.c_int32),
+        ("pad2_", C.c_int32),
     ]
 
 
@@ -102,6 +107,16 @@ class LlfeKernelStat(C.Structure):
     ]
 
 
+class LlfeKmeansAttempt(C.Structure):
+    _fields_ = [
+        ("pp_centers", (C.c_float * 3) * 5),
+        ("centers", (C.c_float * 3) * 5),
+        ("counts", C.c_int32 * 5),
+        ("iters", C.c_int32),
+        ("compactness", C.c_double),
+    ]
+
+
 # every symbol declared in include/llfe.h, with its ctypes signature
 _vp, _i32, _i64, _u32, _u64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint32, C.c_uint64
 SIGNATURES = {
@@ -135,6 +150,8 @@ SIGNATURES = {
     "llfe_shadow_stats": (C.c_int, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _vp]),
     "llfe_color_unique": (C.c_int, [_vp, C.POINTER(LlfeBatch), _u64, _vp, _vp, _vp]),
     "llfe_kmeans": (C.c_int, [_vp, _vp, _i64, _vp, _i32, _i32, _u64, _i64, _vp, _vp]),
+    "llfe_kmeans_attempts": (C.c_int, [_vp, _i32, _vp]),
+    "llfe_palette_rules": (C.c_int, [_vp, _vp, _i32, _vp]),
     "llfe_resize_lanczos_pil": (C.c_int, [_vp, _vp, _i32, _i32, _i32, _vp, _i32, _i32, _vp, _vp]),
     "llfe_reduce_pil": (C.c_int, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp]),
     "llfe_thumbnail_size": (C.c_int, [_i32, _i32, _i32, _i32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),

@@ -22,6 +22,9 @@ from . import _lib as L
 FEATURE_BITS = {"colors": L.FEATURE_COLORS, "shapes": L.FEATURE_SHAPES, "shadows": L.FEATURE_SHADOWS}
 
 
+SHADOW_LEVELS = ("Low", "Moderate", "High")  # llfe_image_result.shadow_level 0 / 1 / 2
+
+
 def feature_mask(features) -> int:
     m = 0
     for f in features:
@@ -46,6 +49,10 @@ class ImageFeatures:
     n_contours: int = 0
     width: int = 0
     height: int = 0
+    # made in C on the host half of collect / process (llfe_image_result): extract_colors'
+    # palette (primary, background, [3 accents]) and analyze_shadow_level's level
+    palette: tuple | None = None
+    shadow_level: str | None = None
 
 
 def _torch():
@@ -304,6 +311,17 @@ class Backend:
         nu, comp = R["n_unique"].tolist(), R["compactness"].tolist()
         ssum, scnt = R["shadow_sum"].tolist(), R["shadow_count"].tolist()
         off, nsh, ncont = R["shape_offset"].tolist(), R["n_shapes"].tolist(), R["n_contours"].tolist()
+        pal = [None] * n
+        if mask & L.FEATURE_COLORS and n:
+            def strs(f, shape):  # char[8] fields (numpy: 8 x S1) -> NUL-stripped bytes
+                return np.ascontiguousarray(R[f]).view("S8").reshape(shape).tolist()
+
+            pr, bg, ac = strs("primary", n), strs("background", n), strs("accent", (n, 3))
+            pal = [(p.decode(), b.decode(), [a[0].decode(), a[1].decode(), a[2].decode()])
+                   for p, b, a in zip(pr, bg, ac)]
+        lv = [None] * n
+        if mask & L.FEATURE_SHADOWS and n:
+            lv = [SHADOW_LEVELS[v] for v in R["shadow_level"].tolist()]
         recs = []
         if mask & L.FEATURE_SHAPES and n:
             tot = max(o + c for o, c in zip(off, nsh))
@@ -316,7 +334,8 @@ class Backend:
         ws = w if isinstance(w, list) else [w] * n
         hs = h if isinstance(h, list) else [h] * n
         out = [ImageFeatures(cen[i, :ncol[i]], cnt[i, :ncol[i]], nu[i], comp[i], ssum[i], scnt[i],
-                             recs[off[i]:off[i] + nsh[i]] if recs else [], ncont[i], ws[i], hs[i]) for i in range(n)]
+                             recs[off[i]:off[i] + nsh[i]] if recs else [], ncont[i], ws[i], hs[i], pal[i], lv[i])
+               for i in range(n)]
         return out
 
     # ------------------------------------------------------------------ async batches
@@ -519,6 +538,24 @@ class Backend:
             centers = np.array([[r.centers_rgb[j][c] for c in range(3)] for j in range(k)], np.uint8).reshape(-1, 3)
             out.append((centers, np.array([r.counts[j] for j in range(k)], np.int64), float(r.compactness)))
         return out
+
+    def kmeans_attempts(self, n):
+        """Diagnostics (llfe_kmeans_attempts): the 10 k-means attempts of each of the first n
+        images of the last process() chunk -> list of n lists of dicts (pp_centers, centers
+        float32 K x 3 before the uint8 truncation, counts, iters, compactness)."""
+        out = (L.LlfeKmeansAttempt * max(n * 10, 1))()
+        self._call("llfe_kmeans_attempts", n, out)
+        recs = []
+        for i in range(n):
+            row = []
+            for a in range(10):
+                r = out[i * 10 + a]
+                row.append({"pp_centers": np.array([[r.pp_centers[k][j] for j in range(3)] for k in range(5)], np.float32),
+                            "centers": np.array([[r.centers[k][j] for j in range(3)] for k in range(5)], np.float32),
+                            "counts": np.array(list(r.counts), np.int64), "iters": int(r.iters),
+                            "compactness": float(r.compactness)})
+            recs.append(row)
+        return recs
 
     def resize_lanczos_pil(self, image, out_w, out_h, box=None):
         """Pillow LANCZOS resize of one H x W x C uint8 image (torch GPU tensor or numpy)."""

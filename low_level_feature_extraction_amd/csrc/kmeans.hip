@@ -1336,6 +1336,8 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
 
     }  // k-means++
     if (tid == 0) o->t_pp = wall_clock64();
+    // (diagnostics, llfe_kmeans_attempts: the k-means++ centres of the attempt)
+    if (tid < kMaxK * 3) (&o->pp_centers[0][0])[tid] = sm.cc[tid / 3][tid % 3];
     }  // kPhase & 1
     if (kPhase == 1) {
         // hand the attempt to the Lloyd launch: chosen centres, Sum |p|^2, counters

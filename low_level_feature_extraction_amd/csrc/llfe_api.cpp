@@ -219,6 +219,7 @@ struct Work {
     DevBuf<int32_t> d_ncubes, d_ncells;
     DevBuf<int64_t> d_nuniq;
     DevBuf<KmeansAttemptOut> d_att;
+    int km_n = 0, km_colors = 0;  // images / n_colors of the last k-means launch (d_att)
     DevBuf<KmeansImageOut> d_kout;
     DevBuf<long long> d_index;  // per-image global indices of the chunk (llfe_batch.indices)
     // GPU contours (contours_gpu.hip); capacities grow when a pass overflows them
@@ -660,6 +661,8 @@ int kmeans_stage(llfe_ctx *ctx, Work &W, const uint32_t *keys, int64_t key_strid
     HIPCHK(ctx, W.d_kscratch.ensure((size_t)n * kAttempts * sstride));
     HIPCHK(ctx, W.d_att.ensure((size_t)n * kAttempts));
     HIPCHK(ctx, W.d_kout.ensure(n));
+    W.km_n = n;
+    W.km_colors = n_colors;
     // per-image cv::RNG state = splitmix64(seed + global index) is derived on the device
     TIMED(ctx, s, "k_kmeans", 0,
           launch_kmeans(keys, key_stride, d_nuniq, n, n_colors, seed, index, W.d_order.p, W.d_kscratch.p,
@@ -687,6 +690,53 @@ int kmeans_stage(llfe_ctx *ctx, Work &W, const uint32_t *keys, int64_t key_strid
     return LLFE_OK;
 }
 
+// ColorExtractor.is_light_color (color_extractor.py:67-71), in the reference's order
+bool is_light_color(int r, int g, int b) {
+    const double R = r / 255.0, G = g / 255.0, B = b / 255.0;
+    return 0.2126 * R + 0.7152 * G + 0.0722 * B > 0.6;
+}
+
+// extract_colors' palette rules (color_extractor.py:231-284) on r's centres and counts:
+// frequency order (stable on ties; np.argsort(-counts)'s tie order is host-dependent in the
+// reference), hex, '#ffffff' / '#000000' dropped, primary, three accents
+// (padded with the last, or the primary), background by the primary's luminance
+void fill_palette(llfe_image_result &r) {
+    const int K = r.n_colors;
+    int ord[kMaxColors];
+    for (int i = 0; i < K; i++) ord[i] = i;
+    if (K > 1) std::stable_sort(ord, ord + K, [&](int a, int b) { return r.counts[a] > r.counts[b]; });
+    char hex[kMaxColors][8];
+    int rgb[kMaxColors][3];
+    int nh = 0;
+    for (int i = 0; i < K; i++) {
+        const uint8_t *c = r.centers_rgb[ord[i]];
+        if ((c[0] == 255 && c[1] == 255 && c[2] == 255) || (c[0] == 0 && c[1] == 0 && c[2] == 0)) continue;
+        std::snprintf(hex[nh], 8, "#%02x%02x%02x", c[0], c[1], c[2]);
+        rgb[nh][0] = c[0], rgb[nh][1] = c[1], rgb[nh][2] = c[2];
+        nh++;
+    }
+    if (nh == 0) {  // nothing left: the contrasting colour for white (:245-256)
+        const char *bg = is_light_color(255, 255, 255) ? "#000000" : "#FFFFFF";
+        std::snprintf(r.primary, 8, "%s", bg);
+        std::snprintf(r.background, 8, "%s", bg);
+        for (auto &a : r.accent) std::snprintf(a, 8, "%s", bg);
+        return;
+    }
+    std::snprintf(r.primary, 8, "%s", hex[0]);
+    int na = 0;
+    for (int i = 1; i < nh && na < 3; i++)
+        if (std::strcmp(hex[i], hex[0]) != 0) std::snprintf(r.accent[na++], 8, "%s", hex[i]);
+    for (; na < 3; na++) std::snprintf(r.accent[na], 8, "%s", na ? r.accent[na - 1] : r.primary);
+    std::snprintf(r.background, 8, "%s", is_light_color(rgb[0][0], rgb[0][1], rgb[0][2]) ? "#000000" : "#FFFFFF");
+}
+
+// ShadowAnalyzer.analyze_shadow_level's decision (shadow pyc @L22-31): 0 Low, 1 Moderate, 2 High
+int32_t shadow_level(uint64_t sum, uint64_t count) {
+    if (count == 0) return 0;
+    const double avg_darkness = 255.0 - (double)sum / (double)count;
+    return avg_darkness < 30 ? 0 : (avg_darkness < 60 ? 1 : 2);
+}
+
 void fill_color_result(const KmeansImageOut &k, llfe_image_result &r) {
     r.n_colors = k.k;
     for (int c = 0; c < kMaxColors; c++) {
@@ -695,6 +745,7 @@ void fill_color_result(const KmeansImageOut &k, llfe_image_result &r) {
     }
     r.n_unique = k.n_unique;
     r.compactness = k.compactness;
+    fill_palette(r);
 }
 
 bool valid_dims(int n, int h, int w) { return n >= 0 && h > 0 && w > 0 && (int64_t)h * w < (1LL << 31); }
@@ -928,9 +979,11 @@ int finish_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, int i0, 
     for (int i = 0; i < n; i++) {
         llfe_image_result &r = results[i0 + i];
         std::memset(&r, 0, sizeof r);
+        r.shadow_level = -1;
         if (want_shd) {
             r.shadow_sum = sh[i];
             r.shadow_count = sh[n + i];
+            r.shadow_level = shadow_level(r.shadow_sum, r.shadow_count);
         }
     }
     if (want_shp && ctx->slot_gpu_ct[slot]) {
@@ -1562,7 +1615,46 @@ int llfe_kmeans(llfe_ctx *ctx, const uint32_t *keys, int64_t key_stride, const i
     HIPCHK(ctx, hipStreamSynchronize(s));
     for (int i = 0; i < n; i++) {
         std::memset(&results[i], 0, sizeof(llfe_image_result));
+        results[i].shadow_level = -1;
         fill_color_result(ctx->h_kout.p[i], results[i]);
+    }
+    return LLFE_OK;
+}
+
+int llfe_palette_rules(const uint8_t *centers_rgb, const int32_t *counts, int32_t k, llfe_image_result *r) {
+    if (!r || k < 0 || k > kMaxColors || (k > 0 && (!centers_rgb || !counts))) return LLFE_ERR_INVALID;
+    r->n_colors = k;
+    for (int i = 0; i < k; i++) {
+        r->counts[i] = counts[i];
+        for (int j = 0; j < 3; j++) r->centers_rgb[i][j] = centers_rgb[3 * i + j];
+    }
+    fill_palette(*r);
+    return LLFE_OK;
+}
+
+int llfe_kmeans_attempts(llfe_ctx *ctx, int32_t n, llfe_kmeans_attempt *out) {
+    if (!ctx || !out || n < 0) return LLFE_ERR_INVALID;
+    if (ctx->any_inflight())
+        return ctx->fail(LLFE_ERR_INVALID, "llfe_kmeans_attempts with submitted batches not yet collected");
+    Work &W = ctx->ws[0];
+    if (n > W.km_n) return ctx->fail(LLFE_ERR_INVALID, "the last k-means launch had %d images", W.km_n);
+    if (W.km_colors > kMaxK) return ctx->fail(LLFE_ERR_UNSUPPORTED, "attempt records only for n_colors <= %d", kMaxK);
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    std::vector<KmeansAttemptOut> a((size_t)n * kAttempts);
+    HIPCHK(ctx, hipDeviceSynchronize());
+    HIPCHK(ctx, hipMemcpy(a.data(), W.d_att.p, sizeof(KmeansAttemptOut) * a.size(), hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < a.size(); i++) {
+        llfe_kmeans_attempt &r = out[i];
+        std::memset(&r, 0, sizeof r);
+        for (int k = 0; k < kMaxK; k++) {
+            for (int j = 0; j < 3; j++) {
+                r.pp_centers[k][j] = a[i].pp_centers[k][j];
+                r.centers[k][j] = a[i].centers[k][j];
+            }
+            r.counts[k] = a[i].counts[k];
+        }
+        r.iters = a[i].iters;
+        r.compactness = a[i].compactness;
     }
     return LLFE_OK;
 }

@@ -158,6 +158,7 @@ struct KmeansAttemptOut {
     uint64_t qtot;             // sum of |p|^2 over the image's colours (k-means++ -> Lloyd launch)
     uint64_t t_lstart;         // Lloyd launch: start of the attempt's workgroup
     uint32_t hw_id2, xcc_id2;  // ... and its placement
+    float pp_centers[kMaxK][3];  // the k-means++ centres (cube-table path; llfe_kmeans_attempts)
 };
 
 struct KmeansImageOut {

@@ -36,17 +36,23 @@ def shapes_result(r) -> dict:
 
 
 def assemble(r, features: Iterable[str]) -> dict:
-    from .color_extractor import ColorExtractor
+    """The reference-shaped results of one image.  The palette strings and the shadow level
+    come made from libllfe's host half (C, off the GIL; llfe_image_result), so this only
+    builds the objects; records without them (none from the batch entry points) take the
+    Python rules."""
+    from .color_extractor import ColorExtractor, palette_features
 
     out = {}
     for f in features:
         f = getattr(f, "value", f)
         if f == "colors":
-            out["colors"] = ColorExtractor._palette(r.centers_rgb, r.counts)
+            p = getattr(r, "palette", None)
+            out["colors"] = palette_features(*p) if p else ColorExtractor._palette(r.centers_rgb, r.counts)
         elif f == "shapes":
             out["shapes"] = shapes_result(r)
         elif f == "shadows":
-            out["shadows"] = {"shadow_level": shadow_level(r.shadow_sum, r.shadow_count)}
+            lv = getattr(r, "shadow_level", None)
+            out["shadows"] = {"shadow_level": lv if lv is not None else shadow_level(r.shadow_sum, r.shadow_count)}
     return out
 
 

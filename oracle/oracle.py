@@ -49,6 +49,7 @@ def lib():
         L = C.CDLL(_LIB_PATH)
         u8p = C.POINTER(C.c_uint8)
         L.orc_kmeans.restype = C.c_double
+        L.orc_kmeans_ex.restype = C.c_double
         L.orc_contour_area.restype = C.c_double
         L.orc_arc_length.restype = C.c_double
         L.orc_convex_hull_area.restype = C.c_double
@@ -324,6 +325,30 @@ def kmeans(data, K, attempts=10, max_count=200, eps=0.2, rng_state=0xFFFFFFFF):
     c = lib().orc_kmeans(_p(data), N, K, max_count, C.c_double(eps), attempts, C.c_uint64(rng_state),
                          _p(labels), _p(centers), _p(counts), _p(iters))
     return c, labels, centers, counts, iters
+
+
+def kmeans_attempts(keys, K, rng_state, exact_sums=False, attempts=10):
+    """Every attempt of cv2.kmeans on the unique colours ``keys`` (packed RGB, np.unique
+    order; llfe_oracle.c orc_kmeans_ex): per attempt its k-means++ centres, final centres
+    (float32, before astype(uint8)), counters, compactness, iterations and the centres after
+    each Lloyd update.  exact_sums: the device's exact int64 cluster sums instead of
+    OpenCV's sequential float32 ones (kmeans.hip / DESIGN.md §5)."""
+    keys = np.asarray(keys, np.uint32)
+    data = np.ascontiguousarray(np.stack([(keys >> 16) & 255, (keys >> 8) & 255, keys & 255], -1), np.float32)
+    N = data.shape[0]
+    labels = np.empty(N, np.int32)
+    best = np.empty((K, 3), np.float32)
+    bcnt = np.empty(K, np.int32)
+    iters = np.empty(attempts, np.int32)
+    pp = np.zeros((attempts, K, 3), np.float32)
+    cen = np.zeros((attempts, K, 3), np.float32)
+    cnt = np.zeros((attempts, K), np.int32)
+    comp = np.zeros(attempts, np.float64)
+    it = np.full((attempts, 100, K, 3), np.nan, np.float32)
+    c = lib().orc_kmeans_ex(_p(data), N, K, 200, C.c_double(0.2), attempts, C.c_uint64(rng_state), int(exact_sums),
+                            _p(labels), _p(best), _p(bcnt), _p(iters), _p(pp), _p(cen), _p(cnt), _p(comp), _p(it))
+    return {"compactness": c, "labels": labels, "centers": best, "counts": bcnt, "iters": iters, "pp": pp,
+            "att_centers": cen, "att_counts": cnt, "att_compactness": comp, "iter_centers": it}
 
 
 def dominant_colors(bgr, noise=None, n_colors=5, rng_state=0xFFFFFFFF):

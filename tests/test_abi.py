@@ -39,9 +39,10 @@ def test_library_exports_every_header_symbol():
 
 
 def test_abi_version_and_struct_sizes():
-    assert L.lib().llfe_abi_version() == 2
+    assert L.lib().llfe_abi_version() == 3
     assert C.sizeof(L.LlfeBatch) == 56
-    assert C.sizeof(L.LlfeImageResult) == 280
+    assert C.sizeof(L.LlfeImageResult) == 328
+    assert C.sizeof(L.LlfeKmeansAttempt) == 152
     assert C.sizeof(L.LlfeShape) == 40
     assert C.sizeof(L.LlfeKernelStat) == 56
     assert C.sizeof(L.LlfeImageDesc) == 40
@@ -71,6 +72,7 @@ def test_struct_layout_matches_header_via_compiler(tmp_path):
         "llfe_shape": [f for f, _ in L.LlfeShape._fields_ if not f.endswith("_")],
         "llfe_kernel_stat": [f for f, _ in L.LlfeKernelStat._fields_],
         "llfe_image_desc": [f for f, _ in L.LlfeImageDesc._fields_],
+        "llfe_kmeans_attempt": [f for f, _ in L.LlfeKmeansAttempt._fields_],
     }
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "llfe.h"', "int main(void){"]
     for st, fs in fields.items():
@@ -86,7 +88,8 @@ def test_struct_layout_matches_header_via_compiler(tmp_path):
         st, f, v = ln.split()
         got[(st, f)] = int(v)
     pystructs = {"llfe_batch": L.LlfeBatch, "llfe_image_result": L.LlfeImageResult, "llfe_shape": L.LlfeShape,
-                 "llfe_kernel_stat": L.LlfeKernelStat, "llfe_image_desc": L.LlfeImageDesc}
+                 "llfe_kernel_stat": L.LlfeKernelStat, "llfe_image_desc": L.LlfeImageDesc,
+                 "llfe_kmeans_attempt": L.LlfeKmeansAttempt}
     for st, cls in pystructs.items():
         assert got[(st, "sizeof")] == C.sizeof(cls), st
         for f in fields[st]:
