@@ -191,13 +191,17 @@ def e2e_host(be, imgs_dev, feats, steps, seed, index_base):
                       f"H2D + full GPU path per batch, two batches in flight (llfe_submit_batch / llfe_collect_batch)"}
 
 
-def e2e_png(be, B, H, W, feats, steps, distinct, seed, fmt="PNG", decode_steps=2):
+def e2e_png(be, B, H, W, feats, steps, distinct, seed, fmt="PNG", decode_steps=2, contours=None):
     """End-to-end from encoded bytes (PNG, or JPEG quality 85):
     host decode on the decode thread pool into pinned host batches, driven through the
     same serving loop as `value` (llfe_submit_batch / llfe_collect_batch, two batches in
     flight), so decoding batch k + 1 overlaps batch k's H2D and kernels.  Beside it, the
     warm decode-only rate of the same threads: the e2e value is decode-bound when it is
-    within 10 % of that rate.  Reported beside `value`, never as it."""
+    within 10 % of that rate.  `split` times the leg's phases on the serving thread (waiting
+    for the decode of the next batch, submit, collect) and the decode producer itself, and
+    the host contour pool's busy share.  contours: the contour mode for the leg ("gpu": the
+    host cores all go to decoding; None: the context's).  Reported beside `value`, never
+    as it."""
     from concurrent.futures import ThreadPoolExecutor
 
     import torch
@@ -217,32 +221,61 @@ def e2e_png(be, B, H, W, feats, steps, distinct, seed, fmt="PNG", decode_steps=2
     for k in range(decode_steps):
         decode.decode_batch(blobs, bufs[k % 3], threads)
     dec_rate = B * decode_steps / (time.perf_counter() - t)
+    mode0 = be.contour_mode()
+    if contours:
+        be.set_contour_mode(contours)
     be.process(bufs[0][:2], feats, seed=seed)  # warm the host-input path
+    dec_s = []
+
+    def produce(buf):
+        t = time.perf_counter()
+        out = decode.decode_batch(blobs, buf, threads)
+        dec_s.append(time.perf_counter() - t)
+        return out
+
+    wait = sub = col = 0.0
+    be.host_contour_stats(reset=True)
     with ThreadPoolExecutor(max_workers=1) as prod:
         t0 = time.perf_counter()
-        fut = prod.submit(decode.decode_batch, blobs, bufs[0], threads)
+        fut = prod.submit(produce, bufs[0])
         pending = []
         for k in range(steps):
+            ta = time.perf_counter()
             batch = fut.result()
+            tb = time.perf_counter()
             # decode batch k + 1 (started before batch k is submitted, so the decode threads
             # never wait on the submission) while batch k - 1 is collected: buffer
             # (k + 1) % 3 last held batch k - 2, collected one step earlier
             if k + 1 < steps:
-                fut = prod.submit(decode.decode_batch, blobs, bufs[(k + 1) % 3], threads)
+                fut = prod.submit(produce, bufs[(k + 1) % 3])
             pending.append(be.submit(batch, feats, seed=seed + k))
+            tc = time.perf_counter()
             if len(pending) == 2:
                 be.collect(pending.pop(0))
+            wait, sub, col = wait + tb - ta, sub + tc - tb, col + time.perf_counter() - tc
+        tc = time.perf_counter()
         while pending:
             be.collect(pending.pop(0))
+        col += time.perf_counter() - tc
         dt = time.perf_counter() - t0
+    hc = be.host_contour_stats(reset=True)
+    if contours:
+        be.set_contour_mode(mode0)
     value = B * steps / dt
     mb = sum(len(p) for p in blobs_d) / distinct / 2**20
     bound = (f"host decode: e2e is {value / dec_rate:.2f} of the {threads}-thread decode-only rate"
              if value >= 0.9 * dec_rate else
              f"not decode alone: e2e is {value / dec_rate:.2f} of the decode-only rate (GPU path / host contour pool)")
+    split = {"ms_per_step": round(dt / steps * 1e3, 2),
+             "decode_ms_per_batch_in_leg": round(sum(dec_s) / len(dec_s) * 1e3, 2),
+             "decode_ms_per_batch_alone": round(B / dec_rate * 1e3, 2),
+             "serving_thread_ms_per_step": {"wait_for_decode": round(wait / steps * 1e3, 2),
+                                            "submit": round(sub / steps * 1e3, 2),
+                                            "collect": round(col / steps * 1e3, 2)},
+             "host_contour_busy": round(hc["busy_ms"] / 1e3 / dt, 3)}
     return {"value": round(value, 2), "unit": "images/s", "decode_threads": threads,
             "decode_only": round(dec_rate, 2), "decode_ms_per_image_per_thread": round(threads / dec_rate * 1e3, 2),
-            "codecs": decode.decoder_info(), "contours": be.contour_mode(), "bound": bound,
+            "codecs": decode.decoder_info(), "contours": contours or mode0, "bound": bound, "split": split,
             "sample": f"{steps} x {B} {fmt}-encoded {W}x{H} synthetic images ({distinct} distinct, {mb:.2f} MiB each), "
                       f"decoded on the host (libllfe {fmt} decoder, cv2.imdecode IMREAD_COLOR semantics) into pinned "
                       f"host batches, then the full GPU path incl. H2D, two batches in flight; decode-only: "
@@ -311,6 +344,8 @@ def main():
     ap.add_argument("--seed", type=int, default=2025)
     ap.add_argument("--e2e-png-steps", type=int, default=6, help="0 disables the PNG end-to-end line")
     ap.add_argument("--e2e-jpeg-steps", type=int, default=6, help="0 disables the JPEG end-to-end line")
+    ap.add_argument("--e2e-alt-contours", type=int, default=1,
+                    help="1: also run the JPEG leg with the other contour mode (host <-> gpu)")
     ap.add_argument("--e2e-at-scale", action="store_true",
                     help="also run the e2e lines when WORLD_SIZE > 1 (off by default: every rank would pin "
                          "~10 GB of host batches and decode on its 1/N core share while the scaling run "
@@ -612,6 +647,13 @@ def main():
     barrier()
     if args.e2e_jpeg_steps > 0:
         e2e_j = all_ranks(e2e_png(be, B, H, W, feats, args.e2e_jpeg_steps, 8, args.seed, fmt="JPEG"), args.e2e_jpeg_steps)
+    e2e_j_alt = None
+    if args.e2e_jpeg_steps > 0 and args.e2e_alt_contours and "shapes" in feats:
+        # the same JPEG leg with the other contour mode: whether the host contour pool's
+        # share of the cores is what keeps the leg below its decode-only rate
+        alt = "gpu" if be.contour_mode() == "host" else "host"
+        e2e_j_alt = all_ranks(e2e_png(be, B, H, W, feats, args.e2e_jpeg_steps, 8, args.seed, fmt="JPEG",
+                                      contours=alt), args.e2e_jpeg_steps)
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -665,6 +707,7 @@ def main():
         "e2e_host": e2e_h,
         "e2e_png": e2e,
         "e2e_jpeg": e2e_j,
+        "e2e_jpeg_other_contour_mode": e2e_j_alt,
     }
     print(json.dumps(out))
     if dist is not None:

@@ -184,7 +184,10 @@ struct KmSmem {
     unsigned long long pD[kParts];       // per partition: sum of D (the winning trial)
     unsigned long long pex[3];
     unsigned long long S[3];
-    uint32_t pbase[kParts + 1];          // first sorted key of each partition
+    uint32_t pbase[kParts + 1];          // first sorted key of each partition (np.unique index)
+    uint32_t kbeg[kParts];               // ... its address in the key array (= pbase, or the
+                                         // segmented layout's hist prefix, KmeansCubes::part_hist)
+    uint32_t kfirst, klast;              // addresses of the first / last key in np.unique order
     int pj[3];
     int icc[kMaxK][3];                   // chosen centres (integer colours)
     unsigned long long sel_pts;          // colours the selection scans read
@@ -348,6 +351,39 @@ __device__ __forceinline__ int dmin_chosen(int x, int y, int z, const ICent &ch,
     return d;
 }
 
+// Partition p's keys in np.unique order, in the key array (wave 0): sm.pbase[p] (np.unique
+// index of its first key, and the total at kParts), sm.kbeg[p] (its first key's address:
+// = pbase when the keys are contiguous, the prefix of the partitions' pixel counts `hist`
+// in k_uq_part's segmented layout), sm.kfirst / sm.klast (addresses of the first and the
+// last key).  Returns, in every lane, the address of np.unique index `idx` (< total).
+__device__ __forceinline__ uint32_t key_layout(KmSmem &sm, const uint32_t *__restrict__ part_uq,
+                                               const uint32_t *__restrict__ hist, uint32_t idx) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t v = part_uq[lane], hv = hist ? hist[lane] : v;
+    uint32_t x = v, hx = hv;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off), hy = __shfl_up(hx, off);
+        if (lane >= off) x += y, hx += hy;
+    }
+    const uint32_t pb = x - v, kb = hx - hv;
+    sm.pbase[lane] = pb;
+    sm.kbeg[lane] = kb;
+    if (lane == 63) sm.pbase[kParts] = x;
+    const unsigned long long ne = __ballot(v != 0);  // (total > 0: some partition is not empty)
+    const int p0 = ne ? (int)__builtin_ctzll(ne) : 0, pl = ne ? 63 - (int)__builtin_clzll(ne) : 0;
+    const uint32_t kf = __shfl(kb, p0), kl = __shfl(kb, pl) + __shfl(v, pl) - 1;
+    if (lane == 0) {
+        sm.kfirst = kf;
+        sm.klast = kl;
+    }
+    // the partition of idx: the last one starting at or before it (empty ones share the
+    // next one's start and precede it)
+    const unsigned long long le = __ballot(pb <= idx);
+    const int P = le ? 63 - (int)__builtin_clzll(le) : 0;
+    return __shfl(kb, P) + (idx - __shfl(pb, P));
+}
+
 // Inlined into the k-means++ kernel (its only caller): 105 VGPRs and no scratch; as a
 // call the kernel needed 128 VGPRs with 2 spilled (LLFE_KM_PP_CALL=1 keeps the call for
 // measurements).
@@ -358,34 +394,25 @@ __device__ __forceinline__
 #endif
 void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, int K, uint64_t &rng,
                          const CubeEnt *__restrict__ ctab, int C, const CellEnt *__restrict__ ltab, int L,
-                         const uint32_t *__restrict__ part_uq, unsigned long long &bytes,
-                         uint32_t &pp_pts, uint32_t &pp_sel, uint64_t &t_sel) {
+                         const uint32_t *__restrict__ part_uq, const uint32_t *__restrict__ hist,
+                         unsigned long long &bytes, uint32_t &pp_pts, uint32_t &pp_sel, uint64_t &t_sel) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint32_t c0 = cvrng_next(rng) % (uint32_t)N;  // (every thread advances its rng copy)
     if (wid == 0) {
-        const uint32_t v = part_uq[lane];
-        uint32_t x = v;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t y = __shfl_up(x, off);
-            if (lane >= off) x += y;
+        const uint32_t a0 = key_layout(sm, part_uq, hist, c0);
+        if (lane == 0) {
+            const uint32_t q0 = pts[a0];
+            sm.icc[0][0] = unpack_r(q0);
+            sm.icc[0][1] = unpack_g(q0);
+            sm.icc[0][2] = unpack_b(q0);
         }
-        sm.pbase[lane] = x - v;
-        if (lane == 63) sm.pbase[kParts] = x;
     }
     if (tid == 0) {
         sm.fail_pts = 0;
         sm.sel_pts = 0;
         sm.qtot = 0;
     }
-    if (tid < kMaxK * 3) (&sm.icc[0][0])[tid] = 0;
-    {
-        const uint32_t q0 = pts[cvrng_next(rng) % (uint32_t)N];
-        if (tid == 0) {
-            sm.icc[0][0] = unpack_r(q0);
-            sm.icc[0][1] = unpack_g(q0);
-            sm.icc[0][2] = unpack_b(q0);
-        }
-    }
+    if (tid >= 64 && tid < 64 + (kMaxK - 1) * 3) (&sm.icc[1][0])[tid - 64] = 0;
     unsigned long long sum0 = 0, qacc = 0;  // qacc: sum |p|^2 over the lane's cubes
     for (int kk = 0; kk < K; kk++) {
         __syncthreads();
@@ -444,9 +471,9 @@ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, int K, uint64
                 uint32_t ca[3], cb2[3], cw0[3], cw1[3];  // partition [a, b), this wave's steps [w0, w1)
     #pragma unroll
                 for (int j = 0; j < 3; j++) {
-                    const int P = sm.pj[j];
-                    ca[j] = P >= 0 ? sm.pbase[P] : 0u;
-                    cb2[j] = P >= 0 ? sm.pbase[P + 1] : 0u;
+                    const int P = sm.pj[j];  // (its keys: addresses [kbeg, kbeg + count))
+                    ca[j] = P >= 0 ? sm.kbeg[P] : 0u;
+                    cb2[j] = P >= 0 ? sm.kbeg[P] + (sm.pbase[P + 1] - sm.pbase[P]) : 0u;
                     const uint32_t A = ca[j] & ~3u;
                     const uint32_t nst = (cb2[j] - A + STEP - 1) / STEP;   // steps over [A, b)
                     const uint32_t per = (nst + KW - 1) / KW;               // steps per wave (<= kSelSteps)
@@ -503,9 +530,10 @@ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, int K, uint64
                     const int j = wid;
                     const double pj = j == 0 ? p[0] : (j == 1 ? p[1] : p[2]);
                     const int P = sm.pj[j];
-                    int ci = P == -2 ? 0 : N - 1;
+                    // (key addresses; p <= 0: the first key, p beyond the total: the last)
+                    int ci = (int)(P == -2 ? sm.kfirst : sm.klast);
                     if (P >= 0) {
-                        const uint32_t a = sm.pbase[P], b = sm.pbase[P + 1];  // (not ca[j]: no dynamic private indexing)
+                        const uint32_t a = sm.kbeg[P], b = a + (sm.pbase[P + 1] - sm.pbase[P]);  // (not ca[j]: no dynamic private indexing)
                         const uint32_t A = a & ~3u;
                         const uint32_t nst = (b - A + STEP - 1) / STEP, per = (nst + KW - 1) / KW;
                         unsigned long long e = sm.pex[j];
@@ -572,7 +600,7 @@ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, int K, uint64
                             }
                             if (lane == 0) atomicAdd(&sm.sel_pts, (unsigned long long)STEP);
                         }
-                        if (found >= 0) ci = min(found, N - 1);
+                        if (found >= 0) ci = found;  // (inside [a, b))
                     }
                     if (lane == 0) sm.pj[j] = ci;
                 }
@@ -1120,7 +1148,9 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
 
     // ------------------------------------------------ k-means++ (generateCentersPP)
     if (use_cubes) {
-        pp_cubes(sm, pts, N, K, rng, ctab, C, cubes.cells + (size_t)img * cubes.cube_stride, cubes.n_cells[img], cubes.part_uq + (size_t)img * kParts, bytes, pp_pts, pp_sel, t_sel);
+        pp_cubes(sm, pts, N, K, rng, ctab, C, cubes.cells + (size_t)img * cubes.cell_stride, cubes.n_cells[img],
+                 cubes.part_uq + (size_t)img * kParts, cubes.part_hist ? cubes.part_hist + (size_t)img * kParts : nullptr,
+                 bytes, pp_pts, pp_sel, t_sel);
     } else {
     int cur = 0;
     {
@@ -1561,7 +1591,7 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
             // Lloyd iteration 74.5 -> 69.8 us, r4b -- not on a ui image's ~3k cubes)
             if (C >= kCellMinCubes) {
                 const int L = cubes.n_cells[img];
-                const CellEnt *ltab = cubes.cells + (size_t)img * cubes.cube_stride;
+                const CellEnt *ltab = cubes.cells + (size_t)img * cubes.cell_stride;
                 int *ql = sm.cq[wid];
                 int base = __builtin_amdgcn_readfirstlane(grab());
                 int ahead = grab();
@@ -1760,19 +1790,33 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
             const Cent cp = load_centres(sm.cprev);
             double md = -1.0;
             int mi = -1;
-            for (int s = sb; s < se; s++) {
-                const int i0 = s * STEP + lane * 4;
-                for (int jj = 0; jj < 4; jj++) {
-                    const int i = i0 + jj;
-                    if (i >= N) break;
-                    P3 pp = unpack(pts[i]);
-                    float bd;
-                    int l = moved_label(sm, i, label5(pp, cp, bd));
-                    if (l != max_k) continue;
-                    double d = (double)d2(pp.x, pp.y, pp.z, bx, by, bz);
-                    if (md <= d) {
-                        md = d;
-                        mi = i;
+            auto visit = [&](int i) {  // key address i (increasing with the np.unique index)
+                P3 pp = unpack(pts[i]);
+                float bd;
+                int l = moved_label(sm, i, label5(pp, cp, bd));
+                if (l != max_k) return;
+                double d = (double)d2(pp.x, pp.y, pp.z, bx, by, bz);
+                if (md <= d) {
+                    md = d;
+                    mi = i;
+                }
+            };
+            if (kCubes && cubes.part_hist) {
+                // segmented keys: partition by partition, in np.unique order
+                if (wid == 0) (void)key_layout(sm, cubes.part_uq + (size_t)img * kParts,
+                                               cubes.part_hist + (size_t)img * kParts, 0u);
+                __syncthreads();
+                for (int P = 0; P < kParts; P++) {
+                    const int a0 = (int)sm.kbeg[P], a1 = a0 + (int)(sm.pbase[P + 1] - sm.pbase[P]);
+                    for (int i = a0 + tid; i < a1; i += KT) visit(i);
+                }
+            } else {
+                for (int s = sb; s < se; s++) {
+                    const int i0 = s * STEP + lane * 4;
+                    for (int jj = 0; jj < 4; jj++) {
+                        const int i = i0 + jj;
+                        if (i >= N) break;
+                        visit(i);
                     }
                 }
             }
@@ -1962,7 +2006,8 @@ __global__ __launch_bounds__(OT) void k_kmeans_order(const long long *__restrict
 
 __global__ void k_kmeans_finalize(const uint32_t *__restrict__ keys, long long key_stride,
                                   const long long *__restrict__ n_unique, int n, int n_colors,
-                                  const KmeansAttemptOut *__restrict__ att, KmeansImageOut *__restrict__ out) {
+                                  const KmeansAttemptOut *__restrict__ att, KmeansImageOut *__restrict__ out,
+                                  const uint32_t *__restrict__ part_uq, const uint32_t *__restrict__ part_hist) {
     int img = blockIdx.x * blockDim.x + threadIdx.x;
     if (img >= n) return;
     long long N = n_unique[img];
@@ -1976,8 +2021,21 @@ __global__ void k_kmeans_finalize(const uint32_t *__restrict__ keys, long long k
         // or no bincount at all (U == 1, count 1): keep the first min(U, kMaxK)
         // colours in np.unique order
         r.k = (int)min(N, (long long)kMaxK);
+        // (segmented keys: the first keys of the first non-empty partitions)
+        uint32_t P = 0, off = 0, seg = 0, left = part_hist ? part_uq[(size_t)img * kParts] : 0u;
         for (int k = 0; k < r.k; k++) {
-            const uint32_t key = keys[(size_t)img * key_stride + k];
+            uint32_t a = (uint32_t)k;
+            if (part_hist) {
+                while (left == 0) {
+                    seg += part_hist[(size_t)img * kParts + P];
+                    P++;
+                    off = 0;
+                    left = part_uq[(size_t)img * kParts + P];
+                }
+                a = seg + off++;
+                left--;
+            }
+            const uint32_t key = keys[(size_t)img * key_stride + a];
             r.centers_rgb[k][0] = (uint8_t)(key >> 16);
             r.centers_rgb[k][1] = (uint8_t)(key >> 8);
             r.centers_rgb[k][2] = (uint8_t)key;
@@ -2073,7 +2131,8 @@ hipError_t launch_kmeans(const uint32_t *keys, int64_t key_stride, const int64_t
                            cubes);
     }
     hipLaunchKernelGGL(k_kmeans_finalize, dim3((n + 255) / 256), dim3(256), 0, s, keys, (long long)key_stride,
-                       (const long long *)n_unique, n, n_colors, attempts, out);
+                       (const long long *)n_unique, n, n_colors, attempts, out, cubes.part_uq,
+                       cubes.cubes ? cubes.part_hist : nullptr);
     return hipGetLastError();
 }
 

@@ -329,14 +329,18 @@ size_t shadow_tiles(int n, int h, int w) { return stencil_parts(n, h, w); }
 // Images per device pass.  One pass per call when the workspace allows it: a bigger
 // pass amortises the k-means launch's tail (its longest attempts run 100 Lloyd
 // iterations) over more work (512 x 1080p per pass: +10 % images/s over 256).  The
-// workspace is ~16 B per pixel + the 5 MB per-image partition cube and cell tables, held
+// workspace is ~16 B per pixel + the 5 MB per-image partition cube and cell tables + the
+// gathered cube / cell tables (<= 4 MiB + 1 MiB), held
 // within LLFE_WORKSPACE_GB (default 24 GB of the 288 GB of HBM) PER IN-FLIGHT SLOT: every
 // slot of llfe_set_inflight owns one such workspace, so depth 3 takes about 3x the budget.
 int chunk_for(int h, int w) {
     double gb = 24.0;
     if (const char *e = getenv("LLFE_WORKSPACE_GB"); e && atof(e) > 0) gb = atof(e);
-    const double per_image = 16.0 * (double)h * (double)w +
-                             (double)kParts * (kCubesPerPart * sizeof(CubeEnt) + kCellsPerPart * sizeof(CellEnt));
+    const double P = (double)h * (double)w;
+    const double cubes = std::min(P, (double)kMaxCubes), cells = std::min(cubes, (double)kParts * kCellsPerPart);
+    const double per_image = 16.0 * P +  // keys, segments, class map, labels, masks
+                             (double)kParts * (kCubesPerPart * sizeof(CubeEnt) + kCellsPerPart * sizeof(CellEnt)) +
+                             cubes * sizeof(CubeEnt) + cells * sizeof(CellEnt);  // the gathered tables
     const double n = gb * 1e9 / per_image;
     return (int)std::max(1.0, std::min(n, (double)kMaxKmeansBatch));
 }
@@ -608,18 +612,23 @@ void grow_contour_caps(Work &W, int n, int h, int w, const CtCounters &ct) {
     if (ct.flags & kCtOverflowShapes) m.shapes = up(m.shapes, d.shapes, (int64_t)ct.shapes);
 }
 
+// contiguous_keys: also gather each image's unique keys into W.d_keys in np.unique order
+// (llfe_color_unique's output, the general-K k-means); otherwise they stay where k_uq_part
+// wrote them (W.d_raw, partition R at the prefix of the partition pixel counts) and the cube
+// k-means reads them there (KmeansCubes::part_hist)
 int color_stage(llfe_ctx *ctx, Work &W, const uint8_t *img, const int8_t *noise, int n, int h, int w, uint64_t seed,
-                ImgIndex index, hipStream_t s) {
+                ImgIndex index, bool contiguous_keys, hipStream_t s) {
     // unique colours -> W.d_keys (sorted, key_stride) + cube table for k-means
     const int64_t P = (int64_t)h * w;
     const int64_t key_stride = (std::max<int64_t>(P, 1) + 3) & ~int64_t(3);
     const int64_t cube_stride = std::min<int64_t>(key_stride, kMaxCubes);
+    const int64_t cell_stride = std::min<int64_t>(cube_stride, (int64_t)kParts * kCellsPerPart);
     HIPCHK(ctx, W.d_raw.ensure((size_t)n * key_stride));
     HIPCHK(ctx, W.d_keys.ensure((size_t)n * key_stride));
     HIPCHK(ctx, W.d_segcubes.ensure((size_t)n * kParts * kCubesPerPart));
     HIPCHK(ctx, W.d_cubes.ensure((size_t)n * cube_stride));
     HIPCHK(ctx, W.d_segcells.ensure((size_t)n * kParts * kCellsPerPart));
-    HIPCHK(ctx, W.d_cells.ensure((size_t)n * cube_stride));
+    HIPCHK(ctx, W.d_cells.ensure((size_t)n * cell_stride));
     HIPCHK(ctx, W.d_ncells.ensure(n));
     HIPCHK(ctx, W.d_pmeta.ensure((size_t)n * kParts * 4));
     HIPCHK(ctx, W.d_nuniq.ensure(n));
@@ -648,7 +657,8 @@ int color_stage(llfe_ctx *ctx, Work &W, const uint8_t *img, const int8_t *noise,
                          W.d_segcells.p, uq, cc, cl, s));
     TIMED(ctx, s, "k_uq_gather", 0,
           launch_uq_gather(W.d_raw.p, n, key_stride, hist, uq, cc, cl, W.d_segcubes.p, W.d_segcells.p, W.d_keys.p,
-                           W.d_cubes.p, W.d_cells.p, cube_stride, W.d_nuniq.p, W.d_ncubes.p, W.d_ncells.p, s));
+                           W.d_cubes.p, W.d_cells.p, cube_stride, cell_stride, W.d_nuniq.p, W.d_ncubes.p, W.d_ncells.p,
+                           contiguous_keys, s));
     return LLFE_OK;
 }
 
@@ -775,6 +785,7 @@ int enqueue_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_
                want_shd = features & LLFE_FEATURE_SHADOWS;
     const int64_t P = (int64_t)h * w;
     const int64_t key_stride = (std::max<int64_t>(P, 1) + 3) & ~int64_t(3);
+    const int n_colors = b->n_colors ? b->n_colors : kMaxK;
     const uint8_t *img;
     const int8_t *noise;
     int rc = stage_input(ctx, W, b, i0, n, &img, &noise, s);
@@ -796,7 +807,7 @@ int enqueue_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_
     // colour front (unique colours), then shapes / shadows (on the other stream), then
     // k-means
     if (want_col) {
-        rc = color_stage(ctx, W, img, noise, n, h, w, seed, index, col_s);
+        rc = color_stage(ctx, W, img, noise, n, h, w, seed, index, /*contiguous_keys=*/n_colors > kMaxK, col_s);
         if (rc) return rc;
     }
     // d_shadow / d_bits of this workspace may still be in the previous chunk's D2H
@@ -844,10 +855,14 @@ int enqueue_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_
         HIPCHK(ctx, hipEventRecord(ctx->mask_done[slot], s));
     }
     if (want_col) {
+        // (n_colors <= 5: the keys in k_uq_part's segmented layout, W.d_raw)
+        const bool seg = n_colors <= kMaxK;
         const KmeansCubes cubes{W.d_cubes.p, std::min<int64_t>(key_stride, kMaxCubes), W.d_ncubes.p,
-                                W.d_pmeta.p + (size_t)2 * n * kParts, W.d_cells.p, W.d_ncells.p};
-        rc = kmeans_stage(ctx, W, W.d_keys.p, key_stride, W.d_nuniq.p, n, b->n_colors ? b->n_colors : kMaxK, seed,
-                          index, cubes, col_s);
+                                W.d_pmeta.p + (size_t)2 * n * kParts, W.d_cells.p, W.d_ncells.p,
+                                std::min<int64_t>(std::min<int64_t>(key_stride, kMaxCubes), (int64_t)kParts * kCellsPerPart),
+                                seg ? W.d_pmeta.p : nullptr};
+        rc = kmeans_stage(ctx, W, seg ? W.d_raw.p : W.d_keys.p, key_stride, W.d_nuniq.p, n, n_colors, seed, index,
+                          cubes, col_s);
         if (rc) return rc;
         HIPCHK(ctx, ctx->h_kout_s[slot].ensure(n));
         HIPCHK(ctx, hipMemcpyAsync(ctx->h_kout_s[slot].p, W.d_kout.p, sizeof(KmeansImageOut) * n,
@@ -1003,10 +1018,11 @@ int finish_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, int i0, 
                 ub += 4.0 * (double)ko[i].n_unique;
             }
             ctx->prof.add_bytes("k_kmeans", kb);
-            // the unique keys: written once (k_uq_part) and read once (k_uq_gather), 8U of
-            // SURVEY.md 8d's colour pass
+            // the unique keys: written once (k_uq_part, 4U of SURVEY.md 8d's 8U) and read
+            // once -- by k_uq_gather when it makes them contiguous (n_colors > 5), else by
+            // k-means itself where k_uq_part wrote them (its passes' 4U bytes)
             ctx->prof.add_bytes("k_uq_part", ub);
-            ctx->prof.add_bytes("k_uq_gather", ub);
+            if ((b->n_colors ? b->n_colors : kMaxK) > kMaxK) ctx->prof.add_bytes("k_uq_gather", ub);
         }
     }
     return LLFE_OK;
@@ -1583,7 +1599,7 @@ int llfe_color_unique(llfe_ctx *ctx, const llfe_batch *b, uint64_t seed, uint32_
     ImgIndex index;
     rc = chunk_index(ctx, W, b, 0, n, s, &index);
     if (rc) return rc;
-    rc = color_stage(ctx, W, img, noise, n, h, w, seed, index, s);
+    rc = color_stage(ctx, W, img, noise, n, h, w, seed, index, /*contiguous_keys=*/true, s);
     if (rc) return rc;
     HIPCHK(ctx, hipMemcpy2DAsync(keys, sizeof(uint32_t) * P, W.d_keys.p, sizeof(uint32_t) * key_stride,
                                  sizeof(uint32_t) * P, n, hipMemcpyDeviceToDevice, s));
@@ -1607,7 +1623,7 @@ int llfe_kmeans(llfe_ctx *ctx, const uint32_t *keys, int64_t key_stride, const i
     Work &W = ctx->ws[0];
     HIPCHK(ctx, W.d_nuniq.ensure(n));
     HIPCHK(ctx, hipMemcpyAsync(W.d_nuniq.p, n_points, sizeof(int64_t) * n, hipMemcpyHostToDevice, s));
-    const KmeansCubes none{nullptr, 0, nullptr, nullptr, nullptr, nullptr};  // plain sweeps over caller-supplied keys
+    const KmeansCubes none{nullptr, 0, nullptr, nullptr, nullptr, nullptr, 0, nullptr};  // plain sweeps over caller-supplied keys
     int rc = kmeans_stage(ctx, W, keys, key_stride, W.d_nuniq.p, n, n_colors, seed, ImgIndex{index_base, nullptr}, none, s);
     if (rc) return rc;
     HIPCHK(ctx, ctx->h_kout.ensure(n));

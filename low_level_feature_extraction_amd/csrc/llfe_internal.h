@@ -202,8 +202,14 @@ struct KmeansCubes {
     int64_t cube_stride;
     const int32_t *n_cubes;
     const uint32_t *part_uq;  // per image: unique colours per red-quarter partition (kParts)
-    const CellEnt *cells;     // per image (cube_stride) cells in partition / cell order
+    const CellEnt *cells;     // per image (cell_stride) cells in partition / cell order
     const int32_t *n_cells;
+    int64_t cell_stride;      // min(cube_stride, kParts * kCellsPerPart): an image has <= 65536 cells
+    // Segmented keys (k_uq_part's layout, no key gather): when part_hist is set, the keys
+    // passed to launch_kmeans hold each image's partitions at the prefix of part_hist (the
+    // partitions' pixel counts: partition R's unique keys at [sum_{r<R} hist_r, + uq_R)),
+    // not contiguously; part_uq gives the unique counts.
+    const uint32_t *part_hist;
 };
 // Unique colours (unique.hip), all per image with stride key_stride (u32 keys):
 //   keys:    pixels -> noised keys into `raw`, partition histogram `hist` (n x 64, zeroed)
@@ -229,8 +235,9 @@ hipError_t launch_uq_part(const uint32_t *seg, int n, int64_t key_stride, int64_
 hipError_t launch_uq_gather(const uint32_t *skeys, int n, int64_t key_stride, const uint32_t *hist, const uint32_t *uq,
                             const uint32_t *cc, const uint32_t *cl, const CubeEnt *seg_cubes,
                             const CellEnt *seg_cells, uint32_t *keys, CubeEnt *cubes, CellEnt *cells,
-                            int64_t cube_stride, int64_t *n_unique, int32_t *n_cubes, int32_t *n_cells,
-                            hipStream_t s);
+                            int64_t cube_stride, int64_t cell_stride, int64_t *n_unique, int32_t *n_cubes,
+                            int32_t *n_cells,
+                            bool copy_keys, hipStream_t s);
 
 // per image: K = min(n_colors, U); attempts run as separate workgroups
 // (ordered largest U first), then a finalize kernel picks the best attempt.

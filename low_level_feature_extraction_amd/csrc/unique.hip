@@ -513,9 +513,11 @@ __global__ __launch_bounds__(UT) void k_uq_part(const uint32_t *__restrict__ seg
     }
 }
 
-// grid (64, n): one workgroup per (partition, image) copies the partition's sorted
-// unique keys, cube entries and cells to their place in the contiguous per-image arrays
-// (a cell's first cube index becomes image-global)
+// grid (64, n): one workgroup per (partition, image) copies the partition's cube entries
+// and cells -- and, with copy_keys, its sorted unique keys -- to their place in the
+// contiguous per-image arrays (a cell's first cube index becomes image-global).  The batch
+// path's k-means reads the keys where k_uq_part wrote them (KmeansCubes::part_hist), so
+// only the small cube / cell tables move: 16 (C + L) instead of 8U + 16 (C + L) bytes.
 constexpr int GT = 256;
 __global__ __launch_bounds__(GT) void k_uq_gather(const uint32_t *__restrict__ skeys, long long key_stride,
                                                   const uint32_t *__restrict__ hist, const uint32_t *__restrict__ uq,
@@ -523,8 +525,9 @@ __global__ __launch_bounds__(GT) void k_uq_gather(const uint32_t *__restrict__ s
                                                   const CubeEnt *__restrict__ seg_cubes,
                                                   const CellEnt *__restrict__ seg_cells, uint32_t *__restrict__ keys,
                                                   CubeEnt *__restrict__ cubes, CellEnt *__restrict__ cells,
-                                                  long long cube_stride, long long *__restrict__ n_unique,
-                                                  int *__restrict__ n_cubes, int *__restrict__ n_cells) {
+                                                  long long cube_stride, long long cell_stride,
+                                                  long long *__restrict__ n_unique,
+                                                  int *__restrict__ n_cubes, int *__restrict__ n_cells, int copy_keys) {
     __shared__ uint32_t sp, su, sc, sl, nu, nc, nl;
     const int R = blockIdx.x, img = blockIdx.y, t = threadIdx.x;
     if (t < 64) {
@@ -552,12 +555,13 @@ __global__ __launch_bounds__(GT) void k_uq_gather(const uint32_t *__restrict__ s
     const uint32_t U = nu, C = nc, L = nl, cbase = sc;
     const uint32_t *sk = skeys + (size_t)img * key_stride + sp;
     uint32_t *ok = keys + (size_t)img * key_stride + su;
-    for (uint32_t i = t; i < U; i += GT) ok[i] = sk[i];
+    if (copy_keys)
+        for (uint32_t i = t; i < U; i += GT) ok[i] = sk[i];
     const CubeEnt *scp = seg_cubes + ((size_t)img * NPART + R) * 4096;
     CubeEnt *oc = cubes + (size_t)img * cube_stride + sc;
     for (uint32_t i = t; i < C; i += GT) oc[i] = scp[i];
     const CellEnt *slp = seg_cells + ((size_t)img * NPART + R) * kCellsPerPart;
-    CellEnt *ol = cells + (size_t)img * cube_stride + sl;
+    CellEnt *ol = cells + (size_t)img * cell_stride + sl;
     for (uint32_t i = t; i < L; i += GT) {
         CellEnt e = slp[i];
         e.first += cbase;
@@ -612,11 +616,12 @@ hipError_t launch_uq_part(const uint32_t *seg, int n, int64_t key_stride, int64_
 hipError_t launch_uq_gather(const uint32_t *skeys, int n, int64_t key_stride, const uint32_t *hist, const uint32_t *uq,
                             const uint32_t *cc, const uint32_t *cl, const CubeEnt *seg_cubes,
                             const CellEnt *seg_cells, uint32_t *keys, CubeEnt *cubes, CellEnt *cells,
-                            int64_t cube_stride, int64_t *n_unique, int32_t *n_cubes, int32_t *n_cells,
-                            hipStream_t s) {
+                            int64_t cube_stride, int64_t cell_stride, int64_t *n_unique, int32_t *n_cubes,
+                            int32_t *n_cells, bool copy_keys, hipStream_t s) {
     hipLaunchKernelGGL(k_uq_gather, dim3(NPART, n), dim3(GT), 0, s, skeys, (long long)key_stride, hist, uq, cc, cl,
-                       seg_cubes, seg_cells, keys, cubes, cells, (long long)cube_stride, (long long *)n_unique,
-                       (int *)n_cubes, (int *)n_cells);
+                       seg_cubes, seg_cells, keys, cubes, cells, (long long)cube_stride, (long long)cell_stride,
+                       (long long *)n_unique,
+                       (int *)n_cubes, (int *)n_cells, copy_keys ? 1 : 0);
     return hipGetLastError();
 }
 
