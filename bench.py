@@ -598,7 +598,13 @@ def main():
         r = roof(name)
         kernels[name] = {"launches": st["launches"], "avg_ms": r["avg_launch_ms"],
                          "share_of_step": round(st["total_ms"] / (dt_kernels * 1e3), 4),
-                         "gbs": r["achieved"] if st["bytes"] else None, "frac": r["frac"] if st["bytes"] else None}
+                         "gbs": r["achieved"] if st["bytes"] else None, "frac": r["frac"] if st["bytes"] else None,
+                         # HBM bytes the PMC counters saw per launch (profiles/traffic_latest.json) over
+                         # the same average duration: beside the algorithmic gbs, so a kernel whose
+                         # algorithmic bytes exceed what it moved (k_kmeans: L2 serves its repeated
+                         # passes) shows both
+                         "pmc_gbs": round(traffic[name] / (r["avg_launch_ms"] * 1e-3) / 1e9, 1)
+                         if traffic.get(name) and r["avg_launch_ms"] > 0 else None}
     # `roofline` is the dominant kernel's (largest total time); k_kmeans' algorithmic
     # bytes are SURVEY.md 8d's 4U per fused multi-attempt pass x (K k-means++ passes + the
     # longest attempt's Lloyd sweeps), k_kmeans_finalize.

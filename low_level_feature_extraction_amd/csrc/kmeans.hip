@@ -28,8 +28,14 @@ namespace llfe {
 namespace {
 
 constexpr int kCellMinCubes = 8192;
+#ifndef LLFE_KM_SPLIT
+#define LLFE_KM_SPLIT 0  // the cube path in two launches (measured slower; kept as a build option)
+#endif
 #ifndef LLFE_KM_LLOYD_QUEUE
-#define LLFE_KM_LLOYD_QUEUE 0  // Lloyd as a work queue too (1) or one workgroup per attempt (0)
+#define LLFE_KM_LLOYD_QUEUE 0  // (split) Lloyd as a work queue too (1) or one workgroup per attempt (0)
+#endif
+#ifndef LLFE_KM_PP_CALL
+#define LLFE_KM_PP_CALL (!LLFE_KM_SPLIT)  // pp_cubes as a call in the one-launch kernel (its register budget)
 #endif  // the sweeps test cells before cubes from this cube count on
 #ifndef LLFE_KM_THREADS
 #define LLFE_KM_THREADS 512
@@ -384,9 +390,9 @@ __device__ __forceinline__ uint32_t key_layout(KmSmem &sm, const uint32_t *__res
     return __shfl(kb, P) + (idx - __shfl(pb, P));
 }
 
-// Inlined into the k-means++ kernel (its only caller): 105 VGPRs and no scratch; as a
-// call the kernel needed 128 VGPRs with 2 spilled (LLFE_KM_PP_CALL=1 keeps the call for
-// measurements).
+// A call in the one-launch kernel (inlined there it spilled 37 VGPRs); inlined into the
+// split build's k-means++ kernel (105 VGPRs, no scratch; as a call that kernel needed 128
+// VGPRs with 2 spilled).
 #if LLFE_KM_PP_CALL
 __device__
 #else
@@ -2085,7 +2091,8 @@ hipError_t launch_kmeans(const uint32_t *keys, int64_t key_stride, const int64_t
     static int slots_pp[64], slots_ll[64];
     const size_t smem = sizeof(KmSmem);
     constexpr bool kLloydQueue = LLFE_KM_LLOYD_QUEUE;
-    const void *plain = (const void *)k_kmeans<false, 3, false>, *pp = (const void *)k_kmeans<true, 1, true>,
+    const void *plain = (const void *)k_kmeans<false, 3, false>,
+               *pp = LLFE_KM_SPLIT ? (const void *)k_kmeans<true, 1, true> : (const void *)k_kmeans<true, 3, false>,
                *lloyd = (const void *)k_kmeans<true, 2, kLloydQueue>;
     int dev = 0;
     {
@@ -2120,6 +2127,11 @@ hipError_t launch_kmeans(const uint32_t *keys, int64_t key_stride, const int64_t
         hipLaunchKernelGGL((k_kmeans<false, 3, false>), dim3(n * kAttempts), dim3(KT), smem, s, keys,
                            (long long)key_stride, (const long long *)n_unique, n_colors, (unsigned long long)seed,
                            index, order, n * kAttempts, nullptr, scratch, (long long)scratch_stride, attempts, cubes);
+    } else if (!LLFE_KM_SPLIT) {
+        // one workgroup per (image, attempt) in LPT order, k-means++ then Lloyd
+        hipLaunchKernelGGL((k_kmeans<true, 3, false>), dim3(n * kAttempts), dim3(KT), smem, s, keys,
+                           (long long)key_stride, (const long long *)n_unique, n_colors, (unsigned long long)seed,
+                           index, order, n * kAttempts, nullptr, nullptr, 0LL, attempts, cubes);
     } else {
         const int tasks = n * kAttempts;
         hipLaunchKernelGGL((k_kmeans<true, 1, true>), dim3(std::min(tasks, slots_pp[dev])), dim3(KT), smem, s, keys,

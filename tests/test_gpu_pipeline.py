@@ -197,10 +197,12 @@ def test_n_colors_below_five_on_cell_tables(backend, orc):
         r = backend.process(x, ("colors",), seed=3, noise=noise, n_colors=k)[0]
         centers, counts, nu, comp = orc.dominant_colors(x[0], noise[0], k, orc.image_rng_state(3, 0))
         assert nu > 300_000  # photo class: ~34k occupied 4 x 4 x 4 cubes, >= the cell path's 8192
-        assert r.n_unique == nu and len(r.centers_rgb) == len(centers) == k
-        if k == 1:  # no k-means (color_extractor.py:185-186): the first unique colour
+        assert r.n_unique == nu and len(r.centers_rgb) == len(centers)
+        if k == 1:  # no k-means (color_extractor.py:185-186): the first unique colours, counts [U, 0, ...]
             assert np.array_equal(np.asarray(r.centers_rgb), np.asarray(centers))
+            assert np.array_equal(np.asarray(r.counts), np.asarray(counts))
             continue
+        assert len(centers) == k
         assert int(np.sum(r.counts)) == nu
         kmeans_bar.check(r.centers_rgb, r.counts, r.compactness, centers, counts, comp, nu, tag=f"cells-K{k}")
 

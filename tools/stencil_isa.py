@@ -3,7 +3,7 @@
 
 Builds stencil_stream.hip with -DLLFE_ST_MARK=1 (stage markers fenced by
 sched_barrier, so no instruction crosses a stage boundary; the counts are those of the
-shipped schedule up to that fencing) and counts, for each of the 11 unrolled row steps
+shipped schedule up to that fencing) and counts, for each of the 12 unrolled row steps
 of the main loop, the VALU instructions (v_*) per stage on the path an interior wave
 takes (12-byte loads, no border REPLICATE, full-width stores), separately for the
 candidate-only blocks (the Canny direction classes and NMS, run only on wave rows with
