@@ -263,12 +263,26 @@ def e2e_png(be, B, H, W, feats, steps, distinct, seed, fmt="PNG", decode_steps=2
         be.set_contour_mode(mode0)
     value = B * steps / dt
     mb = sum(len(p) for p in blobs_d) / distinct / 2**20
-    bound = (f"host decode: e2e is {value / dec_rate:.2f} of the {threads}-thread decode-only rate"
-             if value >= 0.9 * dec_rate else
-             f"not decode alone: e2e is {value / dec_rate:.2f} of the decode-only rate (GPU path / host contour pool)")
+    # what the leg's time went to: its decodes (the producer runs them back to back while
+    # the serving thread submits / collects), the pipeline's fill and drain (the first
+    # batch's decode before any GPU work, the last batches' GPU path and collects after the
+    # last decode), and decode slowed by sharing the cores (host contour pool, driver threads)
+    dec_leg = sum(dec_s) / len(dec_s)
+    decodes_share = steps * dec_leg / dt
+    fill_drain_ms = (dt - steps * dec_leg) * 1e3
+    slow = dec_leg / (B / dec_rate) - 1
+    if decodes_share >= 0.85:
+        bound = (f"host decode: the {threads} decode threads were busy {decodes_share:.2f} of the leg (back to back; "
+                 f"the rest is the pipeline fill / drain, {fill_drain_ms:.0f} ms per {steps}-batch leg); a decode took "
+                 f"{100 * slow:+.0f} % against decode alone (cores shared with the host contour pool and driver "
+                 f"threads); e2e is {value / dec_rate:.2f} of the decode-only rate")
+    else:
+        bound = (f"not decode alone: decodes fill {decodes_share:.2f} of the leg; e2e is {value / dec_rate:.2f} of the "
+                 f"decode-only rate (GPU path / host contour pool)")
     split = {"ms_per_step": round(dt / steps * 1e3, 2),
              "decode_ms_per_batch_in_leg": round(sum(dec_s) / len(dec_s) * 1e3, 2),
              "decode_ms_per_batch_alone": round(B / dec_rate * 1e3, 2),
+             "decodes_share_of_leg": round(decodes_share, 3), "fill_drain_ms_per_leg": round(fill_drain_ms, 1),
              "serving_thread_ms_per_step": {"wait_for_decode": round(wait / steps * 1e3, 2),
                                             "submit": round(sub / steps * 1e3, 2),
                                             "collect": round(col / steps * 1e3, 2)},
@@ -342,8 +356,8 @@ def main():
                          "it does not resize this size: BASELINE configs [3] auto at 1080p, [4] high_quality at 4K)")
     ap.add_argument("--e2e-host-steps", type=int, default=8, help="0 disables the decoded-host-array line")
     ap.add_argument("--seed", type=int, default=2025)
-    ap.add_argument("--e2e-png-steps", type=int, default=6, help="0 disables the PNG end-to-end line")
-    ap.add_argument("--e2e-jpeg-steps", type=int, default=6, help="0 disables the JPEG end-to-end line")
+    ap.add_argument("--e2e-png-steps", type=int, default=8, help="0 disables the PNG end-to-end line")
+    ap.add_argument("--e2e-jpeg-steps", type=int, default=10, help="0 disables the JPEG end-to-end line")
     ap.add_argument("--e2e-alt-contours", type=int, default=1,
                     help="1: also run the JPEG leg with the other contour mode (host <-> gpu)")
     ap.add_argument("--e2e-at-scale", action="store_true",
@@ -453,18 +467,18 @@ def main():
 
     from concurrent.futures import ThreadPoolExecutor
 
-    from low_level_feature_extraction_amd.pipeline import assemble
+    from low_level_feature_extraction_amd.pipeline import assemble_batch
 
     asm_pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="llfe-assemble")
     asm_log = []  # (CPU ms of one batch's assembly)
 
-    def assemble_batch(recs):
+    def assemble_step(recs):
         """The reference-shaped results of one collected batch:
         ColorFeatures by the palette rules (color_extractor.py:231-284), the analyze_shapes
         dict (shape pyc @L184-189) and {"shadow_level": ...} (shadow pyc @L21-31), as
         process_feature_results receives them (utils.py:155-214)."""
         t = time.thread_time()
-        out = [assemble(r, feats) for r in recs]
+        out = assemble_batch(recs, feats)
         asm_log.append((time.thread_time() - t) * 1e3)
         return sum(len(o["shapes"]["shapes"]) for o in out) if "shapes" in feats else 0
 
@@ -479,15 +493,15 @@ def main():
         futs = []
         if not pipelined:
             for k in range(k_steps):
-                futs.append(asm_pool.submit(assemble_batch, be.process(batch, feats, seed=seed0 + k, index_base=base)))
+                futs.append(asm_pool.submit(assemble_step, be.process(batch, feats, seed=seed0 + k, index_base=base)))
         else:
             pending = []
             for k in range(k_steps):
                 pending.append(be.submit(batch, feats, seed=seed0 + k, index_base=base))
                 if len(pending) == be.inflight:
-                    futs.append(asm_pool.submit(assemble_batch, be.collect(pending.pop(0))))
+                    futs.append(asm_pool.submit(assemble_step, be.collect(pending.pop(0))))
             while pending:
-                futs.append(asm_pool.submit(assemble_batch, be.collect(pending.pop(0))))
+                futs.append(asm_pool.submit(assemble_step, be.collect(pending.pop(0))))
         t_last = time.perf_counter()
         shapes = sum(f.result() for f in futs)
         run_steps.tail_ms = (time.perf_counter() - t_last) * 1e3  # assembly left after the last collect
@@ -591,20 +605,28 @@ def main():
             # the HBM fraction of the algorithmic bytes, against HBM peak)
             if r["valu_busy"] > 0.7:
                 r["bound"] = "valu"
+        if traffic.get(name) and avg_ms > 0:  # what the counters saw, beside the algorithmic rate
+            r["hbm_gbs_pmc"] = round(traffic[name] / (avg_ms * 1e-3) / 1e9, 1)
         return r
 
     kernels = {}
     for name, st in stats.items():
         r = roof(name)
+        alg = r["achieved"] if st["bytes"] else None
+        pmc = (round(traffic[name] / (r["avg_launch_ms"] * 1e-3) / 1e9, 1)
+               if traffic.get(name) and r["avg_launch_ms"] > 0 else None)
         kernels[name] = {"launches": st["launches"], "avg_ms": r["avg_launch_ms"],
                          "share_of_step": round(st["total_ms"] / (dt_kernels * 1e3), 4),
-                         "gbs": r["achieved"] if st["bytes"] else None, "frac": r["frac"] if st["bytes"] else None,
-                         # HBM bytes the PMC counters saw per launch (profiles/traffic_latest.json) over
-                         # the same average duration: beside the algorithmic gbs, so a kernel whose
-                         # algorithmic bytes exceed what it moved (k_kmeans: L2 serves its repeated
-                         # passes) shows both
-                         "pmc_gbs": round(traffic[name] / (r["avg_launch_ms"] * 1e-3) / 1e9, 1)
-                         if traffic.get(name) and r["avg_launch_ms"] > 0 else None}
+                         # gbs: the HBM bytes the PMC counters saw per launch (the committed
+                         # profile of this workload, profiles/traffic_latest.json) over the same
+                         # average duration -- what the kernel moved; without a profile, the
+                         # algorithmic rate.  algorithmic_gbs / frac: SURVEY.md 8d's bytes, the
+                         # roofline's definition; a kernel that moves less than its algorithmic
+                         # bytes (k_kmeans: the cube tables stand in for its repeated key passes)
+                         # shows a higher algorithmic than measured rate
+                         "gbs": pmc if pmc is not None else alg,
+                         "gbs_source": "pmc" if pmc is not None else ("algorithmic" if alg is not None else None),
+                         "algorithmic_gbs": alg, "frac": r["frac"] if st["bytes"] else None}
     # `roofline` is the dominant kernel's (largest total time); k_kmeans' algorithmic
     # bytes are SURVEY.md 8d's 4U per fused multi-attempt pass x (K k-means++ passes + the
     # longest attempt's Lloyd sweeps), k_kmeans_finalize.

@@ -16,6 +16,7 @@ from typing import Iterable, List, Optional, Sequence
 import numpy as np
 
 from .backend import Backend, feature_mask  # noqa: F401  (feature_mask validates names)
+from .color_extractor import ColorExtractor, palette_features
 
 
 def shadow_level(mask_sum: int, mask_count: int) -> str:
@@ -35,25 +36,31 @@ def shapes_result(r) -> dict:
             "metadata": {"image_width": r.width, "image_height": r.height}}
 
 
+def _colors_result(r):
+    p = getattr(r, "palette", None)
+    return palette_features(*p) if p else ColorExtractor._palette(r.centers_rgb, r.counts)
+
+
+def _shadows_result(r):
+    lv = getattr(r, "shadow_level", None)
+    return {"shadow_level": lv if lv is not None else shadow_level(r.shadow_sum, r.shadow_count)}
+
+
+_MAKERS = {"colors": _colors_result, "shapes": shapes_result, "shadows": _shadows_result}
+
+
 def assemble(r, features: Iterable[str]) -> dict:
     """The reference-shaped results of one image.  The palette strings and the shadow level
     come made from libllfe's host half (C, off the GIL; llfe_image_result), so this only
     builds the objects; records without them (none from the batch entry points) take the
     Python rules."""
-    from .color_extractor import ColorExtractor, palette_features
+    return assemble_batch([r], features)[0]
 
-    out = {}
-    for f in features:
-        f = getattr(f, "value", f)
-        if f == "colors":
-            p = getattr(r, "palette", None)
-            out["colors"] = palette_features(*p) if p else ColorExtractor._palette(r.centers_rgb, r.counts)
-        elif f == "shapes":
-            out["shapes"] = shapes_result(r)
-        elif f == "shadows":
-            lv = getattr(r, "shadow_level", None)
-            out["shadows"] = {"shadow_level": lv if lv is not None else shadow_level(r.shadow_sum, r.shadow_count)}
-    return out
+
+def assemble_batch(recs, features: Iterable[str]) -> list:
+    """assemble() over a batch of records, the feature dispatch resolved once."""
+    makers = [(f, _MAKERS[f]) for f in (getattr(f, "value", f) for f in features) if f in _MAKERS]
+    return [{f: mk(r) for f, mk in makers} for r in recs]
 
 
 def run_batch(images, features: Sequence[str] = ("colors", "shapes", "shadows"), seed: Optional[int] = None,
@@ -75,7 +82,7 @@ def run_batch(images, features: Sequence[str] = ("colors", "shapes", "shadows"),
         n = int(images.shape[0])
         base = ce._next_index(n) if index_base is None else int(index_base)
         res = be.process(images, feats, seed=seed, noise=noise, index_base=base, n_colors=n_colors)
-        return res if raw else [assemble(r, feats) for r in res]
+        return res if raw else assemble_batch(res, feats)
     # a list of images of any sizes: one ragged llfe_process_images call (size groups
     # share device passes; every image keeps its own global index)
     imgs = [im if hasattr(im, "data_ptr") else np.asarray(im, np.uint8) for im in images]
@@ -88,5 +95,5 @@ def run_batch(images, features: Sequence[str] = ("colors", "shapes", "shadows"),
         nz = [np.asarray(noise[i], np.int8).reshape(-1, 3) for i in range(len(imgs))]
     res = be.process_images(imgs, feats, seed=seed, noise=nz, index_base=base, n_colors=n_colors,
                             preprocessing=preprocessing)
-    out = res if raw else [assemble(r, feats) for r in res]
+    out = res if raw else assemble_batch(res, feats)
     return out  # type: ignore[return-value]

@@ -1,0 +1,29 @@
+#!/bin/bash
+# GPU box: SQ_INSTS_VALU / SQ_WAVES / SALU of k_stencil_stream per synthetic class (3 launches
+# of 512 x 1080p each, tools/debug/stencil_kind.py), one rocprofv3 --pmc pass per class.
+set -u -o pipefail
+O=gpurun_out/stencil_pmc_kind
+mkdir -p $O
+export TMPDIR=/tmp
+for k in photo ui mix; do
+    rm -rf /tmp/spk_$k
+    timeout -s KILL 180 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_BUSY_CYCLES --kernel-trace \
+        -d /tmp/spk_$k -o run --output-format csv -- python3 tools/debug/stencil_kind.py $k > $O/$k.log 2>&1 \
+        || { tail -5 $O/$k.log; exit 1; }
+    f=$(find /tmp/spk_$k -name '*counter_collection.csv' | head -1)
+    python3 - "$f" $k <<'PY' | tee -a $O/summary.txt
+import csv, sys, collections
+rows = [r for r in csv.DictReader(open(sys.argv[1])) if "k_stencil_stream" in r["Kernel_Name"]]
+agg = collections.defaultdict(float)
+disp = set()
+for r in rows:
+    agg[r["Counter_Name"]] += float(r["Counter_Value"])
+    disp.add(r["Dispatch_Id"])
+n = max(len(disp), 1)
+per = {k: v / n for k, v in agg.items()}
+steps = 32 * 278.75 * 512  # waves x full row steps (ya - 5 .. yb + 5, from row 0) per launch, 512 x 1080p
+print(sys.argv[2], "dispatches", n, {k: "%.4g" % v for k, v in per.items()},
+      "VALU per wave-step %.1f" % (per.get("SQ_INSTS_VALU", 0) / steps),
+      "waves %.0f" % per.get("SQ_WAVES", 0))
+PY
+done

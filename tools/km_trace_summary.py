@@ -28,7 +28,9 @@ def main():
     dh = a.T[19].astype(np.uint64) if a.shape[1] >= 20 else z.astype(np.uint64)
     ok = it > 1
     pp = (tpp - t0) / 100.0
-    tl0 = a.T[20] if a.shape[1] >= 23 and (a.T[20] > 0).any() else tpp  # Lloyd start (split launches)
+    # Lloyd start stamp: its own launch's in a split build (a one-launch kernel stamps t_start)
+    split = a.shape[1] >= 23 and ((a.T[20] > 0) & (a.T[20] != t0)).any()
+    tl0 = a.T[20] if split else tpp
     ll = (tll - tl0) / 100.0
     cp = (t1 - tll) / 100.0
     ph = U > 300000
@@ -52,7 +54,6 @@ def main():
     def cu_of(h, x):
         return x * 1000 + ((h >> 13) & 7) * 100 + ((h >> 12) & 1) * 16 + ((h >> 8) & 15)
 
-    split = a.shape[1] >= 23 and (a.T[20] > 0).any()
     phases = [("k-means++", t0, tpp, cu_of(hw, xcc))]
     if split:
         tls, hw2, xcc2 = a.T[20], a.T[21], a.T[22]
