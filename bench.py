@@ -496,12 +496,23 @@ def main():
                 futs.append(asm_pool.submit(assemble_step, be.process(batch, feats, seed=seed0 + k, index_base=base)))
         else:
             pending = []
+            ts = tc = 0.0  # serving thread: wall time in submit / collect
             for k in range(k_steps):
+                t_a = time.perf_counter()
                 pending.append(be.submit(batch, feats, seed=seed0 + k, index_base=base))
+                t_b = time.perf_counter()
+                ts += t_b - t_a
                 if len(pending) == be.inflight:
-                    futs.append(asm_pool.submit(assemble_step, be.collect(pending.pop(0))))
+                    recs = be.collect(pending.pop(0))
+                    tc += time.perf_counter() - t_b
+                    futs.append(asm_pool.submit(assemble_step, recs))
             while pending:
-                futs.append(asm_pool.submit(assemble_step, be.collect(pending.pop(0))))
+                t_b = time.perf_counter()
+                recs = be.collect(pending.pop(0))
+                tc += time.perf_counter() - t_b
+                futs.append(asm_pool.submit(assemble_step, recs))
+            run_steps.serving = {"submit_ms_per_step": round(ts / k_steps * 1e3, 3),
+                                 "collect_ms_per_step": round(tc / k_steps * 1e3, 3)}
         t_last = time.perf_counter()
         shapes = sum(f.result() for f in futs)
         run_steps.tail_ms = (time.perf_counter() - t_last) * 1e3  # assembly left after the last collect
@@ -509,6 +520,17 @@ def main():
 
     pipelined = args.pipeline == "on"
     run_steps(args.warmup, args.seed + 1000, pipelined)
+    # A serving process's startup heap (torch, numpy, this package: ~180k objects) never
+    # becomes garbage; left in the collector's oldest generation, every full collection
+    # walks it -- a 45-90 ms stop of the serving thread (holding the GIL inside collect's
+    # result conversion) every few steps, long enough to drain both in-flight batches and
+    # idle the GPU (round 5, tools/debug/pipe_timeline.py).  gc.freeze() moves it out of
+    # the collector's passes (what long-running Python servers do after start-up); every
+    # object the steps allocate is still collected.
+    import gc
+
+    gc.collect()
+    gc.freeze()
     barrier()
     # hipEvent kernel timings: in the one-batch-at-a-time steps only (two batches in flight
     # overlap, so an event-timed span would include the other batch's kernels)
@@ -521,6 +543,7 @@ def main():
     t1 = time.perf_counter()
     host_ct = be.host_contour_stats(reset=True)
     asm_ms, asm_tail = list(asm_log), run_steps.tail_ms
+    serving = getattr(run_steps, "serving", None) if pipelined else None
     barrier()
     dt = shard.max_over_ranks(t1 - t0, device=coll_dev)
     stats = be.kernel_stats()
@@ -723,6 +746,7 @@ def main():
         "shapes_per_image": round(n_shapes / (B * args.steps), 2),
         # rows a6 / a10 inside the timed steps: every image's ColorFeatures / shapes dict /
         # {"shadow_level"} built on a worker thread beside the serving loop
+        "serving_thread": serving,
         "result_assembly": {"host_cpu_ms_per_step": round(sum(asm_ms) / max(len(asm_ms), 1), 3),
                             "us_per_image": round(sum(asm_ms) / max(len(asm_ms), 1) / B * 1e3, 2),
                             "tail_ms_after_last_collect": round(asm_tail, 3),

@@ -348,13 +348,35 @@ __device__ __forceinline__ int unpack_r(uint32_t k) { return (int)((k >> 16) & 2
 __device__ __forceinline__ int unpack_g(uint32_t k) { return (int)((k >> 8) & 255u); }
 __device__ __forceinline__ int unpack_b(uint32_t k) { return (int)(k & 255u); }
 
-// D(p) = min over the first kk chosen centres (kk >= 1)
-__device__ __forceinline__ int dmin_chosen(int x, int y, int z, const ICent &ch, int kk) {
-    int d = d2i(x, y, z, ch.x[0], ch.y[0], ch.z[0]);
+// D(p) for a packed key by the linear forms: d(p, c) = |p|^2 - H_c(p), H_c(p) = 2 p.c - |c|^2,
+// 2 p.c = dot2((B, R), (2 c_B, 2 c_R)) + G 2 c_G (v_dot2_u32_u16 over one v_mad_u32_u24 whose
+// addend is -|c|^2: the u32 arithmetic wraps to the exact int), so min over the chosen centres
+// = |p|^2 - max H: three VALU ops per centre instead of d2i's six and a min
+struct HCent {
+    u16x2 rb2[kMaxK];      // (2 c_B, 2 c_R)
+    uint32_t g2[kMaxK];    // 2 c_G
+    uint32_t nc2[kMaxK];   // -|c|^2 (mod 2^32)
+};
+__device__ __forceinline__ HCent hcent(const ICent &ch) {
+    HCent h;
 #pragma unroll
-    for (int m = 1; m < kMaxK; m++)
-        if (m < kk) d = min(d, d2i(x, y, z, ch.x[m], ch.y[m], ch.z[m]));
-    return d;
+    for (int m = 0; m < kMaxK; m++) {
+        h.rb2[m] = u16x2{(uint16_t)(2 * ch.z[m]), (uint16_t)(2 * ch.x[m])};
+        h.g2[m] = (uint32_t)(2 * ch.y[m]);
+        h.nc2[m] = 0u - (uint32_t)(ch.x[m] * ch.x[m] + ch.y[m] * ch.y[m] + ch.z[m] * ch.z[m]);
+    }
+    return h;
+}
+template <int KK>
+__device__ __forceinline__ uint32_t dmin_key(uint32_t kq, const HCent &h) {
+    const u16x2 rb = __builtin_bit_cast(u16x2, kq & 0x00FF00FFu);  // (B, R)
+    const uint32_t g = (kq >> 8) & 255u;
+    const uint32_t p2 = __builtin_amdgcn_udot2(rb, rb, __umul24(g, g), false);
+    int Hm = (int)__builtin_amdgcn_udot2(rb, h.rb2[0], g * h.g2[0] + h.nc2[0], false);
+#pragma unroll
+    for (int m = 1; m < KK; m++)
+        Hm = max(Hm, (int)__builtin_amdgcn_udot2(rb, h.rb2[m], g * h.g2[m] + h.nc2[m], false));
+    return p2 - (uint32_t)Hm;
 }
 
 // Partition p's keys in np.unique order, in the key array (wave 0): sm.pbase[p] (np.unique
@@ -474,10 +496,15 @@ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, int K, uint64
                 // scalar loads (~75 us per k-means++ round on a photo).
                 // Step sums alias the Lloyd accumulators (unused until Lloyd).
                 uint32_t(*stp)[KW][kSelSteps] = reinterpret_cast<uint32_t(*)[KW][kSelSteps]>(&sm.accA[0][0]);
+                const HCent hc = hcent(ch);
                 uint32_t ca[3], cb2[3], cw0[3], cw1[3];  // partition [a, b), this wave's steps [w0, w1)
+                // a partition two trials share is scanned once (the later trial reads the
+                // earlier one's step and chunk sums: D is the same for all three)
+                const int P0 = sm.pj[0], P1 = sm.pj[1], P2 = sm.pj[2];
+                const bool dup[3] = {false, P1 >= 0 && P1 == P0, P2 >= 0 && (P2 == P0 || P2 == P1)};
     #pragma unroll
                 for (int j = 0; j < 3; j++) {
-                    const int P = sm.pj[j];  // (its keys: addresses [kbeg, kbeg + count))
+                    const int P = dup[j] ? -1 : sm.pj[j];  // (its keys: addresses [kbeg, kbeg + count))
                     ca[j] = P >= 0 ? sm.kbeg[P] : 0u;
                     cb2[j] = P >= 0 ? sm.kbeg[P] + (sm.pbase[P + 1] - sm.pbase[P]) : 0u;
                     const uint32_t A = ca[j] & ~3u;
@@ -511,8 +538,8 @@ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, int K, uint64
                                 for (int jj = 0; jj < 4; jj++) {
                                     const uint32_t i = i0 + (uint32_t)jj;
                                     const bool in = i >= ca[j] && i < cb2[j];
-                                    const int d = dmin_chosen(unpack_r(kq[jj]), unpack_g(kq[jj]), unpack_b(kq[jj]), ch, KK);
-                                    sd += in ? (uint32_t)d : 0u;
+                                    const uint32_t d = dmin_key<KK>(kq[jj], hc);
+                                    sd += in ? d : 0u;
                                 }
                                 ls += sd;
                                 const uint32_t ssum = wave_sum(sd);  // <= 256 x 195075 < 2^32
@@ -535,7 +562,8 @@ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, int K, uint64
                 if (wid < 3) {
                     const int j = wid;
                     const double pj = j == 0 ? p[0] : (j == 1 ? p[1] : p[2]);
-                    const int P = sm.pj[j];
+                    const int P = j == 0 ? P0 : (j == 1 ? P1 : P2);  // (sm.pj[j] is being overwritten)
+                    const int src = j == 1 ? (dup[1] ? 0 : 1) : (j == 2 ? (!dup[2] ? 2 : (P2 == P0 ? 0 : 1)) : 0);
                     // (key addresses; p <= 0: the first key, p beyond the total: the last)
                     int ci = (int)(P == -2 ? sm.kfirst : sm.klast);
                     if (P >= 0) {
@@ -545,8 +573,8 @@ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, int K, uint64
                         unsigned long long e = sm.pex[j];
                         int w = 0;
                         for (; w < KW - 1; w++) {
-                            if ((double)(e + sm.wchunk[j][w]) >= pj) break;
-                            e += sm.wchunk[j][w];
+                            if ((double)(e + sm.wchunk[src][w]) >= pj) break;
+                            e += sm.wchunk[src][w];
                         }
                         const uint32_t w0 = A + min(nst, (uint32_t)w * per) * STEP, w1 = A + min(nst, (uint32_t)(w + 1) * per) * STEP;
                         const int ns = (int)((w1 - w0) / STEP);
@@ -554,7 +582,7 @@ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, int K, uint64
                         int sidx = ns - 1;
                         for (int s_base = 0; s_base < ns; s_base += 64) {
                             const int si = s_base + lane;
-                            const unsigned long long v = si < ns ? (unsigned long long)stp[j][w][si] : 0ull;
+                            const unsigned long long v = si < ns ? (unsigned long long)stp[src][w][si] : 0ull;
                             unsigned long long x = v;
     #pragma unroll
                             for (int off = 1; off < 64; off <<= 1) {
@@ -582,7 +610,7 @@ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, int K, uint64
                             for (int jj = 0; jj < 4; jj++) {
                                 const uint32_t i = i0 + (uint32_t)jj;
                                 const bool in = i >= a && i < b;
-                                dv[jj] = in ? (uint32_t)dmin_chosen(unpack_r(kq[jj]), unpack_g(kq[jj]), unpack_b(kq[jj]), ch, KK) : 0u;
+                                dv[jj] = in ? dmin_key<KK>(kq[jj], hc) : 0u;
                                 ls += dv[jj];
                             }
                             unsigned long long x = ls;

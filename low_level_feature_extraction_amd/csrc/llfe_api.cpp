@@ -251,6 +251,10 @@ struct Profiler {
     std::vector<hipEvent_t> all, free_;
     std::vector<Rec> pending;
     std::vector<Stat> stats;
+    // debug (LLFE_TIMELINE=file): every collected record's start / end in ms after `base`,
+    // an event recorded when profiling was switched on (tools/debug/pipe_timeline.py)
+    hipEvent_t base = nullptr;
+    FILE *tl = nullptr;
     hipEvent_t ev() {
         if (free_.empty()) {
             hipEvent_t e;
@@ -301,6 +305,9 @@ struct Profiler {
                 stats[r.kid].launches++;
                 stats[r.kid].ms += ms;
                 stats[r.kid].bytes += r.bytes;
+                float t0 = 0.f;
+                if (tl && base && hipEventElapsedTime(&t0, base, r.a) == hipSuccess)
+                    fprintf(tl, "%s %d %.4f %.4f\n", stats[r.kid].name.c_str(), r.slot, t0, t0 + ms);
             }
             free_.push_back(r.a);
             free_.push_back(r.b);
@@ -321,6 +328,8 @@ struct Profiler {
     }
     ~Profiler() {
         for (auto e : all) (void)hipEventDestroy(e);
+        if (base) (void)hipEventDestroy(base);
+        if (tl) fclose(tl);
     }
 };
 
@@ -1128,6 +1137,16 @@ int llfe_set_profiling(llfe_ctx *ctx, int enable) {
     if (!ctx) return LLFE_ERR_INVALID;
     if (enable) ctx->prof.reset();
     ctx->prof.on = enable != 0;
+    if (enable) {
+        if (const char *path = getenv("LLFE_TIMELINE")) {  // debug: absolute kernel intervals
+            HIPCHK(ctx, hipSetDevice(ctx->device));
+            if (!ctx->prof.base) HIPCHK(ctx, hipEventCreate(&ctx->prof.base));
+            HIPCHK(ctx, hipEventRecord(ctx->prof.base, nullptr));
+            HIPCHK(ctx, hipEventSynchronize(ctx->prof.base));
+            if (!ctx->prof.tl) ctx->prof.tl = fopen(path, "a");
+            if (ctx->prof.tl) fprintf(ctx->prof.tl, "# base\n");
+        }
+    }
     return LLFE_OK;
 }
 

@@ -162,7 +162,12 @@ __device__ __forceinline__ uint32_t blur4(uint32_t g0, uint32_t g1, uint32_t g2,
 // Sobel (3x3, on REPLICATE'd blurred rows b0 above, b1, b2 below) -> |dx|+|dy| and the
 // Canny NMS direction class (0 horizontal, 1 vertical, 2 / 3 diagonals) as
 // m | dir << 12 in two u16x2 dwords (cols c0 c1 | c2 c3)
-__device__ __forceinline__ bool sobel4(uint32_t b0, uint32_t b1, uint32_t b2, uint32_t &mlo, uint32_t &mhi) {
+// `live`: the lane holds output columns.  Only those decide whether the wave's row needs the
+// direction classes and NMS: the halo lanes 0 / 63 read zeros past the wave's edge (DPP
+// bound_ctrl), so their magnitudes are not the image's and would make every row look like it
+// has a candidate (round 4 / early round 5: the direction + NMS code ran on every row).
+__device__ __forceinline__ bool sobel4(uint32_t b0, uint32_t b1, uint32_t b2, uint32_t &mlo, uint32_t &mhi,
+                                       bool live) {
     const u16x2 two = {2, 2};
     const u16x2 vs_lo = U(lo2(b0)) + U(lo2(b2)) + U(lo2(b1)) * two;  // [1 2 1] vertical
     const u16x2 vs_hi = U(hi2(b0)) + U(hi2(b2)) + U(hi2(b1)) * two;
@@ -184,7 +189,7 @@ __device__ __forceinline__ bool sobel4(uint32_t b0, uint32_t b1, uint32_t b2, ui
     // the direction class matters only where m > LOW (the NMS below): computed, without
     // branches, only when some lane of the wave has such a pixel
     constexpr int LOW = 50, TG22 = 13573;
-    const bool need = (int)m_lo.x > LOW || (int)m_lo.y > LOW || (int)m_hi.x > LOW || (int)m_hi.y > LOW;
+    const bool need = live && ((int)m_lo.x > LOW || (int)m_lo.y > LOW || (int)m_hi.x > LOW || (int)m_hi.y > LOW);
     const bool wave_need = __ballot(need) != 0;
     if (wave_need) {
         ST_MARK(direction);
@@ -422,7 +427,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, LLFE_ST_MINW) void k_stencil_s
                 // ---- magnitude row t-1 from blurred rows t-2, t-1, t
                 ST_MARK(sobel);
                 uint32_t lo, hi;
-                const bool cand = sobel4(bring[(k + 4) % 6], bring[(k + 5) % 6], B, lo, hi);
+                const bool cand = sobel4(bring[(k + 4) % 6], bring[(k + 5) % 6], B, lo, hi, out_lane);
                 ST_PIN(lo);
                 ST_PIN(hi);
                 const bool row_in = (unsigned)(t - 1) < (unsigned)H;

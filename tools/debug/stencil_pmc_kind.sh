@@ -1,16 +1,19 @@
 #!/bin/bash
-# GPU box: SQ_INSTS_VALU / SQ_WAVES / SALU of k_stencil_stream per synthetic class (3 launches
-# of 512 x 1080p each, tools/debug/stencil_kind.py), one rocprofv3 --pmc pass per class.
+# GPU box: SQ counters of k_stencil_stream per synthetic class (3 launches of 512 x 1080p
+# each, tools/debug/stencil_kind.py), one rocprofv3 --pmc pass per class (8 SQ counters).
 set -u -o pipefail
 O=gpurun_out/stencil_pmc_kind
 mkdir -p $O
+rm -f $O/summary.txt
 export TMPDIR=/tmp
+C="SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY"
 for k in photo ui mix; do
     rm -rf /tmp/spk_$k
-    timeout -s KILL 180 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_BUSY_CYCLES --kernel-trace \
+    timeout -s KILL 180 rocprofv3 --pmc $C --kernel-trace \
         -d /tmp/spk_$k -o run --output-format csv -- python3 tools/debug/stencil_kind.py $k > $O/$k.log 2>&1 \
         || { tail -5 $O/$k.log; exit 1; }
     f=$(find /tmp/spk_$k -name '*counter_collection.csv' | head -1)
+    cp "$f" $O/$k.csv
     python3 - "$f" $k <<'PY' | tee -a $O/summary.txt
 import csv, sys, collections
 rows = [r for r in csv.DictReader(open(sys.argv[1])) if "k_stencil_stream" in r["Kernel_Name"]]
@@ -22,8 +25,7 @@ for r in rows:
 n = max(len(disp), 1)
 per = {k: v / n for k, v in agg.items()}
 steps = 32 * 278.75 * 512  # waves x full row steps (ya - 5 .. yb + 5, from row 0) per launch, 512 x 1080p
-print(sys.argv[2], "dispatches", n, {k: "%.4g" % v for k, v in per.items()},
-      "VALU per wave-step %.1f" % (per.get("SQ_INSTS_VALU", 0) / steps),
-      "waves %.0f" % per.get("SQ_WAVES", 0))
+print(sys.argv[2], "dispatches", n, {k: "%.4g" % v for k, v in sorted(per.items())},
+      "VALU per wave-step %.1f" % (per.get("SQ_INSTS_VALU", 0) / steps))
 PY
 done
