@@ -364,7 +364,7 @@ def main():
                     help="also run the e2e lines when WORLD_SIZE > 1 (off by default: every rank would pin "
                          "~10 GB of host batches and decode on its 1/N core share while the scaling run "
                          "only needs `value`)")
-    ap.add_argument("--per-class-steps", type=int, default=2,
+    ap.add_argument("--per-class-steps", type=int, default=4,
                     help="steps of an all-ui and an all-photo batch (SURVEY.md 8d per-class throughput); 0 disables")
     ap.add_argument("--contours", choices=["auto", "host", "gpu"], default="auto",
                     help="where findContours + the shape loop run: the host pool from the copied-back mask "

@@ -313,6 +313,7 @@ struct Profiler {
             free_.push_back(r.b);
         }
         pending.resize(keep);
+        if (tl) fflush(tl);
     }
     // bytes known only after the launch completed (k-means sweeps)
     void add_bytes(const char *name, double bytes) {

@@ -13,7 +13,10 @@ for k in photo ui mix; do
         -d /tmp/spk_$k -o run --output-format csv -- python3 tools/debug/stencil_kind.py $k > $O/$k.log 2>&1 \
         || { tail -5 $O/$k.log; exit 1; }
     f=$(find /tmp/spk_$k -name '*counter_collection.csv' | head -1)
-    cp "$f" $O/$k.csv
+    python3 -c "
+import csv, sys
+r = csv.DictReader(open(sys.argv[1])); w = csv.DictWriter(open(sys.argv[2], 'w'), r.fieldnames); w.writeheader()
+[w.writerow(x) for x in r if 'k_stencil_stream' in x['Kernel_Name']]" "$f" $O/$k.csv
     python3 - "$f" $k <<'PY' | tee -a $O/summary.txt
 import csv, sys, collections
 rows = [r for r in csv.DictReader(open(sys.argv[1])) if "k_stencil_stream" in r["Kernel_Name"]]
