@@ -52,3 +52,29 @@ def test_direct_colorfeatures_equal_validated(args):
     a, b = palette_features(*args), _validated(*args)
     assert a == b and a.model_dump() == b.model_dump() and a.model_dump_json() == b.model_dump_json()
     assert type(a) is type(b)
+
+
+def test_assemble_batch_matches_per_record_rules():
+    """pipeline.assemble_batch (the serving loop's batch assembly: dispatch resolved once per
+    batch) builds, per record and in `features` order, what the reference's per-feature calls
+    return -- from the C-made palette / shadow level when present, else by the Python rules;
+    unknown feature names are skipped, as assemble() always did."""
+    from low_level_feature_extraction_amd.backend import ImageFeatures
+    from low_level_feature_extraction_amd.models import FeatureType
+    from low_level_feature_extraction_amd.pipeline import assemble, assemble_batch, shadow_level
+
+    cen = np.array([[10, 20, 30], [200, 210, 220], [255, 255, 255]], np.uint8)
+    cnt = np.array([5, 9, 1], np.int64)
+    shapes = [{"type": "rectangle", "x": 1, "y": 2, "width": 3, "height": 4, "border_radius": 0.0, "area": 12.0}]
+    made = ImageFeatures(cen, cnt, 15, 1.0, 800, 10, shapes, 1, 64, 32,
+                         palette=("#c8d2dc", "#000000", ["#0a141e", "#0a141e", "#0a141e"]), shadow_level="Moderate")
+    bare = ImageFeatures(cen, cnt, 15, 1.0, 800, 10, shapes, 1, 64, 32)
+    feats = ["shadows", FeatureType.COLORS if hasattr(FeatureType, "COLORS") else "colors", "shapes", "text"]
+    out = assemble_batch([made, bare], feats)
+    assert [list(o) for o in out] == [["shadows", "colors", "shapes"]] * 2
+    assert out[0]["shadows"] == {"shadow_level": "Moderate"}
+    assert out[1]["shadows"] == {"shadow_level": shadow_level(800, 10)}
+    assert out[0]["colors"] == out[1]["colors"] == ColorExtractor._palette(cen, cnt)
+    assert out[0]["shapes"] == {"shapes": shapes, "total_shapes": 1, "metadata": {"image_width": 64, "image_height": 32}}
+    assert out[0]["shapes"]["shapes"] is not shapes  # a new list per result, as analyze_shapes returns
+    assert assemble(made, feats) == out[0]
