@@ -372,10 +372,10 @@ __device__ __forceinline__ uint32_t dmin_key(uint32_t kq, const HCent &h) {
     const u16x2 rb = __builtin_bit_cast(u16x2, kq & 0x00FF00FFu);  // (B, R)
     const uint32_t g = (kq >> 8) & 255u;
     const uint32_t p2 = __builtin_amdgcn_udot2(rb, rb, __umul24(g, g), false);
-    int Hm = (int)__builtin_amdgcn_udot2(rb, h.rb2[0], g * h.g2[0] + h.nc2[0], false);
+    int Hm = (int)__builtin_amdgcn_udot2(rb, h.rb2[0], __umul24(g, h.g2[0]) + h.nc2[0], false);
 #pragma unroll
     for (int m = 1; m < KK; m++)
-        Hm = max(Hm, (int)__builtin_amdgcn_udot2(rb, h.rb2[m], g * h.g2[m] + h.nc2[m], false));
+        Hm = max(Hm, (int)__builtin_amdgcn_udot2(rb, h.rb2[m], __umul24(g, h.g2[m]) + h.nc2[m], false));
     return p2 - (uint32_t)Hm;
 }
 
@@ -672,12 +672,20 @@ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, int K, uint64
             // and the corner margins 6 sum max(+-(a - b), 0) depend on the centres only.
             // The pairwise corner margins live in LDS (per-lane reads indexed by the lane's
             // owner k); the per-centre constants stay in scalar registers.
-            int C2[kMaxK], T2[3];
-            u16x2 chrb[kMaxK], trb[3];  // (B, R) of the chosen centres and the trials
+            // (B, R) and G of the chosen centres and the trials, doubled: every use below is
+            // 2 p.c (2 o.c, 2 S_u.c), so the doubling costs nothing and saves a shift per use
+            int C2[kMaxK], T2[3], chg2[kMaxK], tg2[3];
+            u16x2 chrb[kMaxK], trb[3];
     #pragma unroll
-            for (int m = 0; m < kMaxK; m++) chrb[m] = u16x2{(uint16_t)ch.z[m], (uint16_t)ch.x[m]};
+            for (int m = 0; m < kMaxK; m++) {
+                chrb[m] = u16x2{(uint16_t)(2 * ch.z[m]), (uint16_t)(2 * ch.x[m])};
+                chg2[m] = 2 * ch.y[m];
+            }
     #pragma unroll
-            for (int j = 0; j < 3; j++) trb[j] = u16x2{(uint16_t)tz[j], (uint16_t)tx[j]};
+            for (int j = 0; j < 3; j++) {
+                trb[j] = u16x2{(uint16_t)(2 * tz[j]), (uint16_t)(2 * tx[j])};
+                tg2[j] = 2 * ty[j];
+            }
     #pragma unroll
             for (int m = 0; m < kMaxK; m++) C2[m] = ch.x[m] * ch.x[m] + ch.y[m] * ch.y[m] + ch.z[m] * ch.z[m];
     #pragma unroll
@@ -693,22 +701,23 @@ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, int K, uint64
                 if (lane < count) {
                     // d(p, c) = |p|^2 - H_c(p), H_c(p) = 2 p.c - |c|^2 (exact integers): the
                     // |p|^2 term is common to D and every trial, so min(D, d(p, t)) =
-                    // |p|^2 - max(max_m H_m, H_t).  p.c = dot2((R, B), (c_R, c_B)) + G c_G:
-                    // one v_dot2_u32_u16 and one 24-bit multiply, then one shift-add, per centre
+                    // |p|^2 - max(max_m H_m, H_t).  2 p.c - |c|^2 = dot2((B, R), 2 (c_B, c_R))
+                    // over the 24-bit multiply-add G 2 c_G - |c|^2 (u32 arithmetic wraps to the
+                    // exact int): two VALU ops per centre
                     const uint32_t kq = stg[(tail + lane) & (kStage - 1)];
                     const u16x2 rb = __builtin_bit_cast(u16x2, kq & 0x00FF00FFu);  // (B, R)
                     const uint32_t g = (kq >> 8) & 255u;
                     const uint32_t p2 = __builtin_amdgcn_udot2(rb, rb, __umul24(g, g), false);
-                    auto H = [&](u16x2 crb, uint32_t cg, int c2) {
-                        return (int)(__builtin_amdgcn_udot2(rb, crb, __umul24(g, cg), false) << 1) - c2;
+                    auto H = [&](u16x2 crb2, int cg2, int c2) {
+                        return (int)__builtin_amdgcn_udot2(rb, crb2, __umul24(g, (uint32_t)cg2) + (0u - (uint32_t)c2), false);
                     };
-                    int Hm = H(chrb[0], (uint32_t)ch.y[0], C2[0]);
+                    int Hm = H(chrb[0], chg2[0], C2[0]);
     #pragma unroll
                     for (int m = 1; m < kMaxK; m++)
-                        if (m < KK) Hm = max(Hm, H(chrb[m], (uint32_t)ch.y[m], C2[m]));
-                    acc0 += p2 - (uint32_t)max(Hm, H(trb[0], (uint32_t)ty[0], T2[0]));
-                    acc1 += p2 - (uint32_t)max(Hm, H(trb[1], (uint32_t)ty[1], T2[1]));
-                    acc2 += p2 - (uint32_t)max(Hm, H(trb[2], (uint32_t)ty[2], T2[2]));
+                        if (m < KK) Hm = max(Hm, H(chrb[m], chg2[m], C2[m]));
+                    acc0 += p2 - (uint32_t)max(Hm, H(trb[0], tg2[0], T2[0]));
+                    acc1 += p2 - (uint32_t)max(Hm, H(trb[1], tg2[1], T2[1]));
+                    acc2 += p2 - (uint32_t)max(Hm, H(trb[2], tg2[2], T2[2]));
                 }
                 tail += count;
             };
@@ -787,17 +796,17 @@ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, int K, uint64
                 // 24-bit multiply (operands <= 255 and sums <= 1792, results < 2^32: exact)
                 const u16x2 orb = u16x2{(uint16_t)oz, (uint16_t)ox};
                 const u16x2 srb = u16x2{(uint16_t)sz, (uint16_t)sx};
-                auto odot = [&](u16x2 crb, int cg) {  // o . c
+                auto odot = [&](u16x2 crb, int cg) {  // o . c (o . 2c with the doubled constants)
                     return (int)__builtin_amdgcn_udot2(orb, crb, __umul24((uint32_t)oy, (uint32_t)cg), false);
                 };
-                auto sdot = [&](u16x2 crb, int cg) {  // S_u . c
+                auto sdot = [&](u16x2 crb, int cg) {  // S_u . c (S_u . 2c with the doubled constants)
                     return (int)__builtin_amdgcn_udot2(srb, crb, __umul24((uint32_t)sy, (uint32_t)cg), false);
                 };
                 int Dc[kMaxK];
     #pragma unroll
                 for (int m = 0; m < kMaxK; m++) {  // (only the KK chosen centres are read)
                     Dc[m] = 0;
-                    if (m < KK) Dc[m] = C2[m] - 2 * odot(chrb[m], ch.y[m]);
+                    if (m < KK) Dc[m] = C2[m] - odot(chrb[m], chg2[m]);
                 }
                 auto sq = [&](int m) { return ex * ch.x[m] + ey * ch.y[m] + ez * ch.z[m]; };
                 int k = 0, bd = Dc[0] - sq(0);
@@ -811,13 +820,13 @@ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, int K, uint64
                     }
                 }
                 // owner k's values (per-lane selects from the uniform tables)
-                int Dk = Dc[0], ky = ch.y[0];
+                int Dk = Dc[0], ky = chg2[0];
                 u16x2 krb = chrb[0];
     #pragma unroll
                 for (int m = 1; m < kMaxK; m++) {
                     if (m >= KK) break;
                     Dk = k == m ? Dc[m] : Dk;
-                    ky = k == m ? ch.y[m] : ky;
+                    ky = k == m ? chg2[m] : ky;
                     krb = k == m ? chrb[m] : krb;
                 }
                 // owned: no other chosen centre is ever strictly closer on the box
@@ -829,17 +838,17 @@ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, int K, uint64
                 }
                 // box sums: P + n D_c(o) - 2 c.S_u, P = n |o|^2 + 2 o.S_u + S_u2
                 const int Pc = __mul24(n, odot(orb, oy)) + 2 * sdot(orb, oy) + s2;
-                const uint32_t ds = (uint32_t)(Pc + __mul24(n, Dk) - 2 * sdot(krb, ky));
+                const uint32_t ds = (uint32_t)(Pc + __mul24(n, Dk) - sdot(krb, ky));
                 uint32_t vv[3];
                 bool dec = owned;
     #pragma unroll
                 for (int j = 0; j < 3; j++) {
-                    const int Dt = T2[j] - 2 * odot(trb[j], ty[j]);
+                    const int Dt = T2[j] - odot(trb[j], tg2[j]);
                     const int f = Dt - Dk;
                     const bool A = f - NAx[j * kMaxK + k] >= 0;  // t_j never strictly closer than c_k
                     const bool B = f + NBx[j * kMaxK + k] <= 0;  // t_j always at least as close
                     dec = dec & (A | B);
-                    vv[j] = A ? ds : (uint32_t)(Pc + __mul24(n, Dt) - 2 * sdot(trb[j], ty[j]));
+                    vv[j] = A ? ds : (uint32_t)(Pc + __mul24(n, Dt) - sdot(trb[j], tg2[j]));
                 }
                 v0 = vv[0];
                 v1 = vv[1];
