@@ -199,6 +199,7 @@ struct KmSmem {
     unsigned long long sel_pts;          // colours the selection scans read
     unsigned long long wchunk[3][KW];    // per trial: sum of D over each wave's chunk
     uint32_t stage[KW][kStage + 64];     // per-wave ring of boundary colours (+ a dummy row)
+    float thrL[2][kMaxK * kMaxK];        // Lloyd margin thresholds [cube / cell][owner k][j]
     int cq[KW][256];                     // per-wave list of the cubes of a chunk's failing cells
     unsigned long long qtot;             // sum of |p|^2 over all colours (exact)
     int marg[kMaxK * kMaxK + 6 * kMaxK]; // k-means++ corner margins: centre pairs, trial vs centre (+/-)
@@ -1488,16 +1489,20 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
                     }
                 }
             }
-            float thr[kMaxK][kMaxK];
-#pragma unroll
-            for (int k = 0; k < kMaxK; k++)
-#pragma unroll
-                for (int j = 0; j < kMaxK; j++)
-                    thr[k][j] = (j == k || j >= K || k >= K)
-                                    ? -__builtin_inff()
-                                    : 3.f * (fabsf(cu.x[j] - cu.x[k]) + fabsf(cu.y[j] - cu.y[k]) +
-                                             fabsf(cu.z[j] - cu.z[k])) +
-                                          1.f;
+            // Pair thresholds T[k][j] in LDS, read per lane for the lane's owner k: a box
+            // passes when d_j(q) - d_k(q) > T[k][j] for every j (T[k][k] = -inf), five
+            // compares against the owner's row instead of the ten centre pairs' compares
+            // combined by the owner masks.  Cube: 3 L1(c_j - c_k) + 1; 4 x 8 x 8 cell:
+            // 3 |dx| + 7 (|dy| + |dz|) + 1 (the half extents).
+            if (tid < 2 * kMaxK * kMaxK) {
+                const int kind = tid / (kMaxK * kMaxK), k = (tid / kMaxK) % kMaxK, j = tid % kMaxK;
+                const float dx = fabsf(sm.c[j][0] - sm.c[k][0]), dy = fabsf(sm.c[j][1] - sm.c[k][1]),
+                            dz = fabsf(sm.c[j][2] - sm.c[k][2]);
+                sm.thrL[kind][k * kMaxK + j] = (j == k || j >= K || k >= K) ? -__builtin_inff()
+                                               : kind == 0 ? 3.f * (dx + dy + dz) + 1.f
+                                                           : 3.f * dx + 7.f * (dy + dz) + 1.f;
+            }
+            __syncthreads();
             unsigned long long fails = 0;
             // boundary colours: each undecided cube's lanes (lane = mask bit) store their
             // colour into this wave's LDS ring at head + rank (a dummy slot per lane when
@@ -1559,22 +1564,11 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
                     const float dv[5] = {d[0].x, d[0].y, d[1].x, d[1].y, d[2].x};
                     const float m1 = fminf(fminf(fminf(dv[0], dv[1]), fminf(dv[2], dv[3])), dv[4]);
                     // k = first minimum; every other centre j must be farther by more than
-                    // T[k][j] at q.  T is symmetric and dv[k] = m1, so the test per pair
-                    // (a, b) is |dv[a] - dv[b]| > T[a][b]: ten compares into lane masks,
-                    // combined per k with scalar mask logic
-                    // (bitwise & | on the lane masks: no short-circuit branches)
-                    const bool e0 = dv[0] == m1, e1 = dv[1] == m1, e2 = dv[2] == m1, e3 = dv[3] == m1;
-                    const bool is0 = e0, is1 = !e0 & e1, is2 = !e0 & !e1 & e2, is3 = !e0 & !e1 & !e2 & e3,
-                               is4 = !(e0 | e1 | e2 | e3);
-                    const bool o01 = fabsf(dv[0] - dv[1]) > thr[0][1], o02 = fabsf(dv[0] - dv[2]) > thr[0][2],
-                               o03 = fabsf(dv[0] - dv[3]) > thr[0][3], o04 = fabsf(dv[0] - dv[4]) > thr[0][4],
-                               o12 = fabsf(dv[1] - dv[2]) > thr[1][2], o13 = fabsf(dv[1] - dv[3]) > thr[1][3],
-                               o14 = fabsf(dv[1] - dv[4]) > thr[1][4], o23 = fabsf(dv[2] - dv[3]) > thr[2][3],
-                               o24 = fabsf(dv[2] - dv[4]) > thr[2][4], o34 = fabsf(dv[3] - dv[4]) > thr[3][4];
-                    pass = (is0 & o01 & o02 & o03 & o04) | (is1 & o01 & o12 & o13 & o14) |
-                           (is2 & o02 & o12 & o23 & o24) | (is3 & o03 & o13 & o23 & o34) |
-                           (is4 & o04 & o14 & o24 & o34);
-                    k = is0 ? 0 : (is1 ? 1 : (is2 ? 2 : (is3 ? 3 : 4)));
+                    // T[k][j] at q (dv[k] = m1, so dv[j] - m1 = |dv[j] - dv[k]|)
+                    k = dv[0] == m1 ? 0 : (dv[1] == m1 ? 1 : (dv[2] == m1 ? 2 : (dv[3] == m1 ? 3 : 4)));
+                    const float *tk = &sm.thrL[0][k * kMaxK];
+                    pass = (dv[0] - m1 > tk[0]) & (dv[1] - m1 > tk[1]) & (dv[2] - m1 > tk[2]) &
+                           (dv[3] - m1 > tk[3]) & (dv[4] - m1 > tk[4]);
                 }
                 if (pass) {
                     const CubeGeo g = cube_geo(e);
@@ -1621,15 +1615,6 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
             // same argument as for a cube: every colour of the box is at least 1 closer to
             // c_k); the cubes of the failing cells of a chunk are listed in the wave's LDS
             // list and go through the cube test 64 at a time.
-            float thrC[kMaxK][kMaxK];
-#pragma unroll
-            for (int k = 0; k < kMaxK; k++)
-#pragma unroll
-                for (int j = 0; j < kMaxK; j++)
-                    thrC[k][j] = (j == k || j >= K || k >= K)
-                                     ? -__builtin_inff()
-                                     : 3.f * fabsf(cu.x[j] - cu.x[k]) + 7.f * (fabsf(cu.y[j] - cu.y[k]) +
-                                                                             fabsf(cu.z[j] - cu.z[k])) + 1.f;
             // (per image, as in k-means++: cells pay off on large cube tables -- a photo's
             // Lloyd iteration 74.5 -> 69.8 us, r4b -- not on a ui image's ~3k cubes)
             if (C >= kCellMinCubes) {
@@ -1661,18 +1646,10 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
                         }
                         const float dv[5] = {d[0].x, d[0].y, d[1].x, d[1].y, d[2].x};
                         const float m1 = fminf(fminf(fminf(dv[0], dv[1]), fminf(dv[2], dv[3])), dv[4]);
-                        const bool e0 = dv[0] == m1, e1 = dv[1] == m1, e2 = dv[2] == m1, e3 = dv[3] == m1;
-                        const bool is0 = e0, is1 = !e0 & e1, is2 = !e0 & !e1 & e2, is3 = !e0 & !e1 & !e2 & e3,
-                                   is4 = !(e0 | e1 | e2 | e3);
-                        const bool o01 = fabsf(dv[0] - dv[1]) > thrC[0][1], o02 = fabsf(dv[0] - dv[2]) > thrC[0][2],
-                                   o03 = fabsf(dv[0] - dv[3]) > thrC[0][3], o04 = fabsf(dv[0] - dv[4]) > thrC[0][4],
-                                   o12 = fabsf(dv[1] - dv[2]) > thrC[1][2], o13 = fabsf(dv[1] - dv[3]) > thrC[1][3],
-                                   o14 = fabsf(dv[1] - dv[4]) > thrC[1][4], o23 = fabsf(dv[2] - dv[3]) > thrC[2][3],
-                                   o24 = fabsf(dv[2] - dv[4]) > thrC[2][4], o34 = fabsf(dv[3] - dv[4]) > thrC[3][4];
-                        pass = (is0 & o01 & o02 & o03 & o04) | (is1 & o01 & o12 & o13 & o14) |
-                               (is2 & o02 & o12 & o23 & o24) | (is3 & o03 & o13 & o23 & o34) |
-                               (is4 & o04 & o14 & o24 & o34);
-                        k = is0 ? 0 : (is1 ? 1 : (is2 ? 2 : (is3 ? 3 : 4)));
+                        k = dv[0] == m1 ? 0 : (dv[1] == m1 ? 1 : (dv[2] == m1 ? 2 : (dv[3] == m1 ? 3 : 4)));
+                        const float *tk = &sm.thrL[1][k * kMaxK];
+                        pass = (dv[0] - m1 > tk[0]) & (dv[1] - m1 > tk[1]) & (dv[2] - m1 > tk[2]) &
+                               (dv[3] - m1 > tk[3]) & (dv[4] - m1 > tk[4]);
                     }
                     if (pass) {
                         // colour sums = n origin + sum u (origin (4R, 8G2, 8B2))

@@ -1,0 +1,30 @@
+#!/bin/bash
+# GPU box (round 5): identity + timing of the k-means++ Lloyd LDS-threshold + ring-push variant, and the
+# k_kmeans VALU count per variant (one PMC pass each, colours-only steps).
+set -u -o pipefail
+mkdir -p gpurun_out/r5l
+export TMPDIR=/tmp
+timeout -k 10 600 bash tools/debug/identity.sh > gpurun_out/r5l/identity.log 2>&1; echo "identity rc=$?"; cat gpurun_out/r5l/identity.log
+timeout -k 10 600 bash tools/debug/run_variants.sh --features colors || exit 1
+timeout -k 10 600 bash tools/debug/run_variants.sh || exit 1
+L=low_level_feature_extraction_amd/libllfe.so
+cp $L /tmp/libllfe_keep4.so
+for v in tools/debug/variants/libllfe_*.so; do
+    cp $v $L
+    rm -rf /tmp/kmv
+    timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES --kernel-trace -d /tmp/kmv -o run --output-format csv -- python3 bench.py --features colors \
+        --pipeline off --steps 2 --warmup 1 --cpu-baseline off --e2e-host-steps 0 --e2e-png-steps 0 --e2e-jpeg-steps 0 --per-class-steps 0 \
+        > gpurun_out/r5l/kmv.json 2> gpurun_out/r5l/kmv.err || { echo "pmc failed"; tail -5 gpurun_out/r5l/kmv.err; cp /tmp/libllfe_keep4.so $L; exit 1; }
+    f=$(find /tmp/kmv -name '*counter_collection.csv' | head -1)
+    python3 - "$f" $(basename $v) <<'PY'
+import csv, sys, collections
+agg = collections.defaultdict(float); disp = set()
+for r in csv.DictReader(open(sys.argv[1])):
+    if "k_kmeans<" not in r["Kernel_Name"]:
+        continue
+    agg[r["Counter_Name"]] += float(r["Counter_Value"]); disp.add(r["Dispatch_Id"])
+n = max(len(disp), 1)
+print(sys.argv[2], "k_kmeans per launch", {c: "%.4g" % (v / n) for c, v in sorted(agg.items())})
+PY
+done
+cp /tmp/libllfe_keep4.so $L
