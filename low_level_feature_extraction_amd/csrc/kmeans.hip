@@ -300,6 +300,13 @@ __device__ __forceinline__ uint32_t lane_sel(unsigned long long m, uint32_t a, u
     return r;
 }
 
+// clear bit `b` of a wave-uniform 64-bit mask with one s_bitset0_b64 (fm &= fm - 1 is three
+// scalar ops: the 64-bit subtract is two)
+__device__ __forceinline__ unsigned long long clear_bit(unsigned long long m, int b) {
+    asm("s_bitset0_b64 %0, %1" : "+s"(m) : "s"(b));
+    return m;
+}
+
 // the colour of mask bit `lane` relative to its cube's origin (bit = i*16 + j*4 + b)
 __device__ __forceinline__ uint32_t lane_offset(int lane) {
     return ((uint32_t)(lane >> 4) << 16) | ((uint32_t)((lane >> 2) & 3) << 8) | (uint32_t)(lane & 3);
@@ -871,7 +878,7 @@ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, int K, uint64
                     for (int u = 0; u < LLFE_KM_UNROLL; u++) {
                         if (u > 0 && !fm) break;
                         const int src = __builtin_ctzll(fm);
-                        fm &= fm - 1;
+                        fm = clear_bit(fm, src);
                         const unsigned long long m =
                             ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(mhi, src) << 32) |
                             (uint32_t)__builtin_amdgcn_readlane(mlo, src);
@@ -1602,7 +1609,7 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
                     for (int u = 0; u < LLFE_KM_UNROLL; u++) {
                         if (u > 0 && !fm) break;
                         const int src = __builtin_ctzll(fm);
-                        fm &= fm - 1;
+                        fm = clear_bit(fm, src);
                         push(src);
                     }
                     LABEL_FULL();
