@@ -14,13 +14,13 @@
 // lanes, 2 on each side are halo (8 columns): every horizontal neighbour a pixel
 // needs -- blur5 +-2, Sobel / NMS +-1, Gauss11 +-5 on the blurred row -- comes from lanes
 // L-2 .. L+2 through DPP wave shifts, so 240 columns per wave are exact (1920 = 8 x
-// 240).  Vertical neighbours live in registers: the gray rows of the blur5 in a
-// 5-row ring, and the blurred rows, the Canny magnitude rows and the CV_32F row-pass
-// results of Gauss11 in 11-slot rings indexed by the row modulo 11 -- the row loop is
-// unrolled 11 times, so every ring slot is a fixed register.  One BGR row is loaded
-// per step (3 dwords per lane, coalesced, two steps ahead), each pixel is read from
-// HBM once plus a 10/270 row halo (the 16/256-column halo of neighbouring strips hits L2), and nothing goes through LDS:
-// no barriers, no halo recomputation beyond those margins.
+// 240).  Vertical neighbours live in registers, in rings whose lengths divide the
+// 12-step unroll of the row loop (input rows 3, gray rows 6, blurred rows 6, CV_32F
+// row-pass results 12, magnitude rows 3), so every ring slot is a fixed register and no
+// step moves ring data.  One BGR row is loaded per step (3 dwords per lane, coalesced, two
+// steps ahead), each pixel is read from HBM once plus a 10/216-row halo (the
+// 16/256-column halo of neighbouring strips hits L2), and nothing goes through LDS: no
+// barriers, no halo recomputation beyond those margins.
 //
 // Per step (blur row c = clamp(t, 0, H-1) enters; REPLICATE of the blurred image):
 //   gray row reflect101(c + 2) -> vertical then horizontal blur5 (exact integer, any
@@ -558,9 +558,12 @@ __global__ __launch_bounds__(256) void k_stream_shadow_reduce(const uint2 *__res
 
 void stream_geometry(int h, int w, int &strips, int &segs, int &seg_rows) {
     strips = (w + kStripW - 1) / kStripW;
-    // ~270-row segments: 10 extra rows per segment (3.7 %), 32 waves per 1080p image
+    // ~216-row segments (40 waves per 1080p image, 16 fill rows per segment).  Measured after
+    // round 5's candidate-lane fix (profiles/r5/r5p/, isolated 512 x 1080p): 270 rows 2.81 ms,
+    // 216 2.60-2.63, 180 2.63-2.64, 135 2.75-2.78, 108 2.58-2.61 (round 2, when every row ran
+    // the NMS code, 270 was the best)
 #ifndef LLFE_ST_SEG
-#define LLFE_ST_SEG 270
+#define LLFE_ST_SEG 216
 #endif
     segs = std::max(1, (h + LLFE_ST_SEG - 1) / LLFE_ST_SEG);
     seg_rows = (h + segs - 1) / segs;

@@ -27,7 +27,7 @@ for r in rows:
     disp.add(r["Dispatch_Id"])
 n = max(len(disp), 1)
 per = {k: v / n for k, v in agg.items()}
-steps = 32 * 278.75 * 512  # waves x full row steps (ya - 5 .. yb + 5, from row 0) per launch, 512 x 1080p
+steps = 40 * 225.0 * 512  # waves x full row steps (ya - 5 .. yb + 5, from row 0) per launch, 512 x 1080p, 216-row segments
 print(sys.argv[2], "dispatches", n, {k: "%.4g" % v for k, v in sorted(per.items())},
       "VALU per wave-step %.1f" % (per.get("SQ_INSTS_VALU", 0) / steps))
 PY
