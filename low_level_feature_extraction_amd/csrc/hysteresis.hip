@@ -6,8 +6,11 @@
 // union-find in a fixed number of launches instead of relaunching a flood fill until it
 // stops moving (weak-pixel networks in noisy images percolate across the whole frame):
 //
-//   k_ccl_local   per 64x64 tile: LDS union-find over candidate pixels (class != 1),
-//                 local root per pixel (u16), strong flag per root, root list per tile
+//   k_tile_list   the tiles the stencil flagged (a class != 1 pixel inside) as a list
+//   k_ccl_local   per flagged 64x64 tile (a work counter hands them out): LDS union-find
+//                 over candidate pixels (class != 1), local root per pixel (u16), strong
+//                 flag per root, root list per tile.  Without the stencil's flags (a class
+//                 map from elsewhere): one workgroup per tile of the batch
 //   k_ccl_border  atomicMin union of the global ids of 8-neighbour candidates that sit
 //                 in different tiles (tile right column / bottom row)
 //   k_ccl_flatten every local root -> its global root (one hop); strong flags OR-ed
@@ -79,17 +82,43 @@ __device__ __forceinline__ void g_union(int *P, int a, int b) {
     }
 }
 
+// One tile's local components (below).  kList: the grid loops over the tiles the stencil
+// flagged (llfe_internal.h HystWork::tflag) instead of one workgroup per tile of the batch.
+template <bool kList>
 __global__ __launch_bounds__(NT) void k_ccl_local(const uint8_t *__restrict__ cls, int H, int W, int ntx, int nty,
                                                   uint16_t *__restrict__ lab, int *__restrict__ parent,
                                                   uint8_t *__restrict__ sroot, uint16_t *__restrict__ roots,
                                                   int *__restrict__ nroots, int *__restrict__ tlist,
-                                                  int *__restrict__ tcount) {
+                                                  int *__restrict__ tcount, const int *__restrict__ ftlist,
+                                                  int *__restrict__ ftcount) {
     __shared__ int L[TP];
     __shared__ uint32_t sflag[TP / 32];
     __shared__ __attribute__((aligned(16))) uint8_t cb[TP];
     __shared__ int cnt;
-    const int tid = threadIdx.x, img = blockIdx.y, t = blockIdx.x;
+    __shared__ int s_it;
     const int ntiles = ntx * nty;
+    const int nft = kList ? ftcount[0] : 1;
+    for (int it0 = 0;; it0++) {
+    // (tid opaque per tile: otherwise the compiler hoists the 16 per-k pixel offsets of
+    // every address out of the tile loop -- 173 VGPRs instead of 40)
+    int tid = threadIdx.x;
+    if (kList) asm volatile("" : "+v"(tid));
+    int img, t;
+    if (kList) {
+        // tiles handed out by a counter (ftcount[1]): the workgroups that start last do
+        // not each bring a fixed share of tiles into the launch's tail
+        if (tid == 0) s_it = atomicAdd(&ftcount[1], 1);
+        __syncthreads();
+        const int it = s_it;  // (read by every thread before the next barrier of this tile)
+        if (it >= nft) break;
+        const int tt = ftlist[it];
+        img = tt / ntiles;
+        t = tt % ntiles;
+    } else {
+        if (it0) break;
+        img = blockIdx.y;
+        t = blockIdx.x;
+    }
     const int tx0 = (t % ntx) * TW, ty0 = (t / ntx) * TH;
     const uint8_t *c = cls + (size_t)img * H * W;
     bool any = false;
@@ -113,7 +142,7 @@ __global__ __launch_bounds__(NT) void k_ccl_local(const uint8_t *__restrict__ cl
     // the later kernels skip the tile on nroots == 0
     if (!__syncthreads_or(any)) {
         if (tid == 0) nroots[(size_t)img * ntiles + t] = 0;
-        return;
+        continue;  // (no thread touches cb / L / sflag / cnt after the barrier)
     }
     uint8_t v[TP / NT];
 #pragma unroll
@@ -158,11 +187,41 @@ __global__ __launch_bounds__(NT) void k_ccl_local(const uint8_t *__restrict__ cl
             roots[gbase + pos] = (uint16_t)i;
         }
     }
-    __syncthreads();
+    __syncthreads();  // (also orders this tile's LDS reads before the next tile's writes)
     if (tid == 0) {
         nroots[(size_t)img * ntiles + t] = cnt;
         tlist[atomicAdd(tcount, 1)] = img * ntiles + t;  // the later passes visit only these
     }
+    }
+}
+
+// The flagged tiles (a byte per tile, set by the stencil where a class != 1 pixel sits)
+// as a list: one atomic per 1024-tile block.
+constexpr int LT = 1024;
+__global__ __launch_bounds__(LT) void k_tile_list(const uint8_t *__restrict__ tflag, int total,
+                                                  int *__restrict__ ftlist, int *__restrict__ ftcount) {
+    __shared__ int wbase[LT / 64];
+    const int i = blockIdx.x * LT + threadIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const bool f = i < total && tflag[i];
+    const unsigned long long m = __ballot(f);
+    if (lane == 0) wbase[wid] = __popcll(m);
+    __syncthreads();
+    if (wid == 0) {
+        const int c = lane < LT / 64 ? wbase[lane] : 0;
+        int x = c;
+#pragma unroll
+        for (int off = 1; off < LT / 64; off <<= 1) {
+            const int y = __shfl_up(x, off);
+            if (lane >= off) x += y;
+        }
+        const int tot = __shfl(x, LT / 64 - 1);
+        int base = 0;
+        if (lane == 0 && tot) base = atomicAdd(ftcount, tot);
+        base = __shfl(base, 0);
+        if (lane < LT / 64) wbase[lane] = base + x - c;
+    }
+    __syncthreads();
+    if (f) ftlist[wbase[wid] + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = i;
 }
 
 __device__ __forceinline__ int gid_of(const uint16_t *lab, int img, int H, int W, int ntx, int ntiles, int y, int x) {
@@ -358,9 +417,22 @@ hipError_t launch_ccl(const uint8_t *cls, int n, int h, int w, const HystWork &w
     hipError_t e;
     if ((e = hipMemsetAsync(wk.tcount, 0, sizeof(int), s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(wk.ebits, 0, sizeof(uint64_t) * words, s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_ccl_local, grid, dim3(NT), 0, s, cls, h, w, ntx, nty, wk.lab, wk.parent, wk.sroot, wk.roots,
-                       wk.nroots, wk.tlist, wk.tcount);
     const dim3 lgrid((unsigned)std::min<int64_t>((int64_t)ntiles * n, kListBlocks));
+    if (wk.tflag) {
+        // only the tiles the stencil flagged: no workgroup per empty tile, no read of its
+        // class bytes (85 % of the ui / photo mix)
+        if ((e = hipMemsetAsync(wk.ftcount, 0, 2 * sizeof(int), s)) != hipSuccess) return e;
+        const int total = ntiles * n;
+        hipLaunchKernelGGL(k_tile_list, dim3((unsigned)((total + LT - 1) / LT)), dim3(LT), 0, s, wk.tflag, total,
+                           wk.ftlist, wk.ftcount);
+        // (a work counter hands out the tiles: 2048 workgroups cover the 7 x 256 resident slots)
+        const dim3 qgrid((unsigned)std::min<int64_t>((int64_t)ntiles * n, 2048));
+        hipLaunchKernelGGL(k_ccl_local<true>, qgrid, dim3(NT), 0, s, cls, h, w, ntx, nty, wk.lab, wk.parent, wk.sroot,
+                           wk.roots, wk.nroots, wk.tlist, wk.tcount, (const int *)wk.ftlist, wk.ftcount);
+    } else {
+        hipLaunchKernelGGL(k_ccl_local<false>, grid, dim3(NT), 0, s, cls, h, w, ntx, nty, wk.lab, wk.parent, wk.sroot,
+                           wk.roots, wk.nroots, wk.tlist, wk.tcount, (const int *)nullptr, (int *)nullptr);
+    }
     hipLaunchKernelGGL(k_ccl_border, lgrid, dim3(128), 0, s, cls, wk.lab, h, w, ntx, nty, wk.tlist, wk.tcount,
                        wk.parent);
     hipLaunchKernelGGL(k_ccl_flatten, lgrid, dim3(NT), 0, s, wk.tlist, wk.tcount, wk.roots, wk.nroots, wk.parent,

@@ -207,11 +207,12 @@ constexpr int kMaxSlots = 3;
 
 // device workspace of one chunk in flight
 struct Work {
-    DevBuf<uint8_t> d_in, d_cls, d_sroot;
+    DevBuf<uint8_t> d_in, d_cls, d_sroot, d_tflag;  // d_tflag: the stencil's hysteresis tile flags
+    bool tflag_valid = false;  // d_tflag belongs to the class map in d_cls (stencil_params)
     DevBuf<int8_t> d_noise, d_nfield;  // d_nfield: the launch's noise field (unique.hip)
     DevBuf<uint64_t> d_bits, d_ebits;
     DevBuf<unsigned long long> d_shadow;
-    DevBuf<int> d_order, d_parent, d_nroots, d_tlist;
+    DevBuf<int> d_order, d_parent, d_nroots, d_tlist, d_ftlist;
     DevBuf<uint16_t> d_lab, d_roots;
     DevBuf<uint32_t> d_raw, d_keys, d_kscratch, d_pmeta, d_tstrong, d_segtab;  // d_segtab: k_uq_scatter's run table
     DevBuf<CubeEnt> d_segcubes, d_cubes;
@@ -549,8 +550,27 @@ int hyst_work(llfe_ctx *ctx, Work &W, int n, int h, int w, HystWork *out) {
     HIPCHK(ctx, W.d_tstrong.ensure(hysteresis_tiles(n, h, w) * hysteresis_tile_words()));
     HIPCHK(ctx, W.d_ebits.ensure((size_t)n * h * words_per_row(w)));
     HIPCHK(ctx, W.d_tlist.ensure(tiles + 1));
+    HIPCHK(ctx, W.d_ftlist.ensure(tiles + 2));
     *out = HystWork{W.d_lab.p,     W.d_parent.p, W.d_sroot.p,       W.d_roots.p,   W.d_nroots.p,
-                    W.d_tstrong.p, W.d_ebits.p,  W.d_tlist.p + 1, W.d_tlist.p};
+                    W.d_tstrong.p, W.d_ebits.p,  W.d_tlist.p + 1, W.d_tlist.p,
+                    W.tflag_valid ? W.d_tflag.p : nullptr, W.d_ftlist.p + 2, W.d_ftlist.p};
+    W.tflag_valid = false;  // (one hysteresis pass per stencil launch)
+    return LLFE_OK;
+}
+
+// The stencil parameters of a class-map launch into W.d_cls: the hysteresis tile flags
+// (zeroed here, on s) that let the hysteresis skip the tiles without a Canny candidate.
+int stencil_params(llfe_ctx *ctx, Work &W, int n, int h, int w, hipStream_t s, StencilParams *sp) {
+    *sp = ctx->sp;
+    W.tflag_valid = false;
+    // LLFE_HYST_TILE_FLAGS=0: no flags, the hysteresis visits every tile (its test path)
+    if (const char *e = getenv("LLFE_HYST_TILE_FLAGS"))
+        if (!strcmp(e, "0")) return LLFE_OK;
+    const size_t tiles = (size_t)n * tiles_x(w) * ((h + 63) / 64);
+    HIPCHK(ctx, W.d_tflag.ensure(tiles));
+    HIPCHK(ctx, hipMemsetAsync(W.d_tflag.p, 0, tiles, s));
+    sp->tflag = W.d_tflag.p;
+    W.tflag_valid = true;
     return LLFE_OK;
 }
 
@@ -824,11 +844,16 @@ int enqueue_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_
     if (ctx->w_mask_slot[q] >= 0) HIPCHK(ctx, hipStreamWaitEvent(s, ctx->mask_done[ctx->w_mask_slot[q]], 0));
     if (want_shp || want_shd) {
         HIPCHK(ctx, W.d_shadow.ensure(2 * (size_t)n + shadow_tiles(n, h, w)));
-        if (want_shp) HIPCHK(ctx, W.d_cls.ensure((size_t)n * P));
+        StencilParams sp = ctx->sp;
+        if (want_shp) {
+            HIPCHK(ctx, W.d_cls.ensure((size_t)n * P));
+            rc = stencil_params(ctx, W, n, h, w, s, &sp);
+            if (rc) return rc;
+        }
         TIMED(ctx, s, "k_stencil", (double)n * P * (3 + (want_shp ? 1 : 0)),
               launch_stencil(img, n, h, w, want_shp ? W.d_cls.p : nullptr, nullptr,
                              want_shd ? W.d_shadow.p : nullptr, want_shd ? W.d_shadow.p + n : nullptr,
-                             (uint2 *)(W.d_shadow.p + 2 * n), ctx->sp, s));
+                             (uint2 *)(W.d_shadow.p + 2 * n), sp, s));
     }
     // shapes + shadows go to the host (event mask_done) while the GPU is still in this
     // chunk's colour stage, so contour tracing overlaps k-means
@@ -927,7 +952,9 @@ int redo_masks(llfe_ctx *ctx, const llfe_batch *b, int i0, int n, hipStream_t s)
     if (rc) return rc;
     HIPCHK(ctx, W.d_cls.ensure((size_t)n * h * w));
     HIPCHK(ctx, W.d_bits.ensure((size_t)n * h * words_per_row(w)));
-    HIPCHK(ctx, launch_stencil(img, n, h, w, W.d_cls.p, nullptr, nullptr, nullptr, nullptr, ctx->sp, s));
+    StencilParams sp;
+    if ((rc = stencil_params(ctx, W, n, h, w, s, &sp))) return rc;
+    HIPCHK(ctx, launch_stencil(img, n, h, w, W.d_cls.p, nullptr, nullptr, nullptr, nullptr, sp, s));
     return run_hysteresis_dilate(ctx, W, n, h, w, W.d_bits.p, nullptr, s);
 }
 
@@ -1101,6 +1128,14 @@ int llfe_init(int device, llfe_ctx **out) {
         if (!strcmp(cm, "host")) c->gpu_contours = false;
     }
     gauss_kernel_f32(11, c->sp.k11);
+    {
+        static const float kG11[11] = {LLFE_GAUSS11_F32};
+        if (std::memcmp(kG11, c->sp.k11, sizeof(kG11)) != 0) {  // (an invariant of this build)
+            std::fprintf(stderr, "llfe: getGaussianKernel(11) differs from the stencil's constants\n");
+            llfe_destroy(c);
+            return LLFE_ERR_UNSUPPORTED;
+        }
+    }
     c->pool = new Pool(default_threads() - 1);
     int nt = c->pool->size() + 1;
     c->work.resize(nt);
@@ -1547,8 +1582,11 @@ int llfe_shape_mask(llfe_ctx *ctx, const uint8_t *bgr, uint8_t *mask, int32_t n,
     hipStream_t s = (hipStream_t)stream;
     Work &W = ctx->ws[0];  // stage entry points run on the caller's stream, slot 0
     HIPCHK(ctx, W.d_cls.ensure((size_t)n * h * w));
-    HIPCHK(ctx, launch_stencil(bgr, n, h, w, W.d_cls.p, nullptr, nullptr, nullptr, nullptr, ctx->sp, s));
-    int rc = run_hysteresis_dilate(ctx, W, n, h, w, nullptr, mask, s);
+    StencilParams sp;
+    int rc = stencil_params(ctx, W, n, h, w, s, &sp);
+    if (rc) return rc;
+    HIPCHK(ctx, launch_stencil(bgr, n, h, w, W.d_cls.p, nullptr, nullptr, nullptr, nullptr, sp, s));
+    rc = run_hysteresis_dilate(ctx, W, n, h, w, nullptr, mask, s);
     if (rc) return rc;
     HIPCHK(ctx, hipStreamSynchronize(s));
     ctx->prof.collect(-2);
@@ -1565,9 +1603,12 @@ int llfe_canny(llfe_ctx *ctx, const uint8_t *bgr, uint8_t *edges, int32_t n, int
     hipStream_t s = (hipStream_t)stream;
     Work &W = ctx->ws[0];
     HIPCHK(ctx, W.d_cls.ensure((size_t)n * h * w));
-    HIPCHK(ctx, launch_stencil(bgr, n, h, w, W.d_cls.p, nullptr, nullptr, nullptr, nullptr, ctx->sp, s));
+    StencilParams sp;
+    int rc = stencil_params(ctx, W, n, h, w, s, &sp);
+    if (rc) return rc;
+    HIPCHK(ctx, launch_stencil(bgr, n, h, w, W.d_cls.p, nullptr, nullptr, nullptr, nullptr, sp, s));
     HystWork wk;
-    const int rc = hyst_work(ctx, W, n, h, w, &wk);
+    rc = hyst_work(ctx, W, n, h, w, &wk);
     if (rc) return rc;
     HIPCHK(ctx, launch_canny_edges(W.d_cls.p, n, h, w, wk, edges, s));
     HIPCHK(ctx, hipStreamSynchronize(s));

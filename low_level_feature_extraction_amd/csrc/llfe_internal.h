@@ -15,8 +15,17 @@ namespace llfe {
 constexpr int kTileW = 64;
 constexpr int kTileH = 32;
 
+// getGaussianKernel(11, 0, CV_32F) (gauss_kernel_f32(11) in llfe_api.cpp, checked equal at
+// llfe_create): the row-streaming stencil takes these as constants
+#define LLFE_GAUSS11_F32                                                                                     \
+    0x1.20c256p-7f, 0x1.bcb86ap-6f, 0x1.0ab50ap-4f, 0x1.f2464cp-4f, 0x1.6a7e1ep-3f, 0x1.9ac20ap-3f,          \
+        0x1.6a7e1ep-3f, 0x1.f2464cp-4f, 0x1.0ab50ap-4f, 0x1.bcb86ap-6f, 0x1.20c256p-7f
+
 struct StencilParams {
     float k11[11];  // CV_32F GaussianBlur 11x11 sigma 0 kernel (adaptiveThreshold)
+    // (row-streaming kernel, with cls) n x ceil(h / 64) x ceil(w / 64) bytes, zeroed by the
+    // caller: set to 1 for every 64 x 64 hysteresis tile holding a class != 1 pixel
+    uint8_t *tflag;
 };
 
 // shape pyc @L18-24 + shadow pyc @L8-21 for a packed NHWC batch.
@@ -56,6 +65,9 @@ struct HystWork {
     uint64_t *ebits;    // n x h x words_per_row, edges before the dilate
     int *tlist;         // tiles with a Canny candidate (n * tiles) and their count
     int *tcount;
+    const uint8_t *tflag;  // (may be null) the stencil's tile flags (StencilParams::tflag)
+    int *ftlist;           // with tflag: the flagged tiles (n * tiles),
+    int *ftcount;          // their count and a work counter (two ints)
 };
 size_t hysteresis_ids(int n, int h, int w);    // >= the GPU contour pass's ids as well
 size_t hysteresis_tiles(int n, int h, int w);  // hysteresis tiles (<= n * tiles_x * tiles_y)

@@ -35,6 +35,8 @@
 namespace llfe {
 namespace {
 
+__device__ __constant__ constexpr float kGauss11[11] = {LLFE_GAUSS11_F32};
+
 // (analysis builds only, -DLLFE_ST_MARK: stage markers in the ISA for the per-stage
 // instruction table of tools/stencil_isa.py)
 // ST_PIN(x) materialises a stage's result before the next marker, so code motion cannot
@@ -336,9 +338,11 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, LLFE_ST_MINW) void k_stencil_s
         in_02 = ((unsigned)x < (unsigned)W ? 1u : 0u) | ((unsigned)(x + 2) < (unsigned)W ? 0x10000u : 0u);
         in_13 = ((unsigned)(x + 1) < (unsigned)W ? 1u : 0u) | ((unsigned)(x + 3) < (unsigned)W ? 0x10000u : 0u);
     }
-    float k11[11];
-#pragma unroll
-    for (int k = 0; k < 11; k++) k11[k] = prm.k11[k];
+    // the CV_32F 11-tap Gaussian (ksize 11, sigma 0: OpenCV's getGaussianKernel, computed in
+    // double and rounded to float) as constants, not kernel arguments: the compiler can
+    // rematerialise them instead of holding 11 SGPRs through the loop (the kernel is at the
+    // SGPR limit).  llfe_create checks prm.k11 against this table (kGauss11).
+    const float *k11 = kGauss11;
 
     // Row steps t (one blurred row enters per step; the loop is unrolled kU = 12 times and
     // every ring's length divides 12, so each ring slot is a fixed register and no step
@@ -373,6 +377,12 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, LLFE_ST_MINW) void k_stencil_s
         Mc[k] = false;
     }
     uint32_t lsum = 0, lcnt = 0;
+    // hysteresis tile flags (prm.tflag): an output lane whose NMS row holds a class != 1
+    // pixel sets its 64 x 64 tile's byte (measured against OR-ing a ballot per row and
+    // storing once per 64-row band: the per-row stores cost the stencil nothing, the band
+    // flushes +90 us per 512 x 1080p through their register pressure)
+    const int tf_ntx = (W + 63) >> 6;
+    uint8_t *const tf_img = CLS && prm.tflag ? prm.tflag + (size_t)img_i * ((H + 63) >> 6) * tf_ntx : nullptr;
 
     for (int tb = tb0; tb < t_end; tb += kU) {
 #pragma unroll
@@ -441,7 +451,10 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, LLFE_ST_MINW) void k_stencil_s
                 if (yn >= ya && yn < yb) {
                     const int ia = (k + 1) % 3, im = (k + 2) % 3, ib = k % 3;
                     uint32_t o = 0x01010101u;
-                    if (Mc[im]) o = nms4(Mlo[ia], Mhi[ia], Mlo[im], Mhi[im], Mlo[ib], Mhi[ib]);
+                    if (Mc[im]) {
+                        o = nms4(Mlo[ia], Mhi[ia], Mlo[im], Mhi[im], Mlo[ib], Mhi[ib]);
+                        if (tf_img && out_lane && o != 0x01010101u) tf_img[(yn >> 6) * tf_ntx + (x >> 6)] = 1;
+                    }
                     ST_PIN(o);
                     ST_MARK(store);
                     if (out_fast) {

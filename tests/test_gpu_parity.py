@@ -65,6 +65,19 @@ def test_shape_mask(backend, orc, h, w):
         assert np.array_equal(got[i], exp), f"mismatch {(got[i] != exp).sum()} px"
 
 
+@pytest.mark.parametrize("h,w", [(5, 7), (65, 130), (270, 480), (1080, 1920)])
+def test_shape_mask_without_tile_flags(backend, orc, h, w, monkeypatch):
+    """The hysteresis without the stencil's tile flags (one workgroup per tile, the path a
+    class map from elsewhere takes) gives the same masks as with them (the default)."""
+    x = np.concatenate([_imgs(h, w), np.stack([_smooth_random(h, w, 3)])])
+    monkeypatch.setenv("LLFE_HYST_TILE_FLAGS", "0")
+    got = backend.shape_mask(x).cpu().numpy()
+    monkeypatch.delenv("LLFE_HYST_TILE_FLAGS")
+    assert np.array_equal(got, backend.shape_mask(x).cpu().numpy())
+    for i in range(len(x)):
+        assert np.array_equal(got[i], orc.shape_mask(x[i]))
+
+
 @pytest.mark.parametrize("h,w", SIZES)
 def test_canny(backend, orc, h, w):
     x = _imgs(h, w)
