@@ -6,18 +6,21 @@
 // union-find in a fixed number of launches instead of relaunching a flood fill until it
 // stops moving (weak-pixel networks in noisy images percolate across the whole frame):
 //
-//   k_tile_list   the tiles the stencil flagged (a class != 1 pixel inside) as a list
-//   k_ccl_local   per flagged 64x64 tile (a work counter hands them out): LDS union-find
-//                 over candidate pixels (class != 1), local root per pixel (u16), strong
-//                 flag per root, root list per tile.  Without the stencil's flags (a class
-//                 map from elsewhere): one workgroup per tile of the batch
+//   k_tile_list   the tiles the stencil flagged (a class != 1 pixel inside) as a list (every
+//                 tile when the class map comes without flags)
+//   k_ccl_runs    per listed 64x64 tile, one wave (lane = row, tiles from a work counter):
+//                 union-find over the rows' candidate runs (class != 1; node = the run's
+//                 first pixel) in LDS, local root per run (lab), strong flag per root, root
+//                 list per tile, and the edge words the tile decides alone: the runs of a
+//                 component with a strong pixel in the tile
 //   k_ccl_border  atomicMin union of the global ids of 8-neighbour candidates that sit
 //                 in different tiles (tile right column / bottom row)
 //   k_ccl_flatten every local root -> its global root (one hop); strong flags OR-ed
 //                 into the global root
-//   k_ccl_strong  per tile: bit per local root whose global root is strong
-//   k_ccl_edge    edge = strong || (maybe && root strong), packed per 64-pixel row
-//                 segment with __ballot (no halo)
+//   k_ccl_strong  per tile: bit per local root promoted by the global unions (not strong
+//                 in its tile, strong through another), and the tiles with one listed
+//   k_ccl_edge    per listed tile (one wave): the runs with a promoted root OR-ed into the
+//                 edge words
 //   k_bits_dilate 3x3 dilate on the packed words (shifts and ORs)
 #include <algorithm>
 
@@ -26,16 +29,27 @@
 namespace llfe {
 namespace {
 
-// 64 x 64 tiles (the GPU contour pass keeps 64 x 32: contours_gpu.hip): the 85 % of tiles
-// without a Canny candidate cost one workgroup launch each in k_ccl_local, so half as many
-// tiles: hysteresis 1.61 -> 1.34 ms per 512 x 1080p
+// 64 x 64 tiles (the GPU contour pass keeps 64 x 32: contours_gpu.hip): one 64-bit word per
+// tile row (round 3: 64 x 64 instead of 64 x 32 tiles, hysteresis 1.61 -> 1.34 ms per 512 x
+// 1080p, when every tile still cost a workgroup launch)
 constexpr int TW = kTileW, TH = 64, TP = TW * TH;  // 4096 pixels per tile
 inline int htiles_y(int h) { return (h + TH - 1) / TH; }
 constexpr int NT = 256;
 static_assert(TW == 64, "k_ccl_dilate packs one 64-pixel word per tile row");
 
+#ifndef LLFE_HYST_WATCHDOG
+#define LLFE_HYST_WATCHDOG 0  // (debug builds) bounded union-find loops, printf on overrun
+#endif
 __device__ __forceinline__ int lds_find(int *L, int a) {
+#if LLFE_HYST_WATCHDOG
+    for (int guard = 0;; guard++) {
+        if (guard > 8192) {
+            printf("llfe watchdog: lds_find a=%d L[a]=%d\n", a, L[a]);
+            return a;
+        }
+#else
     for (;;) {
+#endif
         int p = __hip_atomic_load(L + a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (p == a) return a;
         a = p;
@@ -43,7 +57,15 @@ __device__ __forceinline__ int lds_find(int *L, int a) {
 }
 
 __device__ __forceinline__ void lds_union(int *L, int a, int b) {
+#if LLFE_HYST_WATCHDOG
+    for (int guard = 0;; guard++) {
+        if (guard > 8192) {
+            printf("llfe watchdog: lds_union a=%d b=%d\n", a, b);
+            return;
+        }
+#else
     for (;;) {
+#endif
         a = lds_find(L, a);
         b = lds_find(L, b);
         if (a == b) return;
@@ -59,7 +81,15 @@ __device__ __forceinline__ void lds_union(int *L, int a, int b) {
 }
 
 __device__ __forceinline__ int g_find(int *P, int a) {
+#if LLFE_HYST_WATCHDOG
+    for (int guard = 0;; guard++) {
+        if (guard > (1 << 22)) {
+            printf("llfe watchdog: g_find a=%d P[a]=%d\n", a, P[a]);
+            return a;
+        }
+#else
     for (;;) {
+#endif
         int p = __hip_atomic_load(P + a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (p == a) return a;
         a = p;
@@ -67,7 +97,15 @@ __device__ __forceinline__ int g_find(int *P, int a) {
 }
 
 __device__ __forceinline__ void g_union(int *P, int a, int b) {
+#if LLFE_HYST_WATCHDOG
+    for (int guard = 0;; guard++) {
+        if (guard > (1 << 20)) {
+            printf("llfe watchdog: g_union a=%d b=%d\n", a, b);
+            return;
+        }
+#else
     for (;;) {
+#endif
         a = g_find(P, a);
         b = g_find(P, b);
         if (a == b) return;
@@ -82,116 +120,170 @@ __device__ __forceinline__ void g_union(int *P, int a, int b) {
     }
 }
 
-// One tile's local components (below).  kList: the grid loops over the tiles the stencil
-// flagged (llfe_internal.h HystWork::tflag) instead of one workgroup per tile of the batch.
-template <bool kList>
-__global__ __launch_bounds__(NT) void k_ccl_local(const uint8_t *__restrict__ cls, int H, int W, int ntx, int nty,
-                                                  uint16_t *__restrict__ lab, int *__restrict__ parent,
-                                                  uint8_t *__restrict__ sroot, uint16_t *__restrict__ roots,
-                                                  int *__restrict__ nroots, int *__restrict__ tlist,
-                                                  int *__restrict__ tcount, const int *__restrict__ ftlist,
-                                                  int *__restrict__ ftcount) {
-    __shared__ int L[TP];
-    __shared__ uint32_t sflag[TP / 32];
-    __shared__ __attribute__((aligned(16))) uint8_t cb[TP];
-    __shared__ int cnt;
-    __shared__ int s_it;
-    const int ntiles = ntx * nty;
-    const int nft = kList ? ftcount[0] : 1;
-    for (int it0 = 0;; it0++) {
-    // (tid opaque per tile: otherwise the compiler hoists the 16 per-k pixel offsets of
-    // every address out of the tile loop -- 173 VGPRs instead of 40)
-    int tid = threadIdx.x;
-    if (kList) asm volatile("" : "+v"(tid));
-    int img, t;
-    if (kList) {
-        // tiles handed out by a counter (ftcount[1]): the workgroups that start last do
-        // not each bring a fixed share of tiles into the launch's tail
-        if (tid == 0) s_it = atomicAdd(&ftcount[1], 1);
-        __syncthreads();
-        const int it = s_it;  // (read by every thread before the next barrier of this tile)
-        if (it >= nft) break;
-        const int tt = ftlist[it];
-        img = tt / ntiles;
-        t = tt % ntiles;
+// ------------------------------------------------------------------ run-based local CCL
+// One wave per listed tile, lane = tile row.  A row's candidates (class != 1) are a 64-bit
+// mask and its runs (maximal 1-bit sequences) the union-find nodes -- node id = row * 32 +
+// the run's rank in its row (< 2048: at most 32 runs in 64 pixels) -- united with the runs
+// of the row above that touch them 8-connectedly (the run widened by one pixel each side,
+// AND the row above).  A component's local id (lab, the roots list, parent / sroot at
+// tile base + id) is its root node.
+constexpr int RW = 4;  // waves (tiles in flight) per workgroup
+
+__device__ __forceinline__ unsigned long long bits_upto(int b) {  // bits 0..b (b in -1..63)
+    return b >= 63 ? ~0ull : ((1ull << (b + 1)) - 1ull);
+}
+// length of the 1-run of m starting at bit a (m bit a set)
+__device__ __forceinline__ int run_len(unsigned long long m, int a) {
+    const unsigned long long z = ~(m >> a);
+    return z ? __builtin_ctzll(z) : 64 - a;
+}
+
+// the row's candidate (class != 1) and strong (class 2) masks; zero outside the image
+__device__ __forceinline__ void row_masks(const uint8_t *__restrict__ cls, int img, int H, int W, int tx0, int y,
+                                          unsigned long long &C, unsigned long long &S) {
+    C = S = 0;
+    if (y >= H) return;
+    const uint8_t *row = cls + ((size_t)img * H + y) * W + tx0;
+    const int nx = min(64, W - tx0);
+    if (nx == 64 && (((uintptr_t)row) & 15) == 0) {
+        uint32_t d[16];
+#pragma unroll
+        for (int q = 0; q < 4; q++) *(uint4 *)&d[4 * q] = ((const uint4 *)row)[q];
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            // classes 0 / 1 / 2 per byte: candidate = byte != 1, strong = bit 1; the four
+            // bytes' flag bits (0, 8, 16, 24) gathered to bits 0..3
+            const uint32_t t1 = d[j] ^ 0x01010101u;
+            uint32_t c = (t1 | (t1 >> 1)) & 0x01010101u, s = (d[j] >> 1) & 0x01010101u;
+            c |= c >> 7;
+            s |= s >> 7;
+            c |= c >> 14;
+            s |= s >> 14;
+            C |= (unsigned long long)(c & 15u) << (4 * j);
+            S |= (unsigned long long)(s & 15u) << (4 * j);
+        }
     } else {
-        if (it0) break;
-        img = blockIdx.y;
-        t = blockIdx.x;
-    }
-    const int tx0 = (t % ntx) * TW, ty0 = (t / ntx) * TH;
-    const uint8_t *c = cls + (size_t)img * H * W;
-    bool any = false;
-    static_assert(TP == 16 * NT, "one 16-byte load per thread");
-    if ((W & 15) == 0 && tx0 + TW <= W) {  // one 16-byte load per thread, through LDS
-        const int row = tid >> 2, col = (tid & 3) * 16, y = ty0 + row;
-        const uint4 ones = make_uint4(0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u);
-        const uint4 w = y < H ? *(const uint4 *)(c + (size_t)y * W + tx0 + col) : ones;
-        any = (w.x ^ ones.x) | (w.y ^ ones.y) | (w.z ^ ones.z) | (w.w ^ ones.w);
-        *(uint4 *)&cb[row * TW + col] = w;
-    } else {
-        for (int k = 0; k < TP / NT; k++) {
-            const int i = tid + k * NT, y = ty0 + (i >> 6), x = tx0 + (i & 63);
-            cb[i] = (y < H && x < W) ? c[(size_t)y * W + x] : 1;
-            any |= cb[i] != 1;
+        for (int x = 0; x < nx; x++) {
+            const uint8_t b = row[x];
+            if (b != 1) C |= 1ull << x;
+            if (b == 2) S |= 1ull << x;
         }
     }
-    if (tid < TP / 32) sflag[tid] = 0;
-    if (tid == 0) cnt = 0;
-    // most tiles hold no Canny candidate (85 % over the ui / photo mix): no roots, and
-    // the later kernels skip the tile on nroots == 0
-    if (!__syncthreads_or(any)) {
-        if (tid == 0) nroots[(size_t)img * ntiles + t] = 0;
-        continue;  // (no thread touches cb / L / sflag / cnt after the barrier)
+}
+
+// Outputs as the per-pixel union-find had them (with node ids for pixel ids), except lab:
+// written at each run's first pixel, at x = 63 of the runs that end there, and over the
+// whole of rows 0 and 63 -- every pixel k_ccl_border reads (its tile's right column and
+// bottom row, the neighbours' left column and top row) and every run start k_ccl_edge
+// reads.  Plus the edge words the tile decides alone (runs whose local root holds a strong
+// pixel).
+constexpr int kNodes = 64 * 32;
+__device__ __forceinline__ void ccl_runs_tile(const uint8_t *__restrict__ cls, int H, int W, int ntx, int ntiles,
+                                              int wpr, int tt, int lane, int nb, int *P, uint32_t *sflag, int *cnt,
+                                              uint16_t *__restrict__ lab, int *__restrict__ parent,
+                                              uint8_t *__restrict__ sroot, uint16_t *__restrict__ roots,
+                                              int *__restrict__ nroots, int *__restrict__ tlist,
+                                              int *__restrict__ tcount, uint64_t *__restrict__ ebits) {
+    const int img = tt / ntiles, t = tt % ntiles;
+    const int tx0 = (t % ntx) * TW, ty0 = (t / ntx) * TH, y = ty0 + lane;
+    unsigned long long C, S;
+    row_masks(cls, img, H, W, tx0, y, C, S);
+    if (__ballot(C != 0) == 0) {  // (the tile list without the stencil's flags)
+        if (lane == 0) nroots[(size_t)img * ntiles + t] = 0;
+        return;
     }
-    uint8_t v[TP / NT];
-#pragma unroll
-    for (int k = 0; k < TP / NT; k++) {
-        const int i = tid + k * NT;
-        v[k] = cb[i];
-        L[i] = v[k] != 1 ? i : -1;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < TP / NT; k++) {
-        if (v[k] == 1) continue;
-        int i = tid + k * NT, ly = i >> 6, lx = i & 63;
-        if (lx > 0 && L[i - 1] >= 0) lds_union(L, i, i - 1);
-        if (ly > 0) {
-            if (lx > 0 && L[i - 65] >= 0) lds_union(L, i, i - 65);
-            if (L[i - 64] >= 0) lds_union(L, i, i - 64);
-            if (lx < 63 && L[i - 63] >= 0) lds_union(L, i, i - 63);
+    const unsigned long long starts = C & ~(C << 1);
+    const int nr = __popcll(starts);
+    for (int j = 0; j < nr; j++) P[nb + j] = nb + j;
+    sflag[lane] = 0;  // (kNodes / 32 = 64 words)
+    if (lane == 0) *cnt = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // unions with the runs of the row above (8-connected)
+    unsigned long long Cu = __shfl_up(C, 1);
+    if (lane == 0) Cu = 0;
+    const unsigned long long startsU = Cu & ~(Cu << 1);
+    int j = 0;
+    for (unsigned long long m = starts; m; m &= m - 1, j++) {
+        const int a = __builtin_ctzll(m), b = a + run_len(C, a) - 1;
+        const unsigned long long M = bits_upto(b) & ~bits_upto(a - 1);
+        unsigned long long ov = Cu & (M | (M << 1) | (M >> 1));
+        while (ov) {
+            const int x = __builtin_ctzll(ov);
+            // the run of the row above holding x: its rank = starts above at or below x, - 1
+            const int ju = __popcll(startsU & bits_upto(x)) - 1;
+            lds_union(P, nb + j, nb - 32 + ju);
+            ov &= ~bits_upto(x + run_len(Cu, x) - 1);
         }
     }
-    __syncthreads();
-    int r[TP / NT];
-#pragma unroll
-    for (int k = 0; k < TP / NT; k++) {
-        int i = tid + k * NT;
-        r[k] = -1;
-        if (v[k] == 1) continue;
-        r[k] = lds_find(L, i);
-        if (v[k] == 2) atomicOr(&sflag[r[k] >> 5], 1u << (r[k] & 31));
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // strong flags on the roots
+    j = 0;
+    for (unsigned long long m = starts; m; m &= m - 1, j++) {
+        const int a = __builtin_ctzll(m), b = a + run_len(C, a) - 1;
+        if (S & bits_upto(b) & ~bits_upto(a - 1)) {
+            const int r = lds_find(P, nb + j);
+            atomicOr(&sflag[r >> 5], 1u << (r & 31));
+        }
     }
-    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
     const size_t gbase = ((size_t)img * ntiles + t) * TP;
-#pragma unroll
-    for (int k = 0; k < TP / NT; k++) {
-        if (r[k] < 0) continue;
-        int i = tid + k * NT, ly = i >> 6, lx = i & 63;
-        lab[((size_t)img * H + ty0 + ly) * W + tx0 + lx] = (uint16_t)r[k];
-        if (r[k] == i) {
-            parent[gbase + i] = (int)(gbase + i);
-            sroot[gbase + i] = (sflag[i >> 5] >> (i & 31)) & 1;
-            int pos = atomicAdd(&cnt, 1);
-            roots[gbase + pos] = (uint16_t)i;
+    uint16_t *const lrow = lab + ((size_t)img * H + y) * W + tx0;
+    unsigned long long E = 0;
+    j = 0;
+    for (unsigned long long m = starts; m; m &= m - 1, j++) {
+        const int a = __builtin_ctzll(m), len = run_len(C, a), b = a + len - 1, id = nb + j;
+        const int r = lds_find(P, id);
+        if ((sflag[r >> 5] >> (r & 31)) & 1u) E |= bits_upto(b) & ~bits_upto(a - 1);
+        lrow[a] = (uint16_t)r;
+        if (lane == 0 || lane == 63)
+            for (int q = 1; q < len; q++) lrow[a + q] = (uint16_t)r;
+        else if (b == 63 && a < 63)
+            lrow[63] = (uint16_t)r;
+        if (r == id) {
+            parent[gbase + id] = (int)(gbase + id);
+            sroot[gbase + id] = (sflag[id >> 5] >> (id & 31)) & 1;  // bit 0: strong in the tile
+            roots[gbase + atomicAdd(cnt, 1)] = (uint16_t)id;
         }
     }
-    __syncthreads();  // (also orders this tile's LDS reads before the next tile's writes)
-    if (tid == 0) {
-        nroots[(size_t)img * ntiles + t] = cnt;
+    if (E) ebits[((size_t)img * H + y) * wpr + (tx0 >> 6)] = E;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+        nroots[(size_t)img * ntiles + t] = *cnt;
         tlist[atomicAdd(tcount, 1)] = img * ntiles + t;  // the later passes visit only these
     }
+}
+
+__global__ __launch_bounds__(64 * RW) void k_ccl_runs(const uint8_t *__restrict__ cls, int H, int W, int ntx, int nty,
+                                                    uint16_t *__restrict__ lab, int *__restrict__ parent,
+                                                    uint8_t *__restrict__ sroot, uint16_t *__restrict__ roots,
+                                                    int *__restrict__ nroots, int *__restrict__ tlist,
+                                                    int *__restrict__ tcount, const int *__restrict__ ftlist,
+                                                    int *__restrict__ ftcount, uint64_t *__restrict__ ebits) {
+    __shared__ int Pall[RW][kNodes];
+    __shared__ uint32_t sfl[RW][kNodes / 32];
+    __shared__ int cntw[RW];
+    __shared__ int s_base;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int *const P = Pall[wv];
+    uint32_t *const sflag = sfl[wv];
+    const int ntiles = ntx * nty, nft = ftcount[0], wpr = (W + 63) >> 6;
+    const int nb = lane * 32;  // this row's first node id
+    // RW tiles per workgroup per round from a work counter (ftcount[1]), one per wave, read
+    // through workgroup barriers (a first version with a per-wave counter read by lane 0 and
+    // a `continue` for empty tiles faulted / hung on the GPU, round 5)
+    for (;;) {
+        if (threadIdx.x == 0) s_base = atomicAdd(&ftcount[1], RW);
+        __syncthreads();
+        const int base = s_base;
+        __syncthreads();
+        if (base >= nft) break;
+        const int it = base + wv;
+        if (it < nft) ccl_runs_tile(cls, H, W, ntx, ntiles, wpr, ftlist[it], lane, nb, P, sflag, &cntw[wv], lab, parent,
+                                    sroot, roots, nroots, tlist, tcount, ebits);
     }
 }
 
@@ -202,7 +294,7 @@ __global__ __launch_bounds__(LT) void k_tile_list(const uint8_t *__restrict__ tf
                                                   int *__restrict__ ftlist, int *__restrict__ ftcount) {
     __shared__ int wbase[LT / 64];
     const int i = blockIdx.x * LT + threadIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const bool f = i < total && tflag[i];
+    const bool f = i < total && (!tflag || tflag[i]);  // (no flags: every tile)
     const unsigned long long m = __ballot(f);
     if (lane == 0) wbase[wid] = __popcll(m);
     __syncthreads();
@@ -229,7 +321,7 @@ __device__ __forceinline__ int gid_of(const uint16_t *lab, int img, int H, int W
     return (int)(((size_t)img * ntiles + t) * TP) + lab[((size_t)img * H + y) * W + x];
 }
 
-// The passes after k_ccl_local visit only the tiles it listed (those with a candidate;
+// The passes after k_ccl_runs visit only the tiles it listed (those with a candidate;
 // 15 % of the ui / photo mix): a fixed grid loops over tlist instead of launching one
 // workgroup per tile.  Edge words of unlisted tiles stay zero (memset).
 constexpr int kListBlocks = 4096;
@@ -279,17 +371,22 @@ __global__ __launch_bounds__(NT) void k_ccl_flatten(const int *__restrict__ tlis
         for (int k = threadIdx.x; k < n; k += NT) {
             const int g = (int)(gbase + roots[gbase + k]);
             const int r = g_find(parent, g);
-            if (sroot[g]) sroot[r] = 1;
+            // bit 1 of the global root: some member component is strong (every writer sets
+            // the same bit, bit 0 -- strong in its own tile -- is only read)
+            if (sroot[g] & 1) sroot[r] |= 2;
             if (r != g) parent[g] = r;
         }
     }
 }
 
-// per listed tile: one bit per local root, set when its global root is strong
+// per listed tile: one bit per *promoted* local root -- not strong in its tile, but its
+// global root's component is (sroot != 0) -- and the tiles with such a root listed for
+// k_ccl_edge (most have none: their edge words are final after k_ccl_runs)
 __global__ __launch_bounds__(NT) void k_ccl_strong(const int *__restrict__ tlist, const int *__restrict__ tcount,
                                                     const uint16_t *__restrict__ roots, const int *__restrict__ nroots,
                                                     const int *__restrict__ parent, const uint8_t *__restrict__ sroot,
-                                                    uint32_t *__restrict__ tstrong) {
+                                                    uint32_t *__restrict__ tstrong, int *__restrict__ ptlist,
+                                                    int *__restrict__ ptcount) {
     __shared__ uint32_t rs[TP / 32];
     const int tid = threadIdx.x, ntl = *tcount;
     for (int it = blockIdx.x; it < ntl; it += gridDim.x) {
@@ -297,51 +394,44 @@ __global__ __launch_bounds__(NT) void k_ccl_strong(const int *__restrict__ tlist
         const int n = nroots[tile];
         if (tid < TP / 32) rs[tid] = 0;
         __syncthreads();
+        bool any = false;
         for (int k = tid; k < n; k += NT) {
             const int i = roots[gbase + k];
-            if (sroot[parent[gbase + i]]) atomicOr(&rs[i >> 5], 1u << (i & 31));
+            if (!(sroot[gbase + i] & 1) && sroot[parent[gbase + i]]) {
+                atomicOr(&rs[i >> 5], 1u << (i & 31));
+                any = true;
+            }
         }
-        __syncthreads();
-        if (tid < TP / 32) tstrong[tile * (TP / 32) + tid] = rs[tid];
+        if (__syncthreads_or(any)) {
+            if (tid < TP / 32) tstrong[tile * (TP / 32) + tid] = rs[tid];
+            if (tid == 0) ptlist[atomicAdd(ptcount, 1)] = (int)tile;
+        }
         __syncthreads();
     }
 }
 
-// per listed tile, no halo: edge = strong || (maybe && strong local root); one wave
-// per 64-pixel row segment packs the row's edge word with __ballot
-__global__ __launch_bounds__(NT) void k_ccl_edge(const uint8_t *__restrict__ cls, const uint16_t *__restrict__ lab,
-                                                  int H, int W, int ntx, int nty, const int *__restrict__ tlist,
-                                                  const int *__restrict__ tcount, const uint32_t *__restrict__ tstrong,
-                                                  uint64_t *__restrict__ ebits) {
-    __shared__ uint32_t rs[TP / 32];
-    constexpr int RPW = TH / (NT / 64);  // rows per wave
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int ntiles = ntx * nty, ntl = *tcount, wpr = (W + 63) / 64;
-    for (int it = blockIdx.x; it < ntl; it += gridDim.x) {
-        const int tt = tlist[it], img = tt / ntiles, t = tt % ntiles;
-        const int tx0 = (t % ntx) * TW, ty0 = (t / ntx) * TH, x = tx0 + lane;
-        const size_t tile = (size_t)tt;
-        const uint8_t *c = cls + (size_t)img * H * W;
-        const uint16_t *lb = lab + (size_t)img * H * W;
-        uint32_t v[RPW], l[RPW];
-#pragma unroll
-        for (int r = 0; r < RPW; r++) {
-            const int y = ty0 + wid + r * (NT / 64);
-            const bool in = y < H && x < W;
-            v[r] = in ? c[(size_t)y * W + x] : 1u;
-            l[r] = in ? lb[(size_t)y * W + x] : 0u;  // meaningful only where v == 0
+// per tile with a promoted root (one wave, lane = row): the runs whose local root (lab at
+// the run's first pixel) is promoted OR-ed into the row words k_ccl_runs wrote
+__global__ __launch_bounds__(64 * RW) void k_ccl_edge(const uint8_t *__restrict__ cls, const uint16_t *__restrict__ lab,
+                                                      int H, int W, int ntx, int nty, const int *__restrict__ ptlist,
+                                                      const int *__restrict__ ptcount,
+                                                      const uint32_t *__restrict__ tstrong, uint64_t *__restrict__ ebits) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int ntiles = ntx * nty, ntl = *ptcount, wpr = (W + 63) >> 6;
+    for (int it = blockIdx.x * RW + wv; it < ntl; it += gridDim.x * RW) {
+        const int tt = ptlist[it], img = tt / ntiles, t = tt % ntiles;
+        const int tx0 = (t % ntx) * TW, ty0 = (t / ntx) * TH, y = ty0 + lane;
+        unsigned long long C, S;
+        row_masks(cls, img, H, W, tx0, y, C, S);
+        const uint32_t *rs = tstrong + (size_t)tt * (TP / 32);
+        const uint16_t *lrow = lab + ((size_t)img * H + y) * W + tx0;
+        unsigned long long E = 0;
+        for (unsigned long long m = C & ~(C << 1); m; m &= m - 1) {
+            const int a = __builtin_ctzll(m), b = a + run_len(C, a) - 1;
+            const uint32_t r = lrow[a] & (TP - 1);
+            if ((rs[r >> 5] >> (r & 31)) & 1u) E |= bits_upto(b) & ~bits_upto(a - 1);
         }
-        if (tid < TP / 32) rs[tid] = tstrong[tile * (TP / 32) + tid];
-        __syncthreads();
-#pragma unroll
-        for (int r = 0; r < RPW; r++) {
-            const int y = ty0 + wid + r * (NT / 64);
-            const uint32_t li = l[r] & (TP - 1);
-            const bool on = v[r] == 2u || (v[r] == 0u && ((rs[li >> 5] >> (li & 31)) & 1u));
-            const unsigned long long b = __ballot(on);
-            if (lane == 0 && y < H) ebits[((size_t)img * H + y) * wpr + (tx0 >> 6)] = b;
-        }
-        __syncthreads();
+        if (E) ebits[((size_t)img * H + y) * wpr + (tx0 >> 6)] |= E;
     }
 }
 
@@ -412,35 +502,30 @@ __global__ __launch_bounds__(NT) void k_dilate3_u8(const uint8_t *__restrict__ s
 // the connected-component passes up to the packed edge words wk.ebits
 hipError_t launch_ccl(const uint8_t *cls, int n, int h, int w, const HystWork &wk, hipStream_t s) {
     const int ntx = tiles_x(w), nty = htiles_y(h), ntiles = ntx * nty;
-    dim3 grid(ntiles, n);
     const size_t words = (size_t)n * h * words_per_row(w);
     hipError_t e;
     if ((e = hipMemsetAsync(wk.tcount, 0, sizeof(int), s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(wk.ptcount, 0, sizeof(int), s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(wk.ebits, 0, sizeof(uint64_t) * words, s)) != hipSuccess) return e;
     const dim3 lgrid((unsigned)std::min<int64_t>((int64_t)ntiles * n, kListBlocks));
-    if (wk.tflag) {
-        // only the tiles the stencil flagged: no workgroup per empty tile, no read of its
-        // class bytes (85 % of the ui / photo mix)
-        if ((e = hipMemsetAsync(wk.ftcount, 0, 2 * sizeof(int), s)) != hipSuccess) return e;
-        const int total = ntiles * n;
-        hipLaunchKernelGGL(k_tile_list, dim3((unsigned)((total + LT - 1) / LT)), dim3(LT), 0, s, wk.tflag, total,
-                           wk.ftlist, wk.ftcount);
-        // (a work counter hands out the tiles: 2048 workgroups cover the 7 x 256 resident slots)
-        const dim3 qgrid((unsigned)std::min<int64_t>((int64_t)ntiles * n, 2048));
-        hipLaunchKernelGGL(k_ccl_local<true>, qgrid, dim3(NT), 0, s, cls, h, w, ntx, nty, wk.lab, wk.parent, wk.sroot,
-                           wk.roots, wk.nroots, wk.tlist, wk.tcount, (const int *)wk.ftlist, wk.ftcount);
-    } else {
-        hipLaunchKernelGGL(k_ccl_local<false>, grid, dim3(NT), 0, s, cls, h, w, ntx, nty, wk.lab, wk.parent, wk.sroot,
-                           wk.roots, wk.nroots, wk.tlist, wk.tcount, (const int *)nullptr, (int *)nullptr);
-    }
+    // the tiles to label: the stencil's flagged ones, or every tile of the batch
+    if ((e = hipMemsetAsync(wk.ftcount, 0, 2 * sizeof(int), s)) != hipSuccess) return e;
+    const int total = ntiles * n;
+    hipLaunchKernelGGL(k_tile_list, dim3((unsigned)((total + LT - 1) / LT)), dim3(LT), 0, s, wk.tflag, total, wk.ftlist,
+                       wk.ftcount);
+    // (a work counter hands out the tiles, one per wave; 1024 workgroups cover the 4 x 256
+    // resident ones)
+    const dim3 rgrid((unsigned)std::min<int64_t>(((int64_t)total + RW - 1) / RW, 1024));
+    hipLaunchKernelGGL(k_ccl_runs, rgrid, dim3(64 * RW), 0, s, cls, h, w, ntx, nty, wk.lab, wk.parent, wk.sroot,
+                       wk.roots, wk.nroots, wk.tlist, wk.tcount, (const int *)wk.ftlist, wk.ftcount, wk.ebits);
     hipLaunchKernelGGL(k_ccl_border, lgrid, dim3(128), 0, s, cls, wk.lab, h, w, ntx, nty, wk.tlist, wk.tcount,
                        wk.parent);
     hipLaunchKernelGGL(k_ccl_flatten, lgrid, dim3(NT), 0, s, wk.tlist, wk.tcount, wk.roots, wk.nroots, wk.parent,
                        wk.sroot);
     hipLaunchKernelGGL(k_ccl_strong, lgrid, dim3(NT), 0, s, wk.tlist, wk.tcount, wk.roots, wk.nroots, wk.parent,
-                       wk.sroot, wk.tstrong);
-    hipLaunchKernelGGL(k_ccl_edge, lgrid, dim3(NT), 0, s, cls, wk.lab, h, w, ntx, nty, wk.tlist, wk.tcount, wk.tstrong,
-                       wk.ebits);
+                       wk.sroot, wk.tstrong, wk.ptlist, wk.ptcount);
+    hipLaunchKernelGGL(k_ccl_edge, lgrid, dim3(64 * RW), 0, s, cls, wk.lab, h, w, ntx, nty, (const int *)wk.ptlist,
+                       (const int *)wk.ptcount, wk.tstrong, wk.ebits);
     return hipGetLastError();
 }
 
