@@ -555,7 +555,7 @@ int hyst_work(llfe_ctx *ctx, Work &W, int n, int h, int w, HystWork *out) {
     *out = HystWork{W.d_lab.p,     W.d_parent.p, W.d_sroot.p,       W.d_roots.p,   W.d_nroots.p,
                     W.d_tstrong.p, W.d_ebits.p,  W.d_tlist.p + 1, W.d_tlist.p,
                     W.tflag_valid ? W.d_tflag.p : nullptr, W.d_ftlist.p + 2, W.d_ftlist.p,
-                    W.d_ptlist.p + 1, W.d_ptlist.p};
+                    W.d_ptlist.p};
     W.tflag_valid = false;  // (one hysteresis pass per stencil launch)
     return LLFE_OK;
 }

@@ -68,8 +68,7 @@ struct HystWork {
     const uint8_t *tflag;  // (may be null) the stencil's tile flags (StencilParams::tflag)
     int *ftlist;           // with tflag: the flagged tiles (n * tiles),
     int *ftcount;          // their count and a work counter (two ints)
-    int *ptlist;           // tiles with a root promoted by the global unions (n * tiles)
-    int *ptcount;          // and their count
+    int *pflag;            // per tlist entry: the tile has a root promoted by the global unions
 };
 size_t hysteresis_ids(int n, int h, int w);    // >= the GPU contour pass's ids as well
 size_t hysteresis_tiles(int n, int h, int w);  // hysteresis tiles (<= n * tiles_x * tiles_y)
