@@ -364,8 +364,10 @@ def main():
                     help="also run the e2e lines when WORLD_SIZE > 1 (off by default: every rank would pin "
                          "~10 GB of host batches and decode on its 1/N core share while the scaling run "
                          "only needs `value`)")
-    ap.add_argument("--per-class-steps", type=int, default=4,
-                    help="steps of an all-ui and an all-photo batch (SURVEY.md 8d per-class throughput); 0 disables")
+    ap.add_argument("--per-class-steps", type=int, default=12,
+                    help="steps of an all-ui and an all-photo batch (SURVEY.md 8d per-class throughput; 4 steps "
+                         "left the pipeline's fill and drain in a third of the timed region: ui 21-30k across "
+                         "round-5 runs); 0 disables")
     ap.add_argument("--contours", choices=["auto", "host", "gpu"], default="auto",
                     help="where findContours + the shape loop run: the host pool from the copied-back mask "
                          "(overlaps k-means), the GPU (contours_gpu.hip), or auto (the library's choice: "
