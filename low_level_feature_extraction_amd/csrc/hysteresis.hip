@@ -182,8 +182,7 @@ __device__ __forceinline__ void ccl_runs_tile(const uint8_t *__restrict__ cls, i
                                               int wpr, int tt, int lane, int nb, int *P, uint32_t *sflag, int *cnt,
                                               uint16_t *__restrict__ lab, int *__restrict__ parent,
                                               uint8_t *__restrict__ sroot, uint16_t *__restrict__ roots,
-                                              int *__restrict__ nroots, int *__restrict__ tlist,
-                                              int *__restrict__ tcount, uint64_t *__restrict__ ebits) {
+                                              int *__restrict__ nroots, uint64_t *__restrict__ ebits) {
     const int img = tt / ntiles, t = tt % ntiles;
     const int tx0 = (t % ntx) * TW, ty0 = (t / ntx) * TH, y = ty0 + lane;
     unsigned long long C, S;
@@ -251,17 +250,13 @@ __device__ __forceinline__ void ccl_runs_tile(const uint8_t *__restrict__ cls, i
     if (E) ebits[((size_t)img * H + y) * wpr + (tx0 >> 6)] = E;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    if (lane == 0) {
-        nroots[(size_t)img * ntiles + t] = *cnt;
-        tlist[atomicAdd(tcount, 1)] = img * ntiles + t;  // the later passes visit only these
-    }
+    if (lane == 0) nroots[(size_t)img * ntiles + t] = *cnt;
 }
 
 __global__ __launch_bounds__(64 * RW) void k_ccl_runs(const uint8_t *__restrict__ cls, int H, int W, int ntx, int nty,
                                                     uint16_t *__restrict__ lab, int *__restrict__ parent,
                                                     uint8_t *__restrict__ sroot, uint16_t *__restrict__ roots,
-                                                    int *__restrict__ nroots, int *__restrict__ tlist,
-                                                    int *__restrict__ tcount, const int *__restrict__ ftlist,
+                                                    int *__restrict__ nroots, const int *__restrict__ ftlist,
                                                     int *__restrict__ ftcount, uint64_t *__restrict__ ebits) {
     __shared__ int Pall[RW][kNodes];
     __shared__ uint32_t sfl[RW][kNodes / 32];
@@ -272,18 +267,24 @@ __global__ __launch_bounds__(64 * RW) void k_ccl_runs(const uint8_t *__restrict_
     uint32_t *const sflag = sfl[wv];
     const int ntiles = ntx * nty, nft = ftcount[0], wpr = (W + 63) >> 6;
     const int nb = lane * 32;  // this row's first node id
-    // RW tiles per workgroup per round from a work counter (ftcount[1]), one per wave, read
-    // through workgroup barriers (a first version with a per-wave counter read by lane 0 and
-    // a `continue` for empty tiles faulted / hung on the GPU, round 5)
+    // kGrab tiles per workgroup per round from a work counter (ftcount[1]), read through
+    // workgroup barriers (a first version with a per-wave counter read by lane 0 and a
+    // `continue` for empty tiles faulted / hung on the GPU, round 5); the later passes walk
+    // the same list (no per-tile append: one global atomic per tile on one counter costs
+    // ~100 us per 512 x 1080p)
+    constexpr int kGrab = 2 * RW;
     for (;;) {
-        if (threadIdx.x == 0) s_base = atomicAdd(&ftcount[1], RW);
+        if (threadIdx.x == 0) s_base = atomicAdd(&ftcount[1], kGrab);
         __syncthreads();
         const int base = s_base;
         __syncthreads();
         if (base >= nft) break;
-        const int it = base + wv;
-        if (it < nft) ccl_runs_tile(cls, H, W, ntx, ntiles, wpr, ftlist[it], lane, nb, P, sflag, &cntw[wv], lab, parent,
-                                    sroot, roots, nroots, tlist, tcount, ebits);
+#pragma unroll 1
+        for (int q = wv; q < kGrab; q += RW) {
+            const int it = base + q;
+            if (it < nft) ccl_runs_tile(cls, H, W, ntx, ntiles, wpr, ftlist[it], lane, nb, P, sflag, &cntw[wv], lab,
+                                        parent, sroot, roots, nroots, ebits);
+        }
     }
 }
 
@@ -510,7 +511,6 @@ hipError_t launch_ccl(const uint8_t *cls, int n, int h, int w, const HystWork &w
     const int ntx = tiles_x(w), nty = htiles_y(h), ntiles = ntx * nty;
     const size_t words = (size_t)n * h * words_per_row(w);
     hipError_t e;
-    if ((e = hipMemsetAsync(wk.tcount, 0, sizeof(int), s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(wk.ebits, 0, sizeof(uint64_t) * words, s)) != hipSuccess) return e;
     const dim3 lgrid((unsigned)std::min<int64_t>((int64_t)ntiles * n, kListBlocks));
     // the tiles to label: the stencil's flagged ones, or every tile of the batch
@@ -518,19 +518,21 @@ hipError_t launch_ccl(const uint8_t *cls, int n, int h, int w, const HystWork &w
     const int total = ntiles * n;
     hipLaunchKernelGGL(k_tile_list, dim3((unsigned)((total + LT - 1) / LT)), dim3(LT), 0, s, wk.tflag, total, wk.ftlist,
                        wk.ftcount);
-    // (a work counter hands out the tiles, one per wave; 1024 workgroups cover the 4 x 256
-    // resident ones)
+    // (a work counter hands out the tiles, eight per workgroup; 1024 workgroups cover the
+    // 4 x 256 resident ones)
     const dim3 rgrid((unsigned)std::min<int64_t>(((int64_t)total + RW - 1) / RW, 1024));
     hipLaunchKernelGGL(k_ccl_runs, rgrid, dim3(64 * RW), 0, s, cls, h, w, ntx, nty, wk.lab, wk.parent, wk.sroot,
-                       wk.roots, wk.nroots, wk.tlist, wk.tcount, (const int *)wk.ftlist, wk.ftcount, wk.ebits);
-    hipLaunchKernelGGL(k_ccl_border, lgrid, dim3(128), 0, s, cls, wk.lab, h, w, ntx, nty, wk.tlist, wk.tcount,
+                       wk.roots, wk.nroots, (const int *)wk.ftlist, wk.ftcount, wk.ebits);
+    // the later passes visit the same listed tiles (with the stencil's flags exactly those
+    // with a candidate; without them every tile, the empty ones with nroots = 0)
+    const int *tl = wk.ftlist, *tc = wk.ftcount;
+    hipLaunchKernelGGL(k_ccl_border, lgrid, dim3(128), 0, s, cls, wk.lab, h, w, ntx, nty, tl, tc,
                        wk.parent);
-    hipLaunchKernelGGL(k_ccl_flatten, lgrid, dim3(NT), 0, s, wk.tlist, wk.tcount, wk.roots, wk.nroots, wk.parent,
+    hipLaunchKernelGGL(k_ccl_flatten, lgrid, dim3(NT), 0, s, tl, tc, wk.roots, wk.nroots, wk.parent,
                        wk.sroot);
-    hipLaunchKernelGGL(k_ccl_strong, lgrid, dim3(64 * RW), 0, s, wk.tlist, wk.tcount, wk.roots, wk.nroots, wk.parent,
+    hipLaunchKernelGGL(k_ccl_strong, lgrid, dim3(64 * RW), 0, s, tl, tc, wk.roots, wk.nroots, wk.parent,
                        wk.sroot, wk.tstrong, wk.pflag);
-    hipLaunchKernelGGL(k_ccl_edge, lgrid, dim3(64 * RW), 0, s, cls, wk.lab, h, w, ntx, nty, (const int *)wk.tlist,
-                       (const int *)wk.tcount, (const int *)wk.pflag, wk.tstrong, wk.ebits);
+    hipLaunchKernelGGL(k_ccl_edge, lgrid, dim3(64 * RW), 0, s, cls, wk.lab, h, w, ntx, nty, tl, tc, (const int *)wk.pflag, wk.tstrong, wk.ebits);
     return hipGetLastError();
 }
 
