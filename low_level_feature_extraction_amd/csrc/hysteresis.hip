@@ -322,10 +322,11 @@ __device__ __forceinline__ int gid_of(const uint16_t *lab, int img, int H, int W
     return (int)(((size_t)img * ntiles + t) * TP) + lab[((size_t)img * H + y) * W + x];
 }
 
-// The passes after k_ccl_runs visit only the tiles it listed (those with a candidate;
-// 15 % of the ui / photo mix): a fixed grid loops over tlist instead of launching one
-// workgroup per tile.  Edge words of unlisted tiles stay zero (memset).
-constexpr int kListBlocks = 4096;
+// The passes after k_ccl_runs visit only the listed tiles (those with a candidate; 15 % of
+// the ui / photo mix): a fixed grid loops over the list instead of launching one workgroup
+// per tile of the batch.  Edge words of unlisted tiles stay zero (memset).  16k workgroups
+// (round 5; 4096 before): border + flatten + edge 210 -> 183 us on the mix, 64k no better.
+constexpr int kListBlocks = 16384;
 
 // threads 0..31 the tile's right column (look east), 32..95 its bottom row (look south)
 __global__ __launch_bounds__(128) void k_ccl_border(const uint8_t *__restrict__ cls, const uint16_t *__restrict__ lab,
