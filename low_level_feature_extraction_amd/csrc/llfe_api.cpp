@@ -212,7 +212,7 @@ struct Work {
     DevBuf<int8_t> d_noise, d_nfield;  // d_nfield: the launch's noise field (unique.hip)
     DevBuf<uint64_t> d_bits, d_ebits;
     DevBuf<unsigned long long> d_shadow;
-    DevBuf<int> d_order, d_parent, d_nroots, d_tlist, d_ftlist, d_ptlist;
+    DevBuf<int> d_order, d_parent, d_nroots, d_ftlist, d_ptlist;
     DevBuf<uint16_t> d_lab, d_roots;
     DevBuf<uint32_t> d_raw, d_keys, d_kscratch, d_pmeta, d_tstrong, d_segtab;  // d_segtab: k_uq_scatter's run table
     DevBuf<CubeEnt> d_segcubes, d_cubes;
@@ -549,11 +549,10 @@ int hyst_work(llfe_ctx *ctx, Work &W, int n, int h, int w, HystWork *out) {
     HIPCHK(ctx, W.d_nroots.ensure(tiles));
     HIPCHK(ctx, W.d_tstrong.ensure(hysteresis_tiles(n, h, w) * hysteresis_tile_words()));
     HIPCHK(ctx, W.d_ebits.ensure((size_t)n * h * words_per_row(w)));
-    HIPCHK(ctx, W.d_tlist.ensure(tiles + 1));
     HIPCHK(ctx, W.d_ftlist.ensure(tiles + 2));
     HIPCHK(ctx, W.d_ptlist.ensure(tiles + 1));
     *out = HystWork{W.d_lab.p,     W.d_parent.p, W.d_sroot.p,       W.d_roots.p,   W.d_nroots.p,
-                    W.d_tstrong.p, W.d_ebits.p,  W.d_tlist.p + 1, W.d_tlist.p,
+                    W.d_tstrong.p, W.d_ebits.p,
                     W.tflag_valid ? W.d_tflag.p : nullptr, W.d_ftlist.p + 2, W.d_ftlist.p,
                     W.d_ptlist.p};
     W.tflag_valid = false;  // (one hysteresis pass per stencil launch)

@@ -63,12 +63,10 @@ struct HystWork {
     int *nroots;
     uint32_t *tstrong;  // per tile TP / 32 words (the promoted local roots)
     uint64_t *ebits;    // n x h x words_per_row, edges before the dilate
-    int *tlist;         // tiles with a Canny candidate (n * tiles) and their count
-    int *tcount;
     const uint8_t *tflag;  // (may be null) the stencil's tile flags (StencilParams::tflag)
-    int *ftlist;           // with tflag: the flagged tiles (n * tiles),
+    int *ftlist;           // the tiles to label (flagged ones, or every tile without tflag),
     int *ftcount;          // their count and a work counter (two ints)
-    int *pflag;            // per tlist entry: the tile has a root promoted by the global unions
+    int *pflag;            // per ftlist entry: the tile has a root promoted by the global unions
 };
 size_t hysteresis_ids(int n, int h, int w);    // >= the GPU contour pass's ids as well
 size_t hysteresis_tiles(int n, int h, int w);  // hysteresis tiles (<= n * tiles_x * tiles_y)
