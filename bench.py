@@ -191,6 +191,57 @@ def e2e_host(be, imgs_dev, feats, steps, seed, index_base):
                       f"H2D + full GPU path per batch, two batches in flight (llfe_submit_batch / llfe_collect_batch)"}
 
 
+def served_batcher(imgs_dev, feats, batches, seed, inflight):
+    """The product request path at load (the reference serves one
+    image per /analyze call, app/api/v1/endpoints/analyze.py:94-111): P concurrent asyncio
+    producers each await ``MicroBatcher.analyze`` on its own single 1080p device image
+    (separately allocated, resident in HBM like `value`'s batch), back to back, until
+    ``batches`` x B requests have completed.  The batcher forms launches of up to B
+    (max_batch) and keeps ``inflight`` of them in flight through llfe_submit_images /
+    llfe_collect_batch; every request's reference-shaped result dict is resolved inside
+    the timed region.  Timed like `value` (synchronised clock around the requests)."""
+    import asyncio
+    import itertools
+
+    import torch
+
+    from low_level_feature_extraction_amd.batcher import MicroBatcher
+
+    B = int(imgs_dev.shape[0])
+    producers = (inflight + 1) * B  # enough outstanding requests to keep every slot full
+    dev = [imgs_dev[i % B].clone() for i in range(producers)]  # one allocation per request image
+    torch.cuda.synchronize()
+    bt = MicroBatcher(features=feats, max_batch=B, max_wait_ms=2.0, inflight=inflight, seed=seed)
+
+    async def drive(n_requests):
+        counter = itertools.count()
+
+        async def producer(img):
+            while next(counter) < n_requests:
+                await bt.analyze(img)
+
+        await asyncio.gather(*(producer(t) for t in dev))
+
+    try:
+        asyncio.run(drive(2 * B))  # warm-up: the worker's context, workspaces, gc.freeze
+        n0 = len(bt.batch_sizes)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        asyncio.run(drive(batches * B))
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+    finally:
+        bt.close()
+    sizes = bt.batch_sizes[n0:]
+    return {"value": round(batches * B / dt, 2), "unit": "images/s", "requests": batches * B,
+            "producers": producers, "max_batch": B, "inflight": inflight,
+            "launches": len(sizes), "mean_launch": round(sum(sizes) / max(len(sizes), 1), 1),
+            "max_in_flight": bt.max_in_flight,
+            "sample": f"{batches * B} single {imgs_dev.shape[2]}x{imgs_dev.shape[1]} device images from {producers} "
+                      f"concurrent asyncio producers through MicroBatcher.analyze (llfe_submit_images gather + "
+                      f"the full GPU path, {inflight} launches in flight, results assembled per request)"}
+
+
 def e2e_png(be, B, H, W, feats, steps, distinct, seed, fmt="PNG", decode_steps=2, contours=None):
     """End-to-end from encoded bytes (PNG, or JPEG quality 85):
     host decode on the decode thread pool into pinned host batches, driven through the
@@ -322,6 +373,30 @@ def launch_ranks(n: int, argv: list[str]) -> list[str]:
             "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
 
 
+def visible_gpus(env=os.environ, sysfs="/sys/class/kfd/kfd/topology/nodes") -> int:
+    """GPUs a rank could be given, counted without starting a HIP runtime (the launching
+    parent must not touch the GPU): the kfd topology nodes with SIMDs (CPU nodes have
+    none), or the length of a *_VISIBLE_DEVICES list when one is set."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = env.get(var)
+        if v is not None:
+            return len([x for x in v.split(",") if x.strip() not in ("", "-1")])
+    n = 0
+    try:
+        nodes = os.listdir(sysfs)
+    except OSError:
+        return 0
+    for node in nodes:
+        try:
+            with open(os.path.join(sysfs, node, "properties")) as f:
+                props = dict(line.split(None, 1) for line in f if len(line.split(None, 1)) == 2)
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0").strip() or 0) > 0:
+            n += 1
+    return n
+
+
 def check_world(gpus: int, env=os.environ) -> str:
     """--gpus is authoritative.  'launch': no launcher ran us and N > 1, so start N ranks
     (before anything touches the GPU); 'run': this process is one rank of the N asked for
@@ -368,6 +443,8 @@ def main():
                     help="steps of an all-ui and an all-photo batch (SURVEY.md 8d per-class throughput; 4 steps "
                          "left the pipeline's fill and drain in a third of the timed region: ui 21-30k across "
                          "round-5 runs); 0 disables")
+    ap.add_argument("--batcher-steps", type=int, default=10,
+                    help="0 disables the served_batcher line (single-image requests through MicroBatcher)")
     ap.add_argument("--contours", choices=["auto", "host", "gpu"], default="auto",
                     help="where findContours + the shape loop run: the host pool from the copied-back mask "
                          "(overlaps k-means), the GPU (contours_gpu.hip), or auto (the library's choice: "
@@ -390,14 +467,16 @@ def main():
     if check_world(args.gpus) == "launch":
         # no GPU call has happened in this process: the ranks are children, and this
         # process only waits for them and exits with their status
+        # (the parent never touches the GPU -- counting devices through torch would start a
+        # HIP runtime here -- it reads the kfd topology; each rank then checks that its
+        # LOCAL_RANK names a GPU its own runtime sees)
         import subprocess
 
         if os.environ.get("LLFE_BENCH_SHARE_GPU") != "1":
-            import torch  # device_count() does not initialise the GPU
-
-            have = torch.cuda.device_count()
+            have = visible_gpus()
             if have < args.gpus:
                 raise SystemExit(f"bench.py: --gpus {args.gpus} but {have} GPUs are visible")
+
         sys.exit(subprocess.call(launch_ranks(args.gpus, sys.argv[1:])))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -418,6 +497,9 @@ def main():
     if no_gpu:
         share_gpu = True
     else:
+        if local >= torch.cuda.device_count():
+            raise SystemExit(f"bench.py: rank {rank} needs GPU {local} but {torch.cuda.device_count()} are visible "
+                             f"(--gpus {args.gpus}; LLFE_BENCH_SHARE_GPU=1 rehearses N ranks on one GPU)")
         torch.cuda.set_device(local)
     dist = None
     if world > 1:
@@ -602,6 +684,14 @@ def main():
                                "host_contour_ms_per_image": round(hc["busy_ms"] * hc["threads"] / max(hc["images"], 1), 3)}
             del cb
 
+    # the product request path at the same load: single-image requests through the
+    # MicroBatcher, beside `value`
+    served = None
+    if args.batcher_steps > 0 and pipelined:
+        barrier()
+        served = served_batcher(imgs, feats, args.batcher_steps, args.seed, be.inflight)
+        barrier()
+
     # (the e2e lines run on every rank before rank 0 reports: each rank pays its own
     # host-side work, as a serving node would)
 
@@ -689,6 +779,7 @@ def main():
         line["per_rank"] = True
         return line
 
+    served = all_ranks(served, args.batcher_steps)
     barrier()
     e2e_h = None
     if args.e2e_host_steps > 0:
@@ -754,6 +845,7 @@ def main():
                             "tail_ms_after_last_collect": round(asm_tail, 3),
                             "in_timed_region": True},
         "per_class": per_class,
+        "served_batcher": served,
         # wall share of the timed steps the host contour pool spent tracing (host mode)
         "host_contour_busy": round(host_ct["busy_ms"] / 1e3 / max(t1 - t0, 1e-9), 3),
         "cpu_baseline": cpu,
@@ -763,6 +855,8 @@ def main():
         "e2e_jpeg": e2e_j,
         "e2e_jpeg_other_contour_mode": e2e_j_alt,
     }
+    if served is not None:
+        served["ratio_to_value"] = round(served["value"] / out["value"], 3)
     print(json.dumps(out))
     if dist is not None:
         dist.destroy_process_group()

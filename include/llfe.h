@@ -233,6 +233,21 @@ int llfe_submit_batch(llfe_ctx *ctx, const llfe_batch *batch, uint32_t features,
 int llfe_collect_batch(llfe_ctx *ctx, int64_t ticket, llfe_image_result *results, llfe_shape *shapes,
                        int64_t shape_capacity, int64_t *shapes_needed);
 
+/* llfe_submit_batch for n separately allocated images of ONE size (the request path:
+ * concurrent /analyze requests -- app/api/v1/endpoints/analyze.py:63-129, one image per
+ * request -- sharing one launch, MicroBatcher).  The images (host or device, any row
+ * stride, no parity noise) are gathered on the submit's stream into the in-flight
+ * slot's own input buffer (device sources: one gather kernel; host sources: 2-D
+ * copies), then run exactly as llfe_submit_batch; image i carries global index
+ * indices[i] (its noise / k-means seeds), so its results equal a one-image call's.
+ * Collect with llfe_collect_batch.  The sources must stay valid until the ticket is
+ * collected; the library keeps its own copy of `images` and `indices`. */
+int llfe_submit_images(llfe_ctx *ctx, const llfe_image_desc *images, int32_t n, uint32_t features, int32_t n_colors,
+                       uint64_t seed, const int64_t *indices, llfe_stream stream, int64_t *ticket);
+/* images of h x w one device pass takes: the largest n llfe_submit_batch /
+ * llfe_submit_images accept (the workspace budget, LLFE_WORKSPACE_GB); < 0 on bad sizes */
+int llfe_batch_capacity(int32_t h, int32_t w);
+
 /* ---- stage entry points (parity tests; device in/out unless noted) ------
  * The ones that use the context's workspace (llfe_shape_mask, llfe_canny,
  * llfe_shadow_stats, llfe_color_unique, llfe_kmeans, llfe_find_contours_gpu,

@@ -15,7 +15,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libllfe.so")
 SOURCES = ["llfe_api.cpp", "contours.cpp", "png_decode.cpp", "jpeg_decode.cpp", "stencil.hip", "stencil_stream.hip", "hysteresis.hip", "unique.hip", "kmeans.hip", "kmeans_big.hip", "resize.hip", "contours_gpu.hip",
-           "cvresize.hip", "text.hip"]
+           "cvresize.hip", "text.hip", "gather.hip"]
 HEADERS = ["llfe_internal.h", "contours.h", "kmeans_common.h"]
 ARCH = os.environ.get("LLFE_OFFLOAD_ARCH", "gfx950")
 

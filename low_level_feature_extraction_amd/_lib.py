@@ -134,6 +134,8 @@ SIGNATURES = {
     "llfe_get_inflight": (C.c_int, [_vp]),
     "llfe_submit_batch": (C.c_int, [_vp, C.POINTER(LlfeBatch), _u32, _u64, _vp, C.POINTER(C.c_int64)]),
     "llfe_collect_batch": (C.c_int, [_vp, C.c_int64, _vp, _vp, C.c_int64, C.POINTER(C.c_int64)]),
+    "llfe_submit_images": (C.c_int, [_vp, _vp, _i32, _u32, _i32, _u64, _vp, _vp, C.POINTER(C.c_int64)]),
+    "llfe_batch_capacity": (C.c_int, [_i32, _i32]),
     "llfe_kernel_stats": (C.c_int, [_vp, C.POINTER(LlfeKernelStat), _i32]),
     "llfe_host_contour_stats": (C.c_int, [_vp, C.POINTER(C.c_double), C.POINTER(C.c_int64), C.POINTER(C.c_int32), _i32]),
     "llfe_process_batch": (C.c_int, [_vp, C.POINTER(LlfeBatch), _u32, _u64, _vp, _vp, _i64, C.POINTER(C.c_int64), _vp]),

@@ -356,6 +356,64 @@ class Backend:
         self._inflight[ticket.value] = (n, h, w, mask, keep, nkeep, b)  # inputs stay alive
         return ticket.value
 
+    _DESC_DTYPE = None
+
+    def batch_capacity(self, h: int, w: int) -> int:
+        """Images of h x w one ``submit`` / ``submit_images`` launch takes."""
+        return L.check(self.ctx, self._lib.llfe_batch_capacity(int(h), int(w)))
+
+    def submit_images(self, images, features=("colors", "shapes", "shadows"), seed: int = 0, indices=None,
+                      n_colors: int = 5) -> int:
+        """llfe_submit_images: n separately allocated H x W x 3 BGR uint8 images of one size
+        (torch tensors on the device, or host arrays; rows may be strided, pixels packed),
+        gathered into one launch, image i under global index ``indices[i]``.  Same ticket /
+        ``collect`` / in-flight rules as ``submit``; the images must stay alive until then
+        (the backend holds references)."""
+        n = len(images)
+        if n < 1:
+            raise ValueError("submit_images needs at least one image")
+        if Backend._DESC_DTYPE is None:
+            Backend._DESC_DTYPE = np.dtype(L.LlfeImageDesc)
+        descs = np.zeros(n, Backend._DESC_DTYPE)
+        keep = []
+        ptr, hh, ww, st, dev = [], [], [], [], []
+        for i, im in enumerate(images):
+            if _is_torch(im):
+                t = im
+                if t.dtype != _torch().uint8 or t.dim() != 3 or t.shape[2] != 3:
+                    raise ValueError(f"image {i}: expected H x W x 3 uint8, got {tuple(t.shape)} {t.dtype}")
+                if t.stride(2) != 1 or t.stride(1) != 3 or t.stride(0) < 3 * t.shape[1]:
+                    t = t.contiguous()
+                ptr.append(t.data_ptr())
+                st.append(t.stride(0))
+                dev.append(int(t.is_cuda))
+            else:
+                t = np.asarray(im)
+                if t.dtype != np.uint8 or t.ndim != 3 or t.shape[2] != 3:
+                    raise ValueError(f"image {i}: expected H x W x 3 uint8, got {t.shape} {t.dtype}")
+                if t.strides[2] != 1 or t.strides[1] != 3 or t.strides[0] < 3 * t.shape[1]:
+                    t = np.ascontiguousarray(t)
+                ptr.append(t.ctypes.data)
+                st.append(t.strides[0])
+                dev.append(0)
+            hh.append(t.shape[0])
+            ww.append(t.shape[1])
+            keep.append(t)
+        descs["data"], descs["height"], descs["width"] = ptr, hh, ww
+        descs["row_stride"], descs["on_device"] = st, dev
+        idx = np.ascontiguousarray(np.arange(n) if indices is None else indices, dtype=np.int64)
+        if idx.shape != (n,):
+            raise ValueError("indices must hold one global index per image")
+        mask = feature_mask(features)
+        ticket = C.c_int64(0)
+        stream = self._stream(next((t for t in keep if _is_torch(t) and t.is_cuda), None))
+        self._call("llfe_submit_images", descs.ctypes.data, n, mask, int(n_colors), C.c_uint64(seed & (2**64 - 1)),
+                   idx.ctypes.data, stream, C.byref(ticket))
+        if not hasattr(self, "_inflight"):
+            self._inflight = {}
+        self._inflight[ticket.value] = (n, hh, ww, mask, keep, idx, descs)
+        return ticket.value
+
     def collect(self, ticket: int) -> list:
         n, h, w, mask, keep, nkeep, b = self._inflight[ticket]
         results = (L.LlfeImageResult * max(n, 1))()

@@ -2,26 +2,40 @@
 
 The reference's ``/analyze`` endpoint (app/api/v1/endpoints/analyze.py:63-129) runs
 every request through the per-image extractors on the event-loop thread, one image per
-call.  ``MicroBatcher`` lets concurrent requests share one ``llfe_process_batch``
-launch: requests queue up, a single worker thread (with its own device context) drains
-up to ``max_batch`` images or whatever arrived within ``max_wait_ms`` of the first one,
-runs them through ``pipeline.run_batch`` (which groups them by size) and resolves each
-request's future with exactly the dict ``run_batch`` returns for that image.
+call.  ``MicroBatcher`` lets concurrent requests share launches: requests queue up and a
+single worker thread (with its own device context) drains up to ``max_batch`` images, or
+whatever arrived within ``max_wait_ms`` of the first one, into one launch.
+
+The worker runs the serving loop the headline measures (bench.py): it keeps ``inflight``
+launches in flight through ``Backend.submit_images`` / ``Backend.collect``
+(llfe_submit_images gathers the requests' separately allocated images on the device, so
+batch k + 1's kernels start in the tail of batch k's k-means), and a resolver thread
+turns each collected batch into the reference-shaped results (``pipeline.assemble_batch``)
+and resolves the requests' futures while the worker submits the next batch.  After its
+first batch the worker calls ``gc.collect(); gc.freeze()`` (``freeze_gc``): the serving
+process's start-up heap then stays out of the collector's full passes, which otherwise
+stop the worker for 45-90 ms every few batches -- long enough to drain the in-flight
+launches and idle the GPU.
 
     batcher = MicroBatcher(features=("colors", "shapes", "shadows"))
     result = await batcher.analyze(image_bgr)          # inside an async endpoint
     fut = batcher.submit(image_bgr); fut.result()      # from any thread
 
-Results do not depend on how requests were grouped: every image carries its own global
-index for the noise stream and the k-means seeds.
+Images are H x W x 3 BGR uint8 numpy arrays or torch tensors (host or device).  Every
+request takes a global index when it is submitted (or the one it passes), which fixes its
+noise stream and k-means seeds: its result equals ``run_batch([image],
+index_base=index)``'s whatever it was batched with.  ``run=`` replaces the backend with a
+synchronous batch function ``run(images, features) -> list`` (one launch at a time; CPU
+tests).
 """
 from __future__ import annotations
 
 import asyncio
+import collections
 import queue
 import threading
 import time
-from concurrent.futures import Future
+from concurrent.futures import Future, ThreadPoolExecutor
 from typing import Callable, Optional, Sequence
 
 import numpy as np
@@ -29,31 +43,59 @@ import numpy as np
 _STOP = object()
 
 
+def _is_torch(x) -> bool:
+    return type(x).__module__.startswith("torch") and hasattr(x, "data_ptr")
+
+
 class MicroBatcher:
     def __init__(self, features: Sequence[str] = ("colors", "shapes", "shadows"), max_batch: int = 64,
-                 max_wait_ms: float = 2.0, run: Optional[Callable] = None):
+                 max_wait_ms: float = 2.0, run: Optional[Callable] = None, inflight: int = 2,
+                 seed: Optional[int] = None, n_colors: int = 5, freeze_gc: bool = True, backend=None):
         if max_batch < 1:
             raise ValueError("max_batch must be >= 1")
+        if inflight not in (1, 2, 3):
+            raise ValueError("inflight must be 1, 2 or 3")
         self.features = tuple(getattr(f, "value", f) for f in features)
         self.max_batch = int(max_batch)
         self.max_wait = max(0.0, float(max_wait_ms)) / 1e3
+        self.inflight = int(inflight)
+        self.n_colors = int(n_colors)
+        self.freeze_gc = bool(freeze_gc)
+        self._seed = seed
         self._run = run
+        self._backend = backend  # (tests: a stand-in with submit_images / collect / inflight)
         self._q: "queue.Queue" = queue.Queue()
-        self.batch_sizes: list = []  # sizes of the batches launched so far (diagnostics)
+        self.batch_sizes: list = []  # sizes of the launches so far (diagnostics)
+        # (submit time, collect-start time, collect-end time) per launch, worker clock
+        # (perf_counter): launches overlap when one is submitted before the previous one's
+        # collect returned
+        self.launch_log: list = []
+        self.max_in_flight = 0
         self._closed = False
         self._thread = threading.Thread(target=self._loop, name="llfe-batcher", daemon=True)
         self._thread.start()
 
     # ---------------------------------------------------------------- submission
-    def submit(self, image) -> Future:
-        """Queue one H x W x 3 BGR uint8 image; the future yields its result dict."""
+    def submit(self, image, index: Optional[int] = None) -> Future:
+        """Queue one H x W x 3 BGR uint8 image (numpy array or torch tensor, host or
+        device); the future yields its result dict.  ``index``: its global index (default:
+        the next one of the process counter)."""
         if self._closed:
             raise RuntimeError("MicroBatcher is closed")
-        img = np.ascontiguousarray(np.asarray(image, np.uint8))
-        if img.ndim != 3 or img.shape[2] != 3:
-            raise ValueError(f"expected H x W x 3 BGR uint8 image, got {img.shape}")
+        if _is_torch(image):
+            img = image
+            if str(img.dtype) != "torch.uint8" or img.dim() != 3 or img.shape[2] != 3:
+                raise ValueError(f"expected H x W x 3 BGR uint8 image, got {tuple(img.shape)} {img.dtype}")
+        else:
+            img = np.ascontiguousarray(np.asarray(image, np.uint8))
+            if img.ndim != 3 or img.shape[2] != 3:
+                raise ValueError(f"expected H x W x 3 BGR uint8 image, got {img.shape}")
+        if index is None:
+            from .color_extractor import _next_index
+
+            index = _next_index()
         fut: Future = Future()
-        self._q.put((img, fut))
+        self._q.put((img, fut, int(index)))
         return fut
 
     def submit_bytes(self, image_bytes: bytes, preprocessing: str = "auto") -> Future:
@@ -80,53 +122,35 @@ class MicroBatcher:
         self.close()
 
     # ---------------------------------------------------------------- worker
-    def _run_batch(self, images):
-        if self._run is not None:
-            return self._run(images, self.features)
-        from .pipeline import run_batch
-
-        return run_batch(images, self.features)
+    def _gather(self, block: bool):
+        """Up to max_batch queued requests: the first one (waiting for it when ``block``,
+        else at most max_wait), then whatever arrives within max_wait of it.  Returns
+        (items, stop)."""
+        try:
+            first = self._q.get() if block else self._q.get(timeout=self.max_wait) if self.max_wait > 0 \
+                else self._q.get_nowait()
+        except queue.Empty:
+            return [], False
+        if first is _STOP:
+            return [], True
+        items = [first]
+        deadline = time.monotonic() + self.max_wait
+        while len(items) < self.max_batch:
+            left = deadline - time.monotonic()
+            try:
+                nxt = self._q.get(timeout=left) if left > 0 else self._q.get_nowait()
+            except queue.Empty:
+                break
+            if nxt is _STOP:
+                return [x for x in items if x[1].set_running_or_notify_cancel()], True
+            items.append(nxt)
+        return [x for x in items if x[1].set_running_or_notify_cancel()], False
 
     def _loop(self):
-        stop = False
-        while not stop:
-            item = self._q.get()
-            if item is _STOP:
-                break
-            items = [item]
-            deadline = time.monotonic() + self.max_wait
-            while len(items) < self.max_batch:
-                left = deadline - time.monotonic()
-                try:
-                    nxt = self._q.get(timeout=left) if left > 0 else self._q.get_nowait()
-                except queue.Empty:
-                    break
-                if nxt is _STOP:
-                    stop = True
-                    break
-                items.append(nxt)
-            live = [(im, f) for im, f in items if f.set_running_or_notify_cancel()]
-            if not live:
-                continue
-            self.batch_sizes.append(len(live))
-            try:
-                res = self._run_batch([im for im, _ in live])
-                for (_, f), r in zip(live, res):
-                    f.set_result(r)
-            except Exception as e:
-                if len(live) == 1:
-                    live[0][1].set_exception(e)
-                    continue
-                # one bad image must not fail the requests it was batched with (the
-                # reference isolates every request): rerun them one by one
-                for im, f in live:
-                    try:
-                        f.set_result(self._run_batch([im])[0])
-                    except Exception as e1:
-                        f.set_exception(e1)
-            except BaseException as e:  # interpreter shutdown etc.: fail the batch
-                for _, f in live:
-                    f.set_exception(e)
+        if self._run is not None:
+            self._loop_sync()
+        else:
+            self._loop_pipelined()
         # fail whatever is still queued after close()
         while True:
             try:
@@ -135,3 +159,150 @@ class MicroBatcher:
                 break
             if item is not _STOP:
                 item[1].set_exception(RuntimeError("MicroBatcher is closed"))
+
+    def _loop_sync(self):
+        """``run=`` given: one synchronous launch at a time."""
+        stop = False
+        while not stop:
+            live, stop = self._gather(block=True)
+            if not live:
+                continue
+            self.batch_sizes.append(len(live))
+            try:
+                res = self._run([im for im, _, _ in live], self.features)
+                for (_, f, _), r in zip(live, res):
+                    f.set_result(r)
+            except Exception as e:
+                if len(live) == 1:
+                    live[0][1].set_exception(e)
+                    continue
+                # one bad image must not fail the requests it was batched with (the
+                # reference isolates every request): rerun them one by one
+                for im, f, _ in live:
+                    try:
+                        f.set_result(self._run([im], self.features)[0])
+                    except Exception as e1:
+                        f.set_exception(e1)
+            except BaseException as e:  # interpreter shutdown etc.: fail the batch
+                for _, f, _ in live:
+                    f.set_exception(e)
+
+    def _loop_pipelined(self):
+        from .pipeline import assemble_batch
+
+        try:
+            if self._backend is not None:
+                be = self._backend
+            else:
+                from .backend import Backend
+
+                be = Backend.get()  # this thread's own context
+            if self.inflight > 1:
+                be.inflight = self.inflight
+            depth = self.inflight
+            seed = self._seed
+            if seed is None:
+                from .color_extractor import _SEED as seed
+        except BaseException as e:  # no device: every request fails loudly (no CPU fallback)
+            while True:
+                live, stop = self._gather(block=True)
+                for _, f, _ in live:
+                    f.set_exception(e)
+                if stop:
+                    return
+        resolver = ThreadPoolExecutor(max_workers=1, thread_name_prefix="llfe-batcher-resolve")
+        pending: "collections.deque" = collections.deque()  # (ticket, live, log entry)
+        feats = self.features
+        froze = not self.freeze_gc
+
+        def resolve(recs, live):
+            try:
+                out = assemble_batch(recs, feats)
+            except BaseException as e:
+                for _, f, _ in live:
+                    f.set_exception(e)
+                return
+            for (_, f, _), r in zip(live, out):
+                f.set_result(r)
+
+        def finish_oldest():
+            nonlocal froze
+            ticket, live, log = pending.popleft()
+            log[1] = time.perf_counter()
+            try:
+                recs = be.collect(ticket)
+            except Exception as e:
+                log[2] = time.perf_counter()
+                for _, f, _ in live:
+                    f.set_exception(e)
+                return
+            log[2] = time.perf_counter()
+            resolver.submit(resolve, recs, live)
+            if not froze:
+                # the start-up heap out of the collector's full passes (module docstring)
+                import gc
+
+                gc.collect()
+                gc.freeze()
+                froze = True
+
+        def run_one_by_one(live):
+            # a launch the backend refused (e.g. one malformed image): the requests run
+            # alone, synchronously, so each gets its own result or error
+            from .pipeline import run_batch
+
+            while pending:
+                finish_oldest()
+            for im, f, idx in live:
+                try:
+                    f.set_result(run_batch([im], feats, seed=seed, index_base=idx, n_colors=self.n_colors,
+                                           backend=be)[0])
+                except Exception as e:
+                    f.set_exception(e)
+
+        stop = False
+        try:
+            while not stop or pending:
+                live = []
+                if not stop:
+                    live, stop = self._gather(block=not pending)
+                if not live:
+                    if pending:
+                        finish_oldest()
+                    continue
+                # one launch per image size (the launch packs one size), at most one device
+                # pass each
+                groups: dict = {}
+                for it in live:
+                    groups.setdefault((tuple(it[0].shape), _is_torch(it[0]) and it[0].is_cuda), []).append(it)
+                for (shape, _), grp in groups.items():
+                    cap = max(1, self._capacity(be, shape[0], shape[1]))
+                    for a in range(0, len(grp), cap):
+                        part = grp[a:a + cap]
+                        if len(pending) >= depth:
+                            finish_oldest()
+                        log = [time.perf_counter(), None, None]
+                        try:
+                            ticket = be.submit_images([im for im, _, _ in part], feats, seed=seed,
+                                                      indices=[idx for _, _, idx in part], n_colors=self.n_colors)
+                        except Exception:
+                            run_one_by_one(part)
+                            continue
+                        self.batch_sizes.append(len(part))
+                        self.launch_log.append(log)
+                        pending.append((ticket, part, log))
+                        self.max_in_flight = max(self.max_in_flight, len(pending))
+        except BaseException as e:  # interpreter shutdown etc.: fail what is in flight
+            for _, live, _ in pending:
+                for _, f, _ in live:
+                    if not f.done():
+                        f.set_exception(e)
+            raise
+        finally:
+            resolver.shutdown(wait=True)
+
+    @staticmethod
+    def _capacity(be, h, w) -> int:
+        """Images of h x w one launch takes (llfe_batch_capacity)."""
+        cap = getattr(be, "batch_capacity", None)
+        return int(cap(h, w)) if cap else 1 << 30

@@ -79,7 +79,8 @@ def _direct(primary, background, accent) -> ColorFeatures:
     o = ColorFeatures.__new__(ColorFeatures)
     object.__setattr__(o, "__dict__", {"primary": primary, "background": background, "accent": accent,
                                        "metadata": _md()})
-    object.__setattr__(o, "__pydantic_fields_set__", _FIELDS)
+    # (its own set: pydantic may add names to one instance's fields_set)
+    object.__setattr__(o, "__pydantic_fields_set__", set(_FIELDS))
     object.__setattr__(o, "__pydantic_extra__", None)
     object.__setattr__(o, "__pydantic_private__", None)
     return o

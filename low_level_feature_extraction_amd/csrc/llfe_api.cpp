@@ -413,6 +413,7 @@ struct llfe_ctx {
         uint32_t features = 0;
         std::vector<llfe_image_result> res;
         std::vector<llfe_shape> shp;
+        std::vector<int64_t> idx;  // llfe_submit_images: the images' global indices (b.indices)
     };
     Pending inflight[kMaxSlots];
     bool any_inflight() const {
@@ -459,6 +460,10 @@ struct llfe_ctx {
     hipEvent_t mask_ready[kMaxSlots] = {};
     int w_mask_slot[kMaxSlots] = {-1, -1, -1};
     HostBuf<KmeansImageOut> h_kout;
+    // llfe_submit_images: per slot, the gather table (n source addresses, n row pitches)
+    HostBuf<uint64_t> h_gather_s[kMaxSlots];
+    DevBuf<uint64_t> d_gather_s[kMaxSlots];
+    Work *km_last = nullptr;  // workspace of the last k-means launch (llfe_kmeans_attempts)
     // per-thread host scratch
     std::vector<std::vector<int8_t>> work;
     std::vector<Contours> cont;
@@ -704,6 +709,7 @@ int kmeans_stage(llfe_ctx *ctx, Work &W, const uint32_t *keys, int64_t key_strid
     HIPCHK(ctx, W.d_kout.ensure(n));
     W.km_n = n;
     W.km_colors = n_colors;
+    ctx->km_last = &W;
     // per-image cv::RNG state = splitmix64(seed + global index) is derived on the device
     TIMED(ctx, s, "k_kmeans", 0,
           launch_kmeans(keys, key_stride, d_nuniq, n, n_colors, seed, index, W.d_order.p, W.d_kscratch.p,
@@ -1455,6 +1461,85 @@ int llfe_submit_batch(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uin
     return LLFE_OK;
 }
 
+int llfe_batch_capacity(int32_t h, int32_t w) {
+    if (!valid_dims(1, h, w)) return LLFE_ERR_INVALID;
+    return chunk_for(h, w);
+}
+
+// The request path's micro-batch (MicroBatcher): separately allocated images of one size
+// gathered into the slot's input buffer on the slot's stream, then the same device work
+// as llfe_submit_batch, every image under its own global index.
+int llfe_submit_images(llfe_ctx *ctx, const llfe_image_desc *images, int32_t n, uint32_t features, int32_t n_colors,
+                       uint64_t seed, const int64_t *indices, llfe_stream stream, int64_t *ticket) {
+    if (!ctx || !ticket || n < 1 || !images || !indices) return LLFE_ERR_INVALID;
+    const int h = images[0].height, w = images[0].width;
+    if (!valid_dims(n, h, w)) return ctx->fail(LLFE_ERR_INVALID, "invalid batch n=%d h=%d w=%d", n, h, w);
+    if (n_colors < 0 || n_colors > kMaxColors)
+        return ctx->fail(LLFE_ERR_UNSUPPORTED, "n_colors=%d outside [1, %d]", n_colors, kMaxColors);
+    if (n > chunk_for(h, w))
+        return ctx->fail(LLFE_ERR_UNSUPPORTED, "llfe_submit_images: n=%d exceeds one device pass (%d)", n,
+                         chunk_for(h, w));
+    int nd = 0;
+    for (int i = 0; i < n; i++) {
+        const llfe_image_desc &d = images[i];
+        if (!d.data || d.height != h || d.width != w || (d.row_stride != 0 && d.row_stride < 3 * (int64_t)w))
+            return ctx->fail(LLFE_ERR_INVALID, "image %d: %d x %d stride %lld in a %d x %d submission", i, d.height,
+                             d.width, (long long)d.row_stride, h, w);
+        if (d.noise)
+            return ctx->fail(LLFE_ERR_UNSUPPORTED, "image %d: parity noise goes through llfe_process_images", i);
+        nd += d.on_device ? 1 : 0;
+    }
+    const int slot = (int)(ctx->next_ticket % ctx->inflight_max);
+    auto &pd = ctx->inflight[slot];
+    if (pd.busy) return ctx->fail(LLFE_ERR_CAPACITY, "%d batches already in flight: collect one first", ctx->inflight_max);
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    HIPCHK(ctx, hipEventRecord(ctx->start_ev, (hipStream_t)stream));
+    hipStream_t q = ctx->streams[slot];
+    HIPCHK(ctx, hipStreamWaitEvent(q, ctx->start_ev, 0));
+    Work &W = ctx->ws[slot];
+    const size_t P3 = (size_t)h * w * 3;
+    HIPCHK(ctx, W.d_in.ensure(P3 * n));
+    ctx->prof.cur_slot = slot;
+    if (nd == n) {
+        // every source on the device: one gather launch over a table of addresses and
+        // pitches (pinned, per slot: the slot is not reused before this ticket's collect)
+        HIPCHK(ctx, ctx->h_gather_s[slot].ensure(2 * (size_t)n));
+        HIPCHK(ctx, ctx->d_gather_s[slot].ensure(2 * (size_t)n));
+        uint64_t *tab = ctx->h_gather_s[slot].p;
+        for (int i = 0; i < n; i++) {
+            tab[i] = (uint64_t)(uintptr_t)images[i].data;
+            tab[n + i] = (uint64_t)(images[i].row_stride ? images[i].row_stride : 3 * (int64_t)w);
+        }
+        HIPCHK(ctx, hipMemcpyAsync(ctx->d_gather_s[slot].p, tab, sizeof(uint64_t) * 2 * n, hipMemcpyHostToDevice, q));
+        TIMED(ctx, q, "k_gather_images", 2.0 * (double)P3 * n,
+              launch_gather_images(ctx->d_gather_s[slot].p, n, h, w, W.d_in.p, q));
+    } else {
+        for (int i = 0; i < n; i++) {
+            const llfe_image_desc &d = images[i];
+            const size_t pitch = d.row_stride ? (size_t)d.row_stride : (size_t)w * 3;
+            HIPCHK(ctx, hipMemcpy2DAsync(W.d_in.p + (size_t)i * P3, (size_t)w * 3, d.data, pitch, (size_t)w * 3, h,
+                                         d.on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, q));
+        }
+    }
+    pd.idx.assign(indices, indices + n);
+    llfe_batch b{};
+    b.data = W.d_in.p;
+    b.n = n;
+    b.height = h;
+    b.width = w;
+    b.on_device = 1;
+    b.n_colors = n_colors;
+    b.indices = pd.idx.data();
+    int rc = enqueue_chunk(ctx, &b, features, seed, 0, n, slot, slot);
+    if (rc) return rc;
+    pd.busy = true;
+    pd.done = false;
+    pd.b = b;
+    pd.features = features;
+    *ticket = ctx->next_ticket++;
+    return LLFE_OK;
+}
+
 int llfe_collect_batch(llfe_ctx *ctx, int64_t ticket, llfe_image_result *results, llfe_shape *shapes,
                        int64_t shape_capacity, int64_t *shapes_needed) {
     if (!ctx || !results) return LLFE_ERR_INVALID;
@@ -1714,7 +1799,10 @@ int llfe_kmeans_attempts(llfe_ctx *ctx, int32_t n, llfe_kmeans_attempt *out) {
     if (!ctx || !out || n < 0) return LLFE_ERR_INVALID;
     if (ctx->any_inflight())
         return ctx->fail(LLFE_ERR_INVALID, "llfe_kmeans_attempts with submitted batches not yet collected");
-    Work &W = ctx->ws[0];
+    // the workspace the last k-means launch ran on (slot 0 for the synchronous entry points,
+    // the ticket's slot for llfe_submit_batch / llfe_submit_images)
+    if (!ctx->km_last) return ctx->fail(LLFE_ERR_INVALID, "no k-means launch yet");
+    Work &W = *ctx->km_last;
     if (n > W.km_n) return ctx->fail(LLFE_ERR_INVALID, "the last k-means launch had %d images", W.km_n);
     if (W.km_colors > kMaxK) return ctx->fail(LLFE_ERR_UNSUPPORTED, "attempt records only for n_colors <= %d", kMaxK);
     HIPCHK(ctx, hipSetDevice(ctx->device));

@@ -303,4 +303,8 @@ hipError_t launch_text_gray(const uint8_t *img, long long n, int cn, uint8_t *gr
 hipError_t launch_text_otsu_binary(const uint8_t *g, long long n, unsigned long long *hist, uint8_t *out,
                                    hipStream_t s);
 
+// llfe_submit_images (gather.hip): n device images of h x w x 3 u8 -> one packed batch;
+// tab (device) = n source addresses, then n row pitches in bytes
+hipError_t launch_gather_images(const uint64_t *tab, int n, int h, int w, uint8_t *dst, hipStream_t s);
+
 }  // namespace llfe

@@ -170,3 +170,109 @@ def test_pillow_bomb_guard_untouched_by_concurrent_decodes():
     assert all(isinstance(o, decode.DecodeError) for o in out)  # truncated frames
     assert Image.MAX_IMAGE_PIXELS == limit0
     assert warnings.filters == filters0
+
+
+class _Rec:
+    def __init__(self, level):
+        self.shadow_level = level
+
+
+class _FakePipelinedBackend:
+    """submit_images / collect stand-in: records what a launch held and how many were in
+    flight (the pipelined worker path without a GPU)."""
+
+    def __init__(self, cap=4):
+        self.inflight = 1
+        self.cap = cap
+        self.launches = {}
+        self.next = 0
+        self.open = 0
+        self.max_open = 0
+
+    def batch_capacity(self, h, w):
+        return self.cap
+
+    def submit_images(self, images, features, seed=0, indices=None, n_colors=5):
+        assert len(images) <= self.cap and len({tuple(im.shape) for im in images}) == 1
+        t = self.next
+        self.next += 1
+        self.open += 1
+        assert self.open <= self.inflight, "more launches in flight than the depth"
+        self.max_open = max(self.max_open, self.open)
+        self.launches[t] = [f"{int(np.asarray(im).sum())}:{i}" for im, i in zip(images, indices)]
+        return t
+
+    def collect(self, t):
+        import time
+
+        time.sleep(0.01)  # the launch's device time
+        self.open -= 1
+        return [_Rec(x) for x in self.launches.pop(t)]
+
+
+@pytest.mark.parametrize("depth", [1, 2, 3])
+def test_batcher_pipelined_keeps_launches_in_flight(depth):
+    fake = _FakePipelinedBackend(cap=4)
+    imgs = [np.full((3 + i % 2, 4, 3), i, np.uint8) for i in range(40)]
+    with MicroBatcher(features=("shadows",), max_batch=8, max_wait_ms=30, inflight=depth, backend=fake,
+                      freeze_gc=False) as b:
+        futs = [b.submit(im, index=1000 + i) for i, im in enumerate(imgs)]
+        res = [f.result(timeout=20)["shadows"]["shadow_level"] for f in futs]
+    # each request's own result and global index, whatever it was batched with
+    assert res == [f"{int(im.sum())}:{1000 + i}" for i, im in enumerate(imgs)]
+    assert sum(b.batch_sizes) == 40 and max(b.batch_sizes) <= 4
+    assert fake.max_open == b.max_in_flight == min(depth, len(b.batch_sizes))
+    if depth > 1:  # launch k + 1 submitted before launch k's collect returned
+        log = b.launch_log
+        assert any(log[k + 1][0] < log[k][2] for k in range(len(log) - 1))
+
+
+def test_batcher_pipelined_isolates_a_refused_launch(monkeypatch):
+    fake = _FakePipelinedBackend(cap=8)
+    fake.inflight = 2
+
+    def refuse(images, *a, **k):
+        raise RuntimeError("launch refused")
+
+    monkeypatch.setattr(fake, "submit_images", refuse)
+    from low_level_feature_extraction_amd import pipeline
+
+    def one(images, feats, **kw):
+        if int(images[0].sum()) == 0:
+            raise ValueError("bad image")
+        return [{"ok": kw["index_base"]}]
+
+    monkeypatch.setattr(pipeline, "run_batch", one)
+    with MicroBatcher(features=("shadows",), max_batch=8, max_wait_ms=30, inflight=2, backend=fake,
+                      freeze_gc=False) as b:
+        futs = [b.submit(np.full((2, 2, 3), v, np.uint8), index=7 + i) for i, v in enumerate([1, 0, 2])]
+        assert futs[0].result(timeout=10) == {"ok": 7}
+        with pytest.raises(ValueError, match="bad image"):
+            futs[1].result(timeout=10)
+        assert futs[2].result(timeout=10) == {"ok": 9}
+
+
+@pytest.mark.gpu
+def test_batcher_pipelined_on_gpu_device_images_equal_run_batch():
+    """The request path on the headline's serving loop: single device images from
+    concurrent requests, two launches in flight through llfe_submit_images, every result
+    equal to run_batch's for the same image and global index."""
+    import torch
+
+    from low_level_feature_extraction_amd import synth
+    from low_level_feature_extraction_amd.pipeline import run_batch
+
+    feats = ("colors", "shapes", "shadows")
+    imgs = [synth.synth_numpy(i, 270, 480, seed=11) for i in range(24)]
+    dev = [torch.from_numpy(im).to("cuda:0") for im in imgs]  # separately allocated
+    ref = run_batch(imgs, feats, seed=77, index_base=4000)
+    with MicroBatcher(features=feats, max_batch=8, max_wait_ms=50, inflight=2, seed=77) as b:
+        futs = [b.submit(t, index=4000 + i) for i, t in enumerate(dev)]
+        got = [f.result(timeout=120) for f in futs]
+    for i, (r, g) in enumerate(zip(ref, got)):
+        assert g["shapes"] == r["shapes"], i
+        assert g["shadows"] == r["shadows"], i
+        assert g["colors"] == r["colors"], i
+    assert b.max_in_flight == 2 and len(b.batch_sizes) >= 3
+    log = b.launch_log
+    assert any(log[k + 1][0] < log[k][2] for k in range(len(log) - 1)), "no two launches overlapped"

@@ -80,3 +80,14 @@ def test_gpus2_real_run_on_one_gpu():
     assert d["n_gpus"] == 2 and d["value"] > 0
     assert d["config"]["global_batch"] == 32
     assert d["config"]["parallelism"].startswith("replicas x2")
+
+
+def test_visible_gpus_from_kfd_topology_without_hip(tmp_path):
+    """The launching parent counts GPUs from sysfs (no HIP runtime in the parent)."""
+    nodes = tmp_path / "nodes"
+    for i, simds in enumerate([0, 1024, 1024, 0, 1024]):  # 2 CPU nodes, 3 GPUs
+        (nodes / str(i)).mkdir(parents=True)
+        (nodes / str(i) / "properties").write_text(f"cpu_cores_count 8\nsimd_count {simds}\nmax_waves_per_simd 8\n")
+    assert bench.visible_gpus(env={}, sysfs=str(nodes)) == 3
+    assert bench.visible_gpus(env={"HIP_VISIBLE_DEVICES": "0,1"}, sysfs=str(nodes)) == 2
+    assert bench.visible_gpus(env={}, sysfs=str(tmp_path / "absent")) == 0
