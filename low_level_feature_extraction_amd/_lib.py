@@ -220,8 +220,12 @@ def lib():
                 except Exception as e:  # pragma: no cover - surfaced to caller
                     if not os.path.exists(LIB_PATH):
                         raise RuntimeError(f"libllfe.so is missing and could not be built: {e}") from e
-            L = C.CDLL(LIB_PATH)
+            L = C.CDLL(os.environ.get("LLFE_LIB_PATH", LIB_PATH))
+            # (tools/debug/identity.sh runs older builds, which lack later entry points)
+            old_ok = os.environ.get("LLFE_LIB_PATH") is not None
             for name, (res, args) in SIGNATURES.items():
+                if old_ok and not hasattr(L, name):
+                    continue
                 f = getattr(L, name)
                 f.restype = res
                 f.argtypes = args

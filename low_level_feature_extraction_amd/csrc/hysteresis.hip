@@ -267,11 +267,14 @@ __global__ __launch_bounds__(64 * RW) void k_ccl_runs(const uint8_t *__restrict_
     uint32_t *const sflag = sfl[wv];
     const int ntiles = ntx * nty, nft = ftcount[0], wpr = (W + 63) >> 6;
     const int nb = lane * 32;  // this row's first node id
-    // kGrab tiles per workgroup per round from a work counter (ftcount[1]), read through
-    // workgroup barriers (a first version with a per-wave counter read by lane 0 and a
-    // `continue` for empty tiles faulted / hung on the GPU, round 5); the later passes walk
-    // the same list (no per-tile append: one global atomic per tile on one counter costs
-    // ~100 us per 512 x 1080p)
+    // kGrab tiles per workgroup per round from a work counter (ftcount[1]), its base read
+    // from LDS between two workgroup barriers: the tile index never crosses lanes.  (Round
+    // 5's first version broadcast a per-wave counter from lane 0 with __shfl; hipcc threaded
+    // the latch's lane != 0 path back to that shuffle, so lanes 1-63 relabelled list entry
+    // 0's tile without lane 0, whose root counter reset they skipped: roots[] ran past its
+    // buffer -- DESIGN.md §3, profiles/r6/ccl_root_cause/, tests/test_ccl_isa.py pins this
+    // loop's compiled shape.)  The later passes walk the same list (no per-tile append: one
+    // global atomic per tile on one counter costs ~100 us per 512 x 1080p)
     constexpr int kGrab = 2 * RW;
     for (;;) {
         if (threadIdx.x == 0) s_base = atomicAdd(&ftcount[1], kGrab);

@@ -65,9 +65,47 @@ def test_shape_mask(backend, orc, h, w):
         assert np.array_equal(got[i], exp), f"mismatch {(got[i] != exp).sum()} px"
 
 
+def _sparse_tile_images(h, w, seed):
+    """Flat images with a few hard step edges: flagged 64 x 64 hysteresis tiles separated by
+    empty ones, partial tiles at the right / bottom border, and edges along a tile's first
+    row (a horizontal step between rows 63 and 64), so some listed tiles hold candidates
+    only in the rows of lane 0 or lane 63."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for k in range(3):
+        img = np.full((h, w, 3), 40 + 60 * k, np.uint8)
+        if h > 66:
+            img[64:, : min(w, 64 + 16 * k)] = 220  # step between rows 63 / 64, left tiles only
+        for _ in range(2 + k):
+            y0, x0 = int(rng.integers(0, max(1, h - 8))), int(rng.integers(0, max(1, w - 8)))
+            img[y0:y0 + int(rng.integers(3, 20)), x0:x0 + int(rng.integers(3, 20))] = rng.integers(0, 256, 3)
+        out.append(img)
+    return np.stack(out)
+
+
+@pytest.mark.parametrize("h,w", [(5, 7), (31, 33), (70, 7), (130, 200), (200, 330), (257, 129)])
+def test_shape_mask_sparse_and_partial_tiles(backend, orc, h, w):
+    """The tile shapes round 5's first k_ccl_runs ran away on (a listed tile
+    whose rows >= 1 hold candidates, relabelled by lanes 1-63 without lane 0): tiny and
+    partial tiles, empty tiles between flagged ones, candidates only along a tile's first
+    or last row, with and without the stencil's tile flags; bit-exact vs the oracle."""
+    import os
+
+    x = np.concatenate([_imgs(h, w), _sparse_tile_images(h, w, h * 7 + w)])
+    got = backend.shape_mask(x).cpu().numpy()
+    for i in range(len(x)):
+        assert np.array_equal(got[i], orc.shape_mask(x[i])), i
+    os.environ["LLFE_HYST_TILE_FLAGS"] = "0"
+    try:
+        assert np.array_equal(backend.shape_mask(x).cpu().numpy(), got)
+    finally:
+        del os.environ["LLFE_HYST_TILE_FLAGS"]
+
+
 @pytest.mark.parametrize("h,w", [(5, 7), (65, 130), (270, 480), (1080, 1920)])
 def test_shape_mask_without_tile_flags(backend, orc, h, w, monkeypatch):
-    """The hysteresis without the stencil's tile flags (one workgroup per tile, the path a
+    """The hysteresis without the stencil's tile flags (every tile listed and handed out
+    through the same work counter, empty ones exiting after their row masks: the path a
     class map from elsewhere takes) gives the same masks as with them (the default)."""
     x = np.concatenate([_imgs(h, w), np.stack([_smooth_random(h, w, 3)])])
     monkeypatch.setenv("LLFE_HYST_TILE_FLAGS", "0")
