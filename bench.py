@@ -191,7 +191,7 @@ def e2e_host(be, imgs_dev, feats, steps, seed, index_base):
                       f"H2D + full GPU path per batch, two batches in flight (llfe_submit_batch / llfe_collect_batch)"}
 
 
-def served_batcher(imgs_dev, feats, batches, seed, inflight):
+def served_batcher(imgs_dev, feats, batches, seed, inflight, device):
     """The product request path at load (the reference serves one
     image per /analyze call, app/api/v1/endpoints/analyze.py:94-111): P concurrent asyncio
     producers each await ``MicroBatcher.analyze`` on its own single 1080p device image
@@ -211,7 +211,7 @@ def served_batcher(imgs_dev, feats, batches, seed, inflight):
     producers = (inflight + 1) * B  # enough outstanding requests to keep every slot full
     dev = [imgs_dev[i % B].clone() for i in range(producers)]  # one allocation per request image
     torch.cuda.synchronize()
-    bt = MicroBatcher(features=feats, max_batch=B, max_wait_ms=2.0, inflight=inflight, seed=seed)
+    bt = MicroBatcher(features=feats, max_batch=B, max_wait_ms=2.0, inflight=inflight, seed=seed, device=device)
 
     async def drive(n_requests):
         counter = itertools.count()
@@ -435,10 +435,11 @@ def main():
     ap.add_argument("--e2e-jpeg-steps", type=int, default=10, help="0 disables the JPEG end-to-end line")
     ap.add_argument("--e2e-alt-contours", type=int, default=1,
                     help="1: also run the JPEG leg with the other contour mode (host <-> gpu)")
-    ap.add_argument("--e2e-at-scale", action="store_true",
-                    help="also run the e2e lines when WORLD_SIZE > 1 (off by default: every rank would pin "
-                         "~10 GB of host batches and decode on its 1/N core share while the scaling run "
-                         "only needs `value`)")
+    ap.add_argument("--e2e-at-scale", nargs="?", const="on", default="on", choices=["on", "off"],
+                    help="the e2e lines also at WORLD_SIZE > 1 (default on: every rank decodes its own shard "
+                         "on its NUMA node's core share at the same time, which is the 8-rank node's host-side "
+                         "contention -- decode cores, PCIe, pinned memory placement; each line then carries a "
+                         "per-rank breakdown)")
     ap.add_argument("--per-class-steps", type=int, default=12,
                     help="steps of an all-ui and an all-photo batch (SURVEY.md 8d per-class throughput; 4 steps "
                          "left the pipeline's fill and drain in a third of the timed region: ui 21-30k across "
@@ -480,7 +481,7 @@ def main():
         sys.exit(subprocess.call(launch_ranks(args.gpus, sys.argv[1:])))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world > 1 and not args.e2e_at_scale:
+    if world > 1 and args.e2e_at_scale == "off":
         args.e2e_host_steps = args.e2e_png_steps = args.e2e_jpeg_steps = 0
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -489,6 +490,14 @@ def main():
     share_gpu = os.environ.get("LLFE_BENCH_SHARE_GPU") == "1"
     if share_gpu:
         local = 0
+    # host placement before any thread pool or pinned buffer exists: this rank's threads
+    # (decode, contour pool, the serving loop) on its GPU's NUMA node, that node's cores
+    # split among the ranks whose GPUs sit on it (placement.py; LLFE_NUMA_BIND=0: off)
+    from low_level_feature_extraction_amd import placement
+
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+    placed = placement.bind(int(os.environ.get("LOCAL_RANK", "0")), local_world,
+                            [0] * local_world if share_gpu else None)
 
     import torch
 
@@ -689,7 +698,7 @@ def main():
     served = None
     if args.batcher_steps > 0 and pipelined:
         barrier()
-        served = served_batcher(imgs, feats, args.batcher_steps, args.seed, be.inflight)
+        served = served_batcher(imgs, feats, args.batcher_steps, args.seed, be.inflight, local)
         barrier()
 
     # (the e2e lines run on every rank before rank 0 reports: each rank pays its own
@@ -776,7 +785,10 @@ def main():
         t = B * steps / line["value"]
         line = dict(line)
         line["value"] = round(B * world * steps / shard.max_over_ranks(t, device=coll_dev), 2)
-        line["per_rank"] = True
+        # each rank's own rate and host placement (its GPU's NUMA node and CPU share)
+        line["per_rank"] = shard.all_gather({"rank": rank, "value": round(B * steps / t, 2),
+                                             "numa_node": (placed or {}).get("numa_node"),
+                                             "cpus": (placed or {}).get("cpus")})
         return line
 
     served = all_ranks(served, args.batcher_steps)
@@ -846,6 +858,9 @@ def main():
                             "in_timed_region": True},
         "per_class": per_class,
         "served_batcher": served,
+        # this rank's host placement (placement.py): GPU -> NUMA node -> its share of that
+        # node's cores, the threads its pools take; every rank's in the e2e lines' per_rank
+        "placement": placed,
         # wall share of the timed steps the host contour pool spent tracing (host mode)
         "host_contour_busy": round(host_ct["busy_ms"] / 1e3 / max(t1 - t0, 1e-9), 3),
         "cpu_baseline": cpu,

@@ -148,7 +148,8 @@ int llfe_abi_version(void);
  * also uses PyTorch-ROCm loads libllfe after torch, so both share torch's runtime. */
 const char *llfe_hip_runtime(void);
 /* host threads a new ctx gives its contour pool: the process's share of the usable CPUs
- * (affinity mask and cgroup quota) / LOCAL_WORLD_SIZE, at most 16; LLFE_HOST_THREADS
+ * -- LLFE_RANK_CPUS when the rank was pinned to its GPU's NUMA node (placement.py), else
+ * (affinity mask and cgroup quota) / LOCAL_WORLD_SIZE -- at most 16; LLFE_HOST_THREADS
  * overrides.  Host only. */
 int llfe_default_host_threads(void);
 /* enable (1) / disable (0) event timing; enabling resets the statistics */

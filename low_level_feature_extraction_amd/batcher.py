@@ -50,7 +50,8 @@ def _is_torch(x) -> bool:
 class MicroBatcher:
     def __init__(self, features: Sequence[str] = ("colors", "shapes", "shadows"), max_batch: int = 64,
                  max_wait_ms: float = 2.0, run: Optional[Callable] = None, inflight: int = 2,
-                 seed: Optional[int] = None, n_colors: int = 5, freeze_gc: bool = True, backend=None):
+                 seed: Optional[int] = None, n_colors: int = 5, freeze_gc: bool = True, backend=None,
+                 device: Optional[int] = None):
         if max_batch < 1:
             raise ValueError("max_batch must be >= 1")
         if inflight not in (1, 2, 3):
@@ -64,6 +65,7 @@ class MicroBatcher:
         self._seed = seed
         self._run = run
         self._backend = backend  # (tests: a stand-in with submit_images / collect / inflight)
+        self._device = device  # GPU of the worker's context (default: LLFE_DEVICE / LOCAL_RANK)
         self._q: "queue.Queue" = queue.Queue()
         self.batch_sizes: list = []  # sizes of the launches so far (diagnostics)
         # (submit time, collect-start time, collect-end time) per launch, worker clock
@@ -196,7 +198,7 @@ class MicroBatcher:
             else:
                 from .backend import Backend
 
-                be = Backend.get()  # this thread's own context
+                be = Backend.get(self._device)  # this thread's own context
             if self.inflight > 1:
                 be.inflight = self.inflight
             depth = self.inflight

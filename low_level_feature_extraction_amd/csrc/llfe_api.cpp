@@ -375,9 +375,11 @@ int usable_cpus() {
     return std::max(1, n);
 }
 
-// host cores per GPU process: the usable cores shared by the LOCAL_WORLD_SIZE ranks
-// torchrun starts on the node
+// host cores per GPU process: the rank's own share when placement.bind() pinned it to its
+// GPU's NUMA node (LLFE_RANK_CPUS), else the usable cores shared by the LOCAL_WORLD_SIZE
+// ranks torchrun starts on the node
 int cores_per_process() {
+    if (const char *rc = getenv("LLFE_RANK_CPUS"); rc && atoi(rc) > 0) return atoi(rc);
     int local = 1;
     if (const char *lw = getenv("LOCAL_WORLD_SIZE"); lw && atoi(lw) > 0) local = atoi(lw);
     return std::max(1, usable_cpus() / local);

@@ -182,13 +182,17 @@ def usable_cores() -> int:
 
 
 def default_decode_threads() -> int:
-    """The rank's share of the host cores: usable cores / LOCAL_WORLD_SIZE (one process
-    per GPU shares the node's cores), LLFE_DECODE_THREADS overrides."""
+    """The rank's share of the host cores: the set placement.bind() pinned it to
+    (LLFE_RANK_CPUS), else usable cores / LOCAL_WORLD_SIZE (one process per GPU shares the
+    node's cores); LLFE_DECODE_THREADS overrides."""
     import os
 
     env = os.environ.get("LLFE_DECODE_THREADS")
     if env and int(env) > 0:
         return int(env)
+    rank_cpus = os.environ.get("LLFE_RANK_CPUS")
+    if rank_cpus and int(rank_cpus) > 0:
+        return min(int(rank_cpus), 64)
     local = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1))
     return max(1, min(usable_cores() // local, 64))
 

@@ -41,6 +41,17 @@ def max_over_ranks(value: float, device=None) -> float:
     return float(t.item())
 
 
+def all_gather(obj) -> List:
+    """Every rank's ``obj`` (a small picklable record), in rank order, on every rank;
+    ``[obj]`` without a process group."""
+    dist = _dist()
+    if dist is None:
+        return [obj]
+    out: List = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out
+
+
 def barrier(device=None):
     import torch
 
