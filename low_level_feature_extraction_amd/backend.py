@@ -377,16 +377,23 @@ class Backend:
         descs = np.zeros(n, Backend._DESC_DTYPE)
         keep = []
         ptr, hh, ww, st, dev = [], [], [], [], []
+        u8 = None
         for i, im in enumerate(images):
             if _is_torch(im):
-                t = im
-                if t.dtype != _torch().uint8 or t.dim() != 3 or t.shape[2] != 3:
-                    raise ValueError(f"image {i}: expected H x W x 3 uint8, got {tuple(t.shape)} {t.dtype}")
-                if t.stride(2) != 1 or t.stride(1) != 3 or t.stride(0) < 3 * t.shape[1]:
-                    t = t.contiguous()
+                # (few attribute calls per image: at serving rates this loop holds the GIL
+                # once per request; a strided tensor is packed by one copy)
+                if u8 is None:
+                    u8 = _torch().uint8
+                shp = im.shape
+                if len(shp) != 3 or shp[2] != 3 or im.dtype != u8:
+                    raise ValueError(f"image {i}: expected H x W x 3 uint8, got {tuple(shp)} {im.dtype}")
+                t = im if im.is_contiguous() else im.contiguous()
                 ptr.append(t.data_ptr())
-                st.append(t.stride(0))
-                dev.append(int(t.is_cuda))
+                st.append(3 * shp[1])
+                dev.append(1 if t.is_cuda else 0)
+                hh.append(shp[0])
+                ww.append(shp[1])
+                keep.append(t)
             else:
                 t = np.asarray(im)
                 if t.dtype != np.uint8 or t.ndim != 3 or t.shape[2] != 3:
@@ -396,9 +403,9 @@ class Backend:
                 ptr.append(t.ctypes.data)
                 st.append(t.strides[0])
                 dev.append(0)
-            hh.append(t.shape[0])
-            ww.append(t.shape[1])
-            keep.append(t)
+                hh.append(t.shape[0])
+                ww.append(t.shape[1])
+                keep.append(t)
         descs["data"], descs["height"], descs["width"] = ptr, hh, ww
         descs["row_stride"], descs["on_device"] = st, dev
         idx = np.ascontiguousarray(np.arange(n) if indices is None else indices, dtype=np.int64)

@@ -47,11 +47,72 @@ def _is_torch(x) -> bool:
     return type(x).__module__.startswith("torch") and hasattr(x, "data_ptr")
 
 
+def _settle(fut, r, e):
+    if not fut.done():
+        if e is not None:
+            fut.set_exception(e)
+        else:
+            fut.set_result(r)
+
+
+def _settle_many(items):
+    for fut, r in items:
+        if not fut.done():
+            fut.set_result(r)
+
+
+class _LoopFuture:
+    """The request side of ``analyze``: an asyncio future of the caller's loop, resolved
+    from the batcher's threads.  A batch's results reach each loop in ONE
+    call_soon_threadsafe (``_resolve``), not one wake-up and one wrapped concurrent future
+    per request -- at ~20k requests/s that per-request overhead is what holds the event
+    loop's GIL."""
+
+    __slots__ = ("loop", "fut")
+
+    def __init__(self, loop, fut):
+        self.loop, self.fut = loop, fut
+
+    def set_running_or_notify_cancel(self) -> bool:
+        return not self.fut.cancelled()  # (a cancel racing this read only loses its result)
+
+    def done(self) -> bool:
+        return self.fut.done()
+
+    def set_result(self, r):
+        self._post(_settle, self.fut, r, None)
+
+    def set_exception(self, e):
+        self._post(_settle, self.fut, None, e)
+
+    def _post(self, fn, *args):
+        try:
+            self.loop.call_soon_threadsafe(fn, *args)
+        except RuntimeError:  # the caller's loop is closed: nobody waits for this request
+            pass
+
+
+def _resolve(futs, results):
+    """set_result over a batch: concurrent futures directly, asyncio ones per loop in one
+    call."""
+    by_loop: dict = {}
+    for f, r in zip(futs, results):
+        if isinstance(f, _LoopFuture):
+            by_loop.setdefault(f.loop, []).append((f.fut, r))
+        else:
+            f.set_result(r)
+    for loop, items in by_loop.items():
+        try:
+            loop.call_soon_threadsafe(_settle_many, items)
+        except RuntimeError:
+            pass
+
+
 class MicroBatcher:
     def __init__(self, features: Sequence[str] = ("colors", "shapes", "shadows"), max_batch: int = 64,
                  max_wait_ms: float = 2.0, run: Optional[Callable] = None, inflight: int = 2,
                  seed: Optional[int] = None, n_colors: int = 5, freeze_gc: bool = True, backend=None,
-                 device: Optional[int] = None):
+                 device: Optional[int] = None, fill_wait_ms: float = 8.0):
         if max_batch < 1:
             raise ValueError("max_batch must be >= 1")
         if inflight not in (1, 2, 3):
@@ -59,6 +120,9 @@ class MicroBatcher:
         self.features = tuple(getattr(f, "value", f) for f in features)
         self.max_batch = int(max_batch)
         self.max_wait = max(0.0, float(max_wait_ms)) / 1e3
+        # while launches are in flight (the GPU is busy for a step anyway) a partial batch
+        # waits up to fill_wait_ms for more requests: fuller launches, the same latency bound
+        self.fill_wait = max(self.max_wait, float(fill_wait_ms) / 1e3)
         self.inflight = int(inflight)
         self.n_colors = int(n_colors)
         self.freeze_gc = bool(freeze_gc)
@@ -82,6 +146,11 @@ class MicroBatcher:
         """Queue one H x W x 3 BGR uint8 image (numpy array or torch tensor, host or
         device); the future yields its result dict.  ``index``: its global index (default:
         the next one of the process counter)."""
+        fut: Future = Future()
+        self._enqueue(image, fut, index)
+        return fut
+
+    def _enqueue(self, image, fut, index):
         if self._closed:
             raise RuntimeError("MicroBatcher is closed")
         if _is_torch(image):
@@ -96,9 +165,7 @@ class MicroBatcher:
             from .color_extractor import _next_index
 
             index = _next_index()
-        fut: Future = Future()
         self._q.put((img, fut, int(index)))
-        return fut
 
     def submit_bytes(self, image_bytes: bytes, preprocessing: str = "auto") -> Future:
         """Decode + preprocess (validate_and_preprocess_image semantics) on the calling
@@ -108,8 +175,12 @@ class MicroBatcher:
 
         return self.submit(preprocess_decoded(decode_bgr(image_bytes), preprocessing))
 
-    async def analyze(self, image) -> dict:
-        return await asyncio.wrap_future(self.submit(image))
+    async def analyze(self, image, index: Optional[int] = None) -> dict:
+        """``submit`` for an async endpoint: awaits the image's result dict."""
+        loop = asyncio.get_running_loop()
+        fut = loop.create_future()
+        self._enqueue(image, _LoopFuture(loop, fut), index)
+        return await fut
 
     def close(self, timeout: Optional[float] = None):
         if not self._closed:
@@ -124,19 +195,19 @@ class MicroBatcher:
         self.close()
 
     # ---------------------------------------------------------------- worker
-    def _gather(self, block: bool):
+    def _gather(self, block: bool, wait: Optional[float] = None):
         """Up to max_batch queued requests: the first one (waiting for it when ``block``,
-        else at most max_wait), then whatever arrives within max_wait of it.  Returns
-        (items, stop)."""
+        else at most ``wait``), then whatever arrives within ``wait`` (default max_wait) of
+        it.  Returns (items, stop)."""
+        wait = self.max_wait if wait is None else wait
         try:
-            first = self._q.get() if block else self._q.get(timeout=self.max_wait) if self.max_wait > 0 \
-                else self._q.get_nowait()
+            first = self._q.get() if block else self._q.get(timeout=wait) if wait > 0 else self._q.get_nowait()
         except queue.Empty:
             return [], False
         if first is _STOP:
             return [], True
         items = [first]
-        deadline = time.monotonic() + self.max_wait
+        deadline = time.monotonic() + wait
         while len(items) < self.max_batch:
             left = deadline - time.monotonic()
             try:
@@ -172,8 +243,7 @@ class MicroBatcher:
             self.batch_sizes.append(len(live))
             try:
                 res = self._run([im for im, _, _ in live], self.features)
-                for (_, f, _), r in zip(live, res):
-                    f.set_result(r)
+                _resolve([f for _, f, _ in live], res)
             except Exception as e:
                 if len(live) == 1:
                     live[0][1].set_exception(e)
@@ -224,8 +294,7 @@ class MicroBatcher:
                 for _, f, _ in live:
                     f.set_exception(e)
                 return
-            for (_, f, _), r in zip(live, out):
-                f.set_result(r)
+            _resolve([f for _, f, _ in live], out)
 
         def finish_oldest():
             nonlocal froze
@@ -267,7 +336,7 @@ class MicroBatcher:
             while not stop or pending:
                 live = []
                 if not stop:
-                    live, stop = self._gather(block=not pending)
+                    live, stop = self._gather(block=not pending, wait=self.fill_wait if pending else None)
                 if not live:
                     if pending:
                         finish_oldest()

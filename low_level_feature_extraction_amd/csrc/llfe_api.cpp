@@ -675,7 +675,7 @@ int color_stage(llfe_ctx *ctx, Work &W, const uint8_t *img, const int8_t *noise,
     uint32_t *hist = W.d_pmeta.p, *cl = hist + (size_t)n * kParts, *uq = hist + (size_t)2 * n * kParts,
              *cc = uq + (size_t)n * kParts;
     HIPCHK(ctx, hipMemsetAsync(hist, 0, sizeof(uint32_t) * n * kParts, s));
-    HIPCHK(ctx, W.d_segtab.ensure((size_t)n * uq_steps(P) * kParts));
+    HIPCHK(ctx, W.d_segtab.ensure((size_t)n * uq_tab_words(P)));
     if (!noise) {
         HIPCHK(ctx, W.d_nfield.ensure((size_t)noise_field_pixels(P)));
         HIPCHK(ctx, launch_uq_noise(noise, W.d_nfield.p, P, seed, s));

@@ -237,6 +237,7 @@ int64_t noise_field_pixels(int64_t P);
 hipError_t launch_uq_noise(const int8_t *noise, int8_t *field, int64_t P, uint64_t seed, hipStream_t s);
 // steps of 4096 pixels per image (k_uq_scatter's segments; its run table is n x steps x 64 u32)
 int64_t uq_steps(int64_t P);
+int64_t uq_tab_words(int64_t P);  // k_uq_scatter's run table, u32 words per image
 hipError_t launch_uq_scatter(const uint8_t *bgr, const int8_t *noise, const int8_t *field, int n, int h, int w,
                              uint64_t seed, ImgIndex index, int64_t key_stride, uint32_t *hist, uint32_t *tab,
                              uint32_t *seg, hipStream_t s);

@@ -26,3 +26,7 @@ for n, v in k.items():
 for e in ("e2e_host", "e2e_png", "e2e_jpeg"):
     if d.get(e): print(e, d[e]["value"])
 PY
+if [ "${PROFILE:-0}" = 1 ]; then
+    timeout -k 10 1200 bash tools/profile.sh $TAG > gpurun_out/${TAG}_profile.log 2>&1 || { tail -20 gpurun_out/${TAG}_profile.log; exit 1; }
+    tail -45 gpurun_out/${TAG}_profile.log
+fi
