@@ -339,6 +339,20 @@ __device__ __forceinline__ unsigned long long scan_u64_wg(unsigned long long v, 
     return r;
 }
 
+// per lane: bit `lane` of the wave-uniform mask m ? a : b (one v_cndmask reading m from an
+// SGPR pair); the lanes >= d of a wave as such a mask
+__device__ __forceinline__ uint32_t lane_pick(unsigned long long m, uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, %2, %1, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+    return r;
+}
+__device__ __forceinline__ unsigned long long lanes_from(int d) {
+    const unsigned long long m = d <= 0 ? ~0ull : (d >= 64 ? 0ull : (~0ull << d));
+    // (d is wave-uniform; readfirstlane keeps the mask in SGPRs for lane_pick's operand)
+    return ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(m >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)m);
+}
+
 // grid (64, n).  Reads the partition's keys as its runs in the step segments (`tab`), writes
 // the sorted unique keys to `skeys` at the partition's place in key order (capacity: its
 // hist count), and up to 4096 cube entries to `seg_cubes`.
@@ -380,7 +394,8 @@ __global__ __launch_bounds__(UT) void k_uq_part(const uint32_t *__restrict__ seg
     const uint16_t *sg = (const uint16_t *)(seg + (size_t)img * key_stride);
     const long long nsteps = (P + SK - 1) / SK;
     const unsigned long long *tb = tab + (size_t)img * nsteps * NPART + R;
-    const int lane = t & 63, wid = t >> 6;
+    // (wid through readfirstlane: the run addresses below stay scalar)
+    const int lane = t & 63, wid = __builtin_amdgcn_readfirstlane(t >> 6);
     constexpr int RG = 8;  // runs (and tail loads) in flight per lane (16: 97 VGPRs, one workgroup per CU)
     auto mark = [&](uint32_t k) {
         // flat regions put one colour in every lane: test the bit with a (broadcast) read
@@ -388,12 +403,16 @@ __global__ __launch_bounds__(UT) void k_uq_part(const uint32_t *__restrict__ seg
         const uint32_t wi = ((k >> 16) & 3u) * 2048 + ((k >> 5) & 2047u), bit = 1u << (k & 31u);
         if (k != 0xFFFFFFFFu && !(W[wi] & bit)) atomicOr(&W[wi], bit);
     };
-    // key ix of a run: its 16-bit (g, b) from the segment, its red bits i (r = 4R + i) from
-    // the run's sub-run bounds (run_entry)
-    auto key_at = [&](const uint16_t *rp, uint32_t ix, uint32_t blo, uint32_t bhi) {
-        const uint32_t b1 = blo >> 12 & 0x1FFFu, b2 = (blo >> 25 | bhi << 7) & 0x1FFFu, b3 = bhi >> 6 & 0x1FFFu;
-        const uint32_t i = (ix >= b1) + (ix >= b2) + (ix >= b3);
-        return (uint32_t)rp[ix] | (i << 16);
+    const uint32_t one = 0x10000u, two = 0x20000u, three = 0x30000u;
+    // the red bits (r & 3) << 16 of keys s0 .. s0 + 63 of a run, lane = key - s0: its
+    // sub-run bounds (run_entry, uniform) as lane masks built in scalar code, three
+    // v_cndmask per key (compares into an SGPR pair would each need wait states)
+    auto red_bits = [&](uint32_t lo, uint32_t hi, int s0) {
+        const int b1 = (int)((lo >> 12) & 0x1FFFu), b2 = (int)(((lo >> 25) | (hi << 7)) & 0x1FFFu),
+                  b3 = (int)((hi >> 6) & 0x1FFFu);
+        uint32_t r = lane_pick(lanes_from(b1 - s0), one, 0u);
+        r = lane_pick(lanes_from(b2 - s0), two, r);
+        return lane_pick(lanes_from(b3 - s0), three, r);
     };
     for (long long base = 0; base < nsteps; base += (UT / 64) * 64) {
         const long long sl = base + wid + (UT / 64) * lane;  // this lane's run
@@ -406,9 +425,8 @@ __global__ __launch_bounds__(UT) void k_uq_part(const uint32_t *__restrict__ seg
 #pragma unroll
             for (int j = 0; j < RG; j++) {
                 const uint32_t lo = __builtin_amdgcn_readlane(elo, j0 + j), hi = __builtin_amdgcn_readlane(ehi, j0 + j);
-                const size_t st = (size_t)(base + wid + (UT / 64) * (j0 + j));
-                kk[j] = (uint32_t)lane < (hi >> 19) ? key_at(sg + st * SK + (lo & 0xFFFu), (uint32_t)lane, lo, hi)
-                                                    : 0xFFFFFFFFu;
+                const uint16_t *rp = sg + (size_t)(base + wid + (UT / 64) * (j0 + j)) * SK + (lo & 0xFFFu);
+                kk[j] = (uint32_t)lane < (hi >> 19) ? ((uint32_t)rp[lane] | red_bits(lo, hi, 0)) : 0xFFFFFFFFu;
             }
 #pragma unroll
             for (int j = 0; j < RG; j++) mark(kk[j]);
@@ -423,7 +441,7 @@ __global__ __launch_bounds__(UT) void k_uq_part(const uint32_t *__restrict__ seg
 #pragma unroll
                     for (int i = 0; i < RG; i++) {
                         const uint32_t ix = i0 + 64 * i + lane;
-                        q[i] = ix < c ? key_at(rp, ix, lo, hi) : 0xFFFFFFFFu;
+                        q[i] = ix < c ? ((uint32_t)rp[ix] | red_bits(lo, hi, (int)(i0 + 64 * i))) : 0xFFFFFFFFu;
                     }
 #pragma unroll
                     for (int i = 0; i < RG; i++) mark(q[i]);
