@@ -208,7 +208,6 @@ constexpr int kMaxSlots = 3;
 // device workspace of one chunk in flight
 struct Work {
     DevBuf<uint8_t> d_in, d_cls, d_sroot, d_tflag;  // d_tflag: the stencil's hysteresis tile flags
-    DevBuf<int> d_stq;  // the row-streaming stencil's work counter (StencilParams::queue)
     bool tflag_valid = false;  // d_tflag belongs to the class map in d_cls (stencil_params)
     DevBuf<int8_t> d_noise, d_nfield;  // d_nfield: the launch's noise field (unique.hip)
     DevBuf<uint64_t> d_bits, d_ebits;
@@ -572,12 +571,6 @@ int hyst_work(llfe_ctx *ctx, Work &W, int n, int h, int w, HystWork *out) {
 int stencil_params(llfe_ctx *ctx, Work &W, int n, int h, int w, hipStream_t s, StencilParams *sp) {
     *sp = ctx->sp;
     W.tflag_valid = false;
-    // the stencil's items through a work counter (LLFE_ST_QUEUE=0: one static wave per item)
-    static const bool st_queue = !(getenv("LLFE_ST_QUEUE") && !strcmp(getenv("LLFE_ST_QUEUE"), "0"));
-    if (st_queue) {
-        HIPCHK(ctx, W.d_stq.ensure(1));
-        sp->queue = W.d_stq.p;
-    }
     // LLFE_HYST_TILE_FLAGS=0: no flags, the hysteresis visits every tile (its test path)
     if (const char *e = getenv("LLFE_HYST_TILE_FLAGS"))
         if (!strcmp(e, "0")) return LLFE_OK;

@@ -26,9 +26,6 @@ struct StencilParams {
     // (row-streaming kernel, with cls) n x ceil(h / 64) x ceil(w / 64) bytes, zeroed by the
     // caller: set to 1 for every 64 x 64 hysteresis tile holding a class != 1 pixel
     uint8_t *tflag;
-    // (row-streaming kernel) one device int: its items go through this work counter
-    // (zeroed by the launch); null: one static wave per item
-    int *queue;
 };
 
 // shape pyc @L18-24 + shadow pyc @L8-21 for a packed NHWC batch.

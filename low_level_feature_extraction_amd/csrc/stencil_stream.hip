@@ -292,6 +292,12 @@ __device__ __forceinline__ void rowpass4(uint32_t B, const float *__restrict__ k
 #ifndef LLFE_ST_MINW
 #define LLFE_ST_MINW 4
 #endif
+#ifndef LLFE_ST_LPT
+#define LLFE_ST_LPT 0
+#endif
+#ifndef LLFE_ST_STORE_AUX
+#define LLFE_ST_STORE_AUX 2  // the class-map stores' cache policy (2: non-temporal)
+#endif
 // One wave's work item: strip x segment of one image.  `wid` is wave-uniform (an SGPR):
 // every per-wave quantity below -- strip, segment, row bounds, border flags -- then stays
 // scalar and its branches cost no exec masking.
@@ -461,7 +467,7 @@ __device__ __forceinline__ void stencil_wave(int wid, const uint8_t *__restrict_
                     if (out_fast) {
                         // buffer store: row offset yn * W in an SGPR, the lane's column x in a
                         // VGPR that never changes -- no per-lane 64-bit address per step
-                        __builtin_amdgcn_raw_buffer_store_b32(o, crs, (uint32_t)x, yn * W, 2 /* nt */);
+                        __builtin_amdgcn_raw_buffer_store_b32(o, crs, (uint32_t)x, yn * W, LLFE_ST_STORE_AUX);
                     } else if (out_lane) {
                         uint8_t *const dst = cimg + ((size_t)yn * W + x);
 #pragma unroll
@@ -547,45 +553,22 @@ template <bool CLS, bool SHD>
 __global__ __launch_bounds__(64 * kWavesPerBlock, LLFE_ST_MINW) void k_stencil_stream(
     const uint8_t *__restrict__ bgr, int H, int W, int strips, int segs, int seg_rows, int total_waves, int vec,
     uint8_t *__restrict__ cls, uint2 *__restrict__ wave_part, StencilParams prm) {
-    const int wid = blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    int wid = blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     if (wid >= total_waves) return;  // whole wave leaves
-    stencil_wave<CLS, SHD>(wid, bgr, H, W, strips, segs, seg_rows, vec, cls, wave_part, prm);
-}
-
-// Work-queue form (round 6): one-wave workgroups, as many as are resident at once, each
-// taking items from a counter until the batch is done.  The static grid's waves are
-// dispatched in order to fixed XCDs (workgroup i on XCD i mod 8): a freed slot waits
-// behind a workgroup whose XCD is full, and with items of unequal length (Canny rows on
-// "ui" images, the border strips' byte loads) the slots sat ~27 % empty over the launch
-// (PMC: wave lifetimes / (slots x duration)).  Items go in LPT order -- the
-// two border strips of every segment first, then the interior ones.  The item index comes
-// from LDS between two barriers, the form tests/test_ccl_isa.py pins for k_ccl_runs (no
-// cross-lane broadcast of a lane's value; DESIGN.md §3 "The round-5 fault").
-template <bool CLS, bool SHD>
-__global__ __launch_bounds__(64, LLFE_ST_MINW) void k_stencil_stream_q(
-    const uint8_t *__restrict__ bgr, int H, int W, int strips, int segs, int seg_rows, int total_waves, int vec,
-    uint8_t *__restrict__ cls, uint2 *__restrict__ wave_part, StencilParams prm) {
-    __shared__ int s_item;
-    const int per_img_seg = total_waves / strips;  // (image, segment) pairs
-    const int n_edge = strips > 1 ? 2 * per_img_seg : per_img_seg;
-    for (;;) {
-        if (threadIdx.x == 0) s_item = atomicAdd(prm.queue, 1);
-        __syncthreads();
-        const int q = __builtin_amdgcn_readfirstlane(s_item);
-        __syncthreads();
-        if (q >= total_waves) break;
-        // LPT order: items [0, n_edge) are the border strips (0 and strips - 1) of every
-        // (image, segment), the rest the interior strips
-        int wid;
-        if (q < n_edge) {
-            const int pair = strips > 1 ? q >> 1 : q;
-            wid = pair * strips + (strips > 1 && (q & 1) ? strips - 1 : 0);
+#if LLFE_ST_LPT
+    // (experiment) LPT dispatch order: the border strips (0 and strips - 1) of every (image,
+    // segment) first -- their byte loads make them the longest items -- then the interior
+    if (strips > 2) {
+        const int n_edge = 2 * (total_waves / strips);
+        if (wid < n_edge) {
+            wid = (wid >> 1) * strips + ((wid & 1) ? strips - 1 : 0);
         } else {
-            const int r = q - n_edge, inner = strips - 2;
+            const int r = wid - n_edge, inner = strips - 2;
             wid = (r / inner) * strips + 1 + r % inner;
         }
-        stencil_wave<CLS, SHD>(wid, bgr, H, W, strips, segs, seg_rows, vec, cls, wave_part, prm);
     }
+#endif
+    stencil_wave<CLS, SHD>(wid, bgr, H, W, strips, segs, seg_rows, vec, cls, wave_part, prm);
 }
 
 // per image: sum of its waves' (sum, count)
@@ -647,38 +630,16 @@ hipError_t launch_stencil_stream(const uint8_t *bgr, int n, int h, int w, uint8_
     const long long waves = (long long)n * strips * segs;
     const int vec = ((((uintptr_t)bgr | (uintptr_t)cls) & 3) == 0 && (w & 3) == 0) ? 1 : 0;
     const bool shd = shadow_sum != nullptr;
-    if (p.queue) {  // work queue: the resident one-wave workgroups (4 per SIMD) loop over the items
-        static int cus = 0;
-        if (!cus) {
-            int dev = 0;
-            if (hipGetDevice(&dev) != hipSuccess ||
-                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-                cus = 256;
-        }
-        const int grid = (int)std::min<long long>(waves, (long long)cus * 4 * LLFE_ST_MINW);
-        hipError_t e = hipMemsetAsync(p.queue, 0, sizeof(int), s);
-        if (e != hipSuccess) return e;
-        if (cls && shd)
-            hipLaunchKernelGGL((k_stencil_stream_q<true, true>), dim3(grid), dim3(64), 0, s, bgr, h, w, strips, segs,
-                               seg_rows, (int)waves, vec, cls, wave_part, p);
-        else if (cls)
-            hipLaunchKernelGGL((k_stencil_stream_q<true, false>), dim3(grid), dim3(64), 0, s, bgr, h, w, strips, segs,
-                               seg_rows, (int)waves, vec, cls, wave_part, p);
-        else if (shd)
-            hipLaunchKernelGGL((k_stencil_stream_q<false, true>), dim3(grid), dim3(64), 0, s, bgr, h, w, strips, segs,
-                               seg_rows, (int)waves, vec, cls, wave_part, p);
-    } else {
-        const int blocks = (int)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
-        if (cls && shd)
-            hipLaunchKernelGGL((k_stencil_stream<true, true>), dim3(blocks), dim3(64 * kWavesPerBlock), 0, s, bgr, h, w,
-                               strips, segs, seg_rows, (int)waves, vec, cls, wave_part, p);
-        else if (cls)
-            hipLaunchKernelGGL((k_stencil_stream<true, false>), dim3(blocks), dim3(64 * kWavesPerBlock), 0, s, bgr, h,
-                               w, strips, segs, seg_rows, (int)waves, vec, cls, wave_part, p);
-        else if (shd)
-            hipLaunchKernelGGL((k_stencil_stream<false, true>), dim3(blocks), dim3(64 * kWavesPerBlock), 0, s, bgr, h,
-                               w, strips, segs, seg_rows, (int)waves, vec, cls, wave_part, p);
-    }
+    const int blocks = (int)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
+    if (cls && shd)
+        hipLaunchKernelGGL((k_stencil_stream<true, true>), dim3(blocks), dim3(64 * kWavesPerBlock), 0, s, bgr, h, w,
+                           strips, segs, seg_rows, (int)waves, vec, cls, wave_part, p);
+    else if (cls)
+        hipLaunchKernelGGL((k_stencil_stream<true, false>), dim3(blocks), dim3(64 * kWavesPerBlock), 0, s, bgr, h,
+                           w, strips, segs, seg_rows, (int)waves, vec, cls, wave_part, p);
+    else if (shd)
+        hipLaunchKernelGGL((k_stencil_stream<false, true>), dim3(blocks), dim3(64 * kWavesPerBlock), 0, s, bgr, h,
+                           w, strips, segs, seg_rows, (int)waves, vec, cls, wave_part, p);
     if (shd)
         hipLaunchKernelGGL(k_stream_shadow_reduce, dim3(n), dim3(256), 0, s, wave_part, strips * segs, shadow_sum,
                            shadow_cnt);

@@ -9,9 +9,8 @@
 // partition is deduplicated in a 32 KB LDS bitmap by one workgroup.
 //
 //   k_uq_noise    the launch's noise field (no caller noise): one image's worth, hashed
-//   k_uq_scatter  pixel -> key r<<16|g<<8|b, each 4096-pixel step counting-sorted by r
-//                 in LDS into its own segment of 16-bit (g, b) keys + a run table that
-//                 carries the red bits + per-image partition totals
+//   k_uq_scatter  pixel -> key r<<16|g<<8|b, each 4096-pixel step counting-sorted by R
+//                 in LDS into its own segment + run table + per-image partition totals
 //   k_uq_part     one 512-thread workgroup per (image, R): the partition's runs over the
 //                 steps -> LDS bitmap of its 4 x 256 x 256 colours -> its sorted unique keys
 //                 (at the partition's place in key order) and its 4x4x4 cubes (occupancy
@@ -203,40 +202,27 @@ __device__ __forceinline__ uint32_t part_base(const uint32_t *h, int lane, uint3
 }
 
 constexpr int SK = KB * PPT;  // keys per scatter block step
-constexpr int NBIN = 256;     // the scatter sorts a step by the full red value r = 4 R + i
 
-// run-table entry of (step, partition R): the run's segment offset (12 bits), the offsets
-// within the run where r = 4R + 1, 4R + 2, 4R + 3 begin (13 bits each) and its length
-// (13 bits) -- the key's red bits travel here, so the segment holds 16-bit (g, b) keys
-__device__ __forceinline__ unsigned long long run_entry(uint32_t off, uint32_t b1, uint32_t b2, uint32_t b3,
-                                                        uint32_t count) {
-    return (unsigned long long)off | ((unsigned long long)b1 << 12) | ((unsigned long long)b2 << 25) |
-           ((unsigned long long)b3 << 38) | ((unsigned long long)count << 51);
-}
-
-// Step segments: each 4096-pixel step's keys, counting-sorted by red value in LDS, go to
-// the step's own 4096-entry segment as 16-bit (g, b) keys (coalesced, no global cursors),
-// with the step's 64 run entries (run_entry: offset, red sub-run bounds, length) in `tab`
-// and the per-image partition totals in `hist`; k_uq_part reads a partition as its runs
-// over the steps.  (Round 6: 2 instead of 4 bytes per key each way between the two
-// kernels -- the front's traffic beyond SURVEY 8d's bytes was this round trip.)
+// Step segments: each 4096-pixel step's keys, counting-sorted by partition in LDS, go to the
+// step's own 4096-key segment (coalesced, no global cursors), with the step's 64 (offset,
+// count) run entries in `tab` and the per-image partition totals in `hist`; k_uq_part reads
+// a partition as its runs over the steps.  (No separate histogram pass over the pixels.)
 template <bool kField>
 __global__ __launch_bounds__(KB) void k_uq_scatter(const uint8_t *__restrict__ bgr, NoiseSrc ns, long long P,
                                                    long long key_stride, ImgIndex index, uint32_t *__restrict__ hist,
-                                                   unsigned long long *__restrict__ tab, uint32_t *__restrict__ seg) {
-    __shared__ uint32_t cnt[NBIN], lbase[NBIN], nlut[128], wsum[KB / 64];
-    __shared__ __attribute__((aligned(16))) uint32_t stage[SK];  // (the sorted keys use its first half as u16)
-    const int img = blockIdx.y, t = threadIdx.x, lane = t & 63, wid = t >> 6;
+                                                   uint32_t *__restrict__ tab, uint32_t *__restrict__ seg) {
+    __shared__ uint32_t cnt[NPART], lbase[NPART], nlut[128];
+    __shared__ __attribute__((aligned(16))) uint32_t stage[SK];
+    const int img = blockIdx.y, t = threadIdx.x;
     if (kField && t < 128) nlut[t] = noise_lut_entry((uint32_t)t);  // (visible after the first barrier below)
     const uint8_t *src = bgr + (size_t)img * P * 3;
     const long long off = field_offset(ns, index.at(img));
-    uint16_t *out = (uint16_t *)(seg + (size_t)img * key_stride);  // (2 key_stride u16 >= P)
-    uint16_t *const stage16 = (uint16_t *)stage;
+    uint32_t *out = seg + (size_t)img * key_stride;
     const long long nsteps = (P + SK - 1) / SK;
     for (long long st = blockIdx.x; st < nsteps; st += gridDim.x) {
         const long long p0 = st * SK + (long long)t * PPT;
         const int n = (int)max(0LL, min((long long)PPT, P - p0));
-        cnt[t] = 0;  // (KB == NBIN)
+        if (t < NPART) cnt[t] = 0;
         __syncthreads();
         uint32_t kv[PPT], pos[PPT];
         // (the staging uses this wave's 3 KB of `stage`, free until the keys are sorted into it)
@@ -249,7 +235,7 @@ __global__ __launch_bounds__(KB) void k_uq_scatter(const uint8_t *__restrict__ b
         // run's base, which a backward pass hands to the run's other keys.
         uint32_t bins[PPT], endm = 0;
 #pragma unroll
-        for (int i = 0; i < PPT; i++) bins[i] = kv[i] >> 16;
+        for (int i = 0; i < PPT; i++) bins[i] = kv[i] >> 18;
         {
             int run_start = 0;
 #pragma unroll
@@ -270,39 +256,26 @@ __global__ __launch_bounds__(KB) void k_uq_scatter(const uint8_t *__restrict__ b
             }
         }
         __syncthreads();
-        {  // exclusive prefix of the 256 bin counts (thread t = bin t)
+        if (t < 64) {
             const uint32_t c = cnt[t];
             uint32_t x = c;
 #pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t y = __shfl_up(x, o);
-                if (lane >= o) x += y;
+            for (int off = 1; off < 64; off <<= 1) {
+                uint32_t y = __shfl_up(x, off);
+                if (t >= off) x += y;
             }
-            if (lane == 63) wsum[wid] = x;
-            __syncthreads();
-            uint32_t wb = 0;
-#pragma unroll
-            for (int k = 0; k < KB / 64; k++) wb += k < wid ? wsum[k] : 0u;
-            lbase[t] = wb + x - c;
-        }
-        __syncthreads();
-        if (t < NPART) {  // partition R = t: bins 4R .. 4R + 3 are consecutive in the step
-            const uint32_t c0 = cnt[4 * t], c1 = cnt[4 * t + 1], c2 = cnt[4 * t + 2], c3 = cnt[4 * t + 3];
-            const uint32_t b1 = c0, b2 = b1 + c1, b3 = b2 + c2, c = b3 + c3;
-            tab[((size_t)img * nsteps + st) * NPART + t] = run_entry(lbase[4 * t], b1, b2, b3, c);
+            lbase[t] = x - c;
+            tab[((size_t)img * nsteps + st) * NPART + t] = (x - c) | (c << 16);
             if (c) atomicAdd(hist + (size_t)img * NPART + t, c);
         }
+        __syncthreads();
 #pragma unroll
         for (int i = 0; i < PPT; i++)
-            if (i < n) stage16[lbase[bins[i]] + pos[i]] = (uint16_t)kv[i];
+            if (i < n) stage[lbase[bins[i]] + pos[i]] = kv[i];
         __syncthreads();
         const int tot = (int)min((long long)SK, P - st * SK);
-        uint16_t *o = out + st * SK;
-        if (tot == SK) {  // 16-B stores: 8 keys per lane per instruction
-            for (int i = t; i < SK / 8; i += KB) ((uint4 *)o)[i] = ((const uint4 *)stage16)[i];
-        } else {
-            for (int i = t; i < tot; i += KB) o[i] = stage16[i];
-        }
+        uint32_t *o = out + st * SK;
+        for (int i = t; i < tot; i += KB) o[i] = stage[i];
         __syncthreads();
     }
 }
@@ -339,26 +312,11 @@ __device__ __forceinline__ unsigned long long scan_u64_wg(unsigned long long v, 
     return r;
 }
 
-// per lane: bit `lane` of the wave-uniform mask m ? a : b (one v_cndmask reading m from an
-// SGPR pair); the lanes >= d of a wave as such a mask
-__device__ __forceinline__ uint32_t lane_pick(unsigned long long m, uint32_t a, uint32_t b) {
-    uint32_t r;
-    asm("v_cndmask_b32_e64 %0, %2, %1, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
-    return r;
-}
-__device__ __forceinline__ unsigned long long lanes_from(int d) {
-    const unsigned long long m = d <= 0 ? ~0ull : (d >= 64 ? 0ull : (~0ull << d));
-    // (d is wave-uniform; readfirstlane keeps the mask in SGPRs for lane_pick's operand)
-    return ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(m >> 32)) << 32) |
-           (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)m);
-}
-
 // grid (64, n).  Reads the partition's keys as its runs in the step segments (`tab`), writes
 // the sorted unique keys to `skeys` at the partition's place in key order (capacity: its
 // hist count), and up to 4096 cube entries to `seg_cubes`.
 __global__ __launch_bounds__(UT) void k_uq_part(const uint32_t *__restrict__ seg, long long key_stride, long long P,
-                                                const uint32_t *__restrict__ hist,
-                                                const unsigned long long *__restrict__ tab,
+                                                const uint32_t *__restrict__ hist, const uint32_t *__restrict__ tab,
                                                 uint32_t *__restrict__ skeys,
                                                 CubeEnt *__restrict__ seg_cubes, CellEnt *__restrict__ seg_cells,
                                                 uint32_t *__restrict__ uq, uint32_t *__restrict__ cc,
@@ -391,11 +349,10 @@ __global__ __launch_bounds__(UT) void k_uq_part(const uint32_t *__restrict__ seg
     // (one table load per lane for up to 64 runs), then the runs' first keys (one per lane,
     // photo runs average ~64 keys) are loaded RG runs at a time, and the rest of the long runs
     // (flat "ui" partitions: ~4096 keys per run) with RG loads in flight
-    const uint16_t *sg = (const uint16_t *)(seg + (size_t)img * key_stride);
+    const uint32_t *sg = seg + (size_t)img * key_stride;
     const long long nsteps = (P + SK - 1) / SK;
-    const unsigned long long *tb = tab + (size_t)img * nsteps * NPART + R;
-    // (wid through readfirstlane: the run addresses below stay scalar)
-    const int lane = t & 63, wid = __builtin_amdgcn_readfirstlane(t >> 6);
+    const uint32_t *tb = tab + (size_t)img * nsteps * NPART + R;
+    const int lane = t & 63, wid = t >> 6;
     constexpr int RG = 8;  // runs (and tail loads) in flight per lane (16: 97 VGPRs, one workgroup per CU)
     auto mark = [&](uint32_t k) {
         // flat regions put one colour in every lane: test the bit with a (broadcast) read
@@ -403,45 +360,32 @@ __global__ __launch_bounds__(UT) void k_uq_part(const uint32_t *__restrict__ seg
         const uint32_t wi = ((k >> 16) & 3u) * 2048 + ((k >> 5) & 2047u), bit = 1u << (k & 31u);
         if (k != 0xFFFFFFFFu && !(W[wi] & bit)) atomicOr(&W[wi], bit);
     };
-    const uint32_t one = 0x10000u, two = 0x20000u, three = 0x30000u;
-    // the red bits (r & 3) << 16 of keys s0 .. s0 + 63 of a run, lane = key - s0: its
-    // sub-run bounds (run_entry, uniform) as lane masks built in scalar code, three
-    // v_cndmask per key (compares into an SGPR pair would each need wait states)
-    auto red_bits = [&](uint32_t lo, uint32_t hi, int s0) {
-        const int b1 = (int)((lo >> 12) & 0x1FFFu), b2 = (int)(((lo >> 25) | (hi << 7)) & 0x1FFFu),
-                  b3 = (int)((hi >> 6) & 0x1FFFu);
-        uint32_t r = lane_pick(lanes_from(b1 - s0), one, 0u);
-        r = lane_pick(lanes_from(b2 - s0), two, r);
-        return lane_pick(lanes_from(b3 - s0), three, r);
-    };
     for (long long base = 0; base < nsteps; base += (UT / 64) * 64) {
         const long long sl = base + wid + (UT / 64) * lane;  // this lane's run
-        const unsigned long long e = sl < nsteps ? tb[(size_t)sl * NPART] : 0ull;
-        const uint32_t elo = (uint32_t)e, ehi = (uint32_t)(e >> 32);
-        const unsigned long long live = __ballot((ehi >> 19) != 0u);
+        const uint32_t e = sl < nsteps ? tb[(size_t)sl * NPART] : 0u;
+        const unsigned long long live = __ballot(e != 0u);
         for (int j0 = 0; j0 < 64; j0 += RG) {
             if (!((live >> j0) & ((1ull << RG) - 1))) continue;  // (uniform)
             uint32_t kk[RG];
 #pragma unroll
             for (int j = 0; j < RG; j++) {
-                const uint32_t lo = __builtin_amdgcn_readlane(elo, j0 + j), hi = __builtin_amdgcn_readlane(ehi, j0 + j);
-                const uint16_t *rp = sg + (size_t)(base + wid + (UT / 64) * (j0 + j)) * SK + (lo & 0xFFFu);
-                kk[j] = (uint32_t)lane < (hi >> 19) ? ((uint32_t)rp[lane] | red_bits(lo, hi, 0)) : 0xFFFFFFFFu;
+                const uint32_t ej = __builtin_amdgcn_readlane(e, j0 + j);
+                const size_t st = (size_t)(base + wid + (UT / 64) * (j0 + j));
+                kk[j] = (uint32_t)lane < (ej >> 16) ? sg[st * SK + (ej & 0xFFFFu) + lane] : 0xFFFFFFFFu;
             }
 #pragma unroll
             for (int j = 0; j < RG; j++) mark(kk[j]);
 #pragma unroll
             for (int j = 0; j < RG; j++) {
-                const uint32_t lo = __builtin_amdgcn_readlane(elo, j0 + j), hi = __builtin_amdgcn_readlane(ehi, j0 + j);
-                const uint32_t c = hi >> 19;
+                const uint32_t ej = __builtin_amdgcn_readlane(e, j0 + j), c = ej >> 16;
                 if (c <= 64) continue;  // (uniform)
-                const uint16_t *rp = sg + (size_t)(base + wid + (UT / 64) * (j0 + j)) * SK + (lo & 0xFFFu);
+                const uint32_t *rp = sg + (size_t)(base + wid + (UT / 64) * (j0 + j)) * SK + (ej & 0xFFFFu);
                 for (uint32_t i0 = 64; i0 < c; i0 += 64 * RG) {
                     uint32_t q[RG];
 #pragma unroll
                     for (int i = 0; i < RG; i++) {
                         const uint32_t ix = i0 + 64 * i + lane;
-                        q[i] = ix < c ? ((uint32_t)rp[ix] | red_bits(lo, hi, (int)(i0 + 64 * i))) : 0xFFFFFFFFu;
+                        q[i] = ix < c ? rp[ix] : 0xFFFFFFFFu;
                     }
 #pragma unroll
                     for (int i = 0; i < RG; i++) mark(q[i]);
@@ -644,7 +588,6 @@ hipError_t launch_uq_noise(const int8_t *noise, int8_t *field, int64_t P, uint64
 }
 
 int64_t uq_steps(int64_t P) { return (P + SK - 1) / SK; }
-int64_t uq_tab_words(int64_t P) { return uq_steps(P) * NPART * 2; }  // u64 run entries
 
 hipError_t launch_uq_scatter(const uint8_t *bgr, const int8_t *noise, const int8_t *field, int n, int h, int w,
                              uint64_t seed, ImgIndex index, int64_t key_stride, uint32_t *hist, uint32_t *tab,
@@ -655,18 +598,18 @@ hipError_t launch_uq_scatter(const uint8_t *bgr, const int8_t *noise, const int8
     const NoiseSrc ns = noise_src(noise, (int8_t *)field, P, seed);
     if (ns.L)
         hipLaunchKernelGGL(k_uq_scatter<true>, dim3(bx, n), dim3(KB), 0, s, bgr, ns, (long long)P, (long long)key_stride,
-                           index, hist, (unsigned long long *)tab, seg);
+                           index, hist, tab, seg);
     else
         hipLaunchKernelGGL(k_uq_scatter<false>, dim3(bx, n), dim3(KB), 0, s, bgr, ns, (long long)P,
-                           (long long)key_stride, index, hist, (unsigned long long *)tab, seg);
+                           (long long)key_stride, index, hist, tab, seg);
     return hipGetLastError();
 }
 
 hipError_t launch_uq_part(const uint32_t *seg, int n, int64_t key_stride, int64_t P, const uint32_t *hist,
                           const uint32_t *tab, uint32_t *skeys, CubeEnt *seg_cubes, CellEnt *seg_cells, uint32_t *uq,
                           uint32_t *cc, uint32_t *cl, hipStream_t s) {
-    hipLaunchKernelGGL(k_uq_part, dim3(NPART, n), dim3(UT), 0, s, seg, (long long)key_stride, (long long)P, hist,
-                       (const unsigned long long *)tab, skeys, seg_cubes, seg_cells, uq, cc, cl);
+    hipLaunchKernelGGL(k_uq_part, dim3(NPART, n), dim3(UT), 0, s, seg, (long long)key_stride, (long long)P, hist, tab,
+                       skeys, seg_cubes, seg_cells, uq, cc, cl);
     return hipGetLastError();
 }
 
@@ -682,4 +625,7 @@ hipError_t launch_uq_gather(const uint32_t *skeys, int n, int64_t key_stride, co
     return hipGetLastError();
 }
 
+}  // namespace llfe
+namespace llfe {
+int64_t uq_tab_words(int64_t P) { return uq_steps(P) * 64; }  // u32 run entries (offset | count << 16)
 }  // namespace llfe
