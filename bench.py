@@ -233,7 +233,14 @@ def served_batcher(imgs_dev, feats, batches, seed, inflight, device):
     finally:
         bt.close()
     sizes = bt.batch_sizes[n0:]
-    return {"value": round(batches * B / dt, 2), "unit": "images/s", "requests": batches * B,
+    log = [e for e in bt.launch_log[n0:] if e[2] is not None]
+    # the worker's clock per launch: blocked in collect (the GPU still on it), and from one
+    # collect's return to the next submit (gather + descriptors + llfe_submit_images)
+    wait = [e[2] - e[1] for e in log]
+    gap = [log[k + 1][0] - log[k][2] for k in range(len(log) - 1) if log[k + 1][0] > log[k][2]]
+    worker = {"collect_wait_ms": round(1e3 * sum(wait) / max(len(wait), 1), 3),
+              "collect_to_next_submit_ms": round(1e3 * sum(gap) / max(len(gap), 1), 3)}
+    return {"value": round(batches * B / dt, 2), "unit": "images/s", "requests": batches * B, "worker": worker,
             "producers": producers, "max_batch": B, "inflight": inflight,
             "launches": len(sizes), "mean_launch": round(sum(sizes) / max(len(sizes), 1), 1),
             "max_in_flight": bt.max_in_flight,
@@ -444,6 +451,7 @@ def main():
                     help="steps of an all-ui and an all-photo batch (SURVEY.md 8d per-class throughput; 4 steps "
                          "left the pipeline's fill and drain in a third of the timed region: ui 21-30k across "
                          "round-5 runs); 0 disables")
+    ap.add_argument("--batcher-inflight", type=int, default=0, help="launches the batcher keeps in flight (0: as value)")
     ap.add_argument("--batcher-steps", type=int, default=10,
                     help="0 disables the served_batcher line (single-image requests through MicroBatcher)")
     ap.add_argument("--contours", choices=["auto", "host", "gpu"], default="auto",
@@ -698,7 +706,7 @@ def main():
     served = None
     if args.batcher_steps > 0 and pipelined:
         barrier()
-        served = served_batcher(imgs, feats, args.batcher_steps, args.seed, be.inflight, local)
+        served = served_batcher(imgs, feats, args.batcher_steps, args.seed, args.batcher_inflight or be.inflight, local)
         barrier()
 
     # (the e2e lines run on every rank before rank 0 reports: each rank pays its own

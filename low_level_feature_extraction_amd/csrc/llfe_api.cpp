@@ -654,8 +654,8 @@ void grow_contour_caps(Work &W, int n, int h, int w, const CtCounters &ct) {
 // (llfe_color_unique's output, the general-K k-means); otherwise they stay where k_uq_part
 // wrote them (W.d_raw, partition R at the prefix of the partition pixel counts) and the cube
 // k-means reads them there (KmeansCubes::part_hist)
-int color_stage(llfe_ctx *ctx, Work &W, const uint8_t *img, const int8_t *noise, int n, int h, int w, uint64_t seed,
-                ImgIndex index, bool contiguous_keys, hipStream_t s) {
+int color_stage(llfe_ctx *ctx, Work &W, const uint8_t *img, const uint64_t *img_tab, const int8_t *noise, int n, int h,
+                int w, uint64_t seed, ImgIndex index, bool contiguous_keys, hipStream_t s) {
     // unique colours -> W.d_keys (sorted, key_stride) + cube table for k-means
     const int64_t P = (int64_t)h * w;
     const int64_t key_stride = (std::max<int64_t>(P, 1) + 3) & ~int64_t(3);
@@ -687,7 +687,7 @@ int color_stage(llfe_ctx *ctx, Work &W, const uint8_t *img, const int8_t *noise,
     // scatter and k_uq_part (4P each way) are the implementation's, not counted.
     // keys -> per-step segments sorted by partition + run table + partition totals
     TIMED(ctx, s, "k_uq_scatter", (double)n * P * (noise ? 6 : 3),
-          launch_uq_scatter(img, noise, W.d_nfield.p, n, h, w, seed, index, key_stride, hist, W.d_segtab.p,
+          launch_uq_scatter(img, img_tab, noise, W.d_nfield.p, n, h, w, seed, index, key_stride, hist, W.d_segtab.p,
                             W.d_keys.p, s));
     // the partitions' sorted unique keys go to the (free) d_raw
     TIMED(ctx, s, "k_uq_part", (double)n * 4194304.0,
@@ -814,8 +814,10 @@ int chunk_index(llfe_ctx *ctx, Work &W, const llfe_batch *b, int i0, int n, hipS
 // Device half of one chunk, on slot `slot`'s stream and workspace: every kernel, then
 // the D2H of the per-image results into host slot `slot`, with events the host half
 // waits on.
+// img_tab (device, llfe_submit_images): image i of the chunk at img_tab[i], read in place by
+// the scatter and the stencil (b->data then only names the first image)
 int enqueue_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_t seed, int i0, int n, int slot,
-                  int q) {
+                  int q, const uint64_t *img_tab = nullptr) {
     ctx->prof.cur_slot = slot;
     Work &W = ctx->ws[q];
     hipStream_t s = ctx->streams[q];
@@ -846,7 +848,7 @@ int enqueue_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_
     // colour front (unique colours), then shapes / shadows (on the other stream), then
     // k-means
     if (want_col) {
-        rc = color_stage(ctx, W, img, noise, n, h, w, seed, index, /*contiguous_keys=*/n_colors > kMaxK, col_s);
+        rc = color_stage(ctx, W, img, img_tab, noise, n, h, w, seed, index, /*contiguous_keys=*/n_colors > kMaxK, col_s);
         if (rc) return rc;
     }
     // d_shadow / d_bits of this workspace may still be in the previous chunk's D2H
@@ -854,6 +856,7 @@ int enqueue_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_
     if (want_shp || want_shd) {
         HIPCHK(ctx, W.d_shadow.ensure(2 * (size_t)n + shadow_tiles(n, h, w)));
         StencilParams sp = ctx->sp;
+        sp.img_tab = img_tab;
         if (want_shp) {
             HIPCHK(ctx, W.d_cls.ensure((size_t)n * P));
             rc = stencil_params(ctx, W, n, h, w, s, &sp);
@@ -1500,11 +1503,19 @@ int llfe_submit_images(llfe_ctx *ctx, const llfe_image_desc *images, int32_t n, 
     HIPCHK(ctx, hipStreamWaitEvent(q, ctx->start_ev, 0));
     Work &W = ctx->ws[slot];
     const size_t P3 = (size_t)h * w * 3;
-    HIPCHK(ctx, W.d_in.ensure(P3 * n));
     ctx->prof.cur_slot = slot;
+    // in place when every image is a packed, 16-B aligned device image: the scatter and the
+    // stencil (the only readers of the input) take image i's address from a table; else (host
+    // sources, strided rows, the GPU contour mode, whose capacity redo re-reads a packed
+    // batch) the images are gathered into the slot's input buffer first
+    bool in_place = nd == n && !ctx->gpu_contours;
+    for (int i = 0; in_place && i < n; i++)
+        in_place = (images[i].row_stride == 0 || images[i].row_stride == 3 * (int64_t)w) &&
+                   (((uintptr_t)images[i].data) & 15) == 0;
+    const uint64_t *d_tab = nullptr;
     if (nd == n) {
-        // every source on the device: one gather launch over a table of addresses and
-        // pitches (pinned, per slot: the slot is not reused before this ticket's collect)
+        // a table of addresses and pitches (pinned, per slot: the slot is not reused before
+        // this ticket's collect), then one gather launch unless the kernels read in place
         HIPCHK(ctx, ctx->h_gather_s[slot].ensure(2 * (size_t)n));
         HIPCHK(ctx, ctx->d_gather_s[slot].ensure(2 * (size_t)n));
         uint64_t *tab = ctx->h_gather_s[slot].p;
@@ -1513,9 +1524,15 @@ int llfe_submit_images(llfe_ctx *ctx, const llfe_image_desc *images, int32_t n, 
             tab[n + i] = (uint64_t)(images[i].row_stride ? images[i].row_stride : 3 * (int64_t)w);
         }
         HIPCHK(ctx, hipMemcpyAsync(ctx->d_gather_s[slot].p, tab, sizeof(uint64_t) * 2 * n, hipMemcpyHostToDevice, q));
-        TIMED(ctx, q, "k_gather_images", 2.0 * (double)P3 * n,
-              launch_gather_images(ctx->d_gather_s[slot].p, n, h, w, W.d_in.p, q));
+        if (in_place) {
+            d_tab = ctx->d_gather_s[slot].p;
+        } else {
+            HIPCHK(ctx, W.d_in.ensure(P3 * n));
+            TIMED(ctx, q, "k_gather_images", 2.0 * (double)P3 * n,
+                  launch_gather_images(ctx->d_gather_s[slot].p, n, h, w, W.d_in.p, q));
+        }
     } else {
+        HIPCHK(ctx, W.d_in.ensure(P3 * n));
         for (int i = 0; i < n; i++) {
             const llfe_image_desc &d = images[i];
             const size_t pitch = d.row_stride ? (size_t)d.row_stride : (size_t)w * 3;
@@ -1525,14 +1542,14 @@ int llfe_submit_images(llfe_ctx *ctx, const llfe_image_desc *images, int32_t n, 
     }
     pd.idx.assign(indices, indices + n);
     llfe_batch b{};
-    b.data = W.d_in.p;
+    b.data = d_tab ? images[0].data : W.d_in.p;
     b.n = n;
     b.height = h;
     b.width = w;
     b.on_device = 1;
     b.n_colors = n_colors;
     b.indices = pd.idx.data();
-    int rc = enqueue_chunk(ctx, &b, features, seed, 0, n, slot, slot);
+    int rc = enqueue_chunk(ctx, &b, features, seed, 0, n, slot, slot, d_tab);
     if (rc) return rc;
     pd.busy = true;
     pd.done = false;
@@ -1748,7 +1765,7 @@ int llfe_color_unique(llfe_ctx *ctx, const llfe_batch *b, uint64_t seed, uint32_
     ImgIndex index;
     rc = chunk_index(ctx, W, b, 0, n, s, &index);
     if (rc) return rc;
-    rc = color_stage(ctx, W, img, noise, n, h, w, seed, index, /*contiguous_keys=*/true, s);
+    rc = color_stage(ctx, W, img, nullptr, noise, n, h, w, seed, index, /*contiguous_keys=*/true, s);
     if (rc) return rc;
     HIPCHK(ctx, hipMemcpy2DAsync(keys, sizeof(uint32_t) * P, W.d_keys.p, sizeof(uint32_t) * key_stride,
                                  sizeof(uint32_t) * P, n, hipMemcpyDeviceToDevice, s));

@@ -26,6 +26,9 @@ struct StencilParams {
     // (row-streaming kernel, with cls) n x ceil(h / 64) x ceil(w / 64) bytes, zeroed by the
     // caller: set to 1 for every 64 x 64 hysteresis tile holding a class != 1 pixel
     uint8_t *tflag;
+    // (row-streaming kernel) image i at img_tab[i] instead of bgr + i * h * w * 3 -- the
+    // separately allocated device images of llfe_submit_images, no gather; null: packed
+    const uint64_t *img_tab;
 };
 
 // shape pyc @L18-24 + shadow pyc @L8-21 for a packed NHWC batch.
@@ -238,7 +241,9 @@ hipError_t launch_uq_noise(const int8_t *noise, int8_t *field, int64_t P, uint64
 // steps of 4096 pixels per image (k_uq_scatter's segments; its run table is n x steps x 64 u32)
 int64_t uq_steps(int64_t P);
 int64_t uq_tab_words(int64_t P);  // k_uq_scatter's run table, u32 words per image
-hipError_t launch_uq_scatter(const uint8_t *bgr, const int8_t *noise, const int8_t *field, int n, int h, int w,
+// img_tab (may be null): image i at img_tab[i] instead of bgr + i * h * w * 3
+hipError_t launch_uq_scatter(const uint8_t *bgr, const uint64_t *img_tab, const int8_t *noise, const int8_t *field,
+                             int n, int h, int w,
                              uint64_t seed, ImgIndex index, int64_t key_stride, uint32_t *hist, uint32_t *tab,
                              uint32_t *seg, hipStream_t s);
 hipError_t launch_uq_part(const uint32_t *seg, int n, int64_t key_stride, int64_t P, const uint32_t *hist,

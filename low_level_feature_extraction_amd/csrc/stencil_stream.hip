@@ -310,7 +310,7 @@ __device__ __forceinline__ void stencil_wave(int wid, const uint8_t *__restrict_
     const int rest = wid / strips;
     const int seg = rest % segs;
     const int img_i = rest / segs;
-    const uint8_t *img = bgr + (size_t)img_i * H * W * 3;
+    const uint8_t *img = prm.img_tab ? (const uint8_t *)prm.img_tab[img_i] : bgr + (size_t)img_i * H * W * 3;
     uint8_t *cimg = CLS ? cls + (size_t)img_i * H * W : nullptr;
     // the image's class map as a buffer (H * W < 2^31 bytes: valid_dims)
     const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(cimg, (short)0, CLS ? H * W : 0, 0x00020000);

@@ -208,14 +208,15 @@ constexpr int SK = KB * PPT;  // keys per scatter block step
 // count) run entries in `tab` and the per-image partition totals in `hist`; k_uq_part reads
 // a partition as its runs over the steps.  (No separate histogram pass over the pixels.)
 template <bool kField>
-__global__ __launch_bounds__(KB) void k_uq_scatter(const uint8_t *__restrict__ bgr, NoiseSrc ns, long long P,
+__global__ __launch_bounds__(KB) void k_uq_scatter(const uint8_t *__restrict__ bgr, const uint64_t *__restrict__ img_tab,
+                                                   NoiseSrc ns, long long P,
                                                    long long key_stride, ImgIndex index, uint32_t *__restrict__ hist,
                                                    uint32_t *__restrict__ tab, uint32_t *__restrict__ seg) {
     __shared__ uint32_t cnt[NPART], lbase[NPART], nlut[128];
     __shared__ __attribute__((aligned(16))) uint32_t stage[SK];
     const int img = blockIdx.y, t = threadIdx.x;
     if (kField && t < 128) nlut[t] = noise_lut_entry((uint32_t)t);  // (visible after the first barrier below)
-    const uint8_t *src = bgr + (size_t)img * P * 3;
+    const uint8_t *src = img_tab ? (const uint8_t *)img_tab[img] : bgr + (size_t)img * P * 3;
     const long long off = field_offset(ns, index.at(img));
     uint32_t *out = seg + (size_t)img * key_stride;
     const long long nsteps = (P + SK - 1) / SK;
@@ -589,7 +590,8 @@ hipError_t launch_uq_noise(const int8_t *noise, int8_t *field, int64_t P, uint64
 
 int64_t uq_steps(int64_t P) { return (P + SK - 1) / SK; }
 
-hipError_t launch_uq_scatter(const uint8_t *bgr, const int8_t *noise, const int8_t *field, int n, int h, int w,
+hipError_t launch_uq_scatter(const uint8_t *bgr, const uint64_t *img_tab, const int8_t *noise, const int8_t *field,
+                             int n, int h, int w,
                              uint64_t seed, ImgIndex index, int64_t key_stride, uint32_t *hist, uint32_t *tab,
                              uint32_t *seg, hipStream_t s) {
     const int64_t P = (int64_t)h * w;
@@ -597,10 +599,10 @@ hipError_t launch_uq_scatter(const uint8_t *bgr, const int8_t *noise, const int8
     if (bx < 1) bx = 1;
     const NoiseSrc ns = noise_src(noise, (int8_t *)field, P, seed);
     if (ns.L)
-        hipLaunchKernelGGL(k_uq_scatter<true>, dim3(bx, n), dim3(KB), 0, s, bgr, ns, (long long)P, (long long)key_stride,
+        hipLaunchKernelGGL(k_uq_scatter<true>, dim3(bx, n), dim3(KB), 0, s, bgr, img_tab, ns, (long long)P, (long long)key_stride,
                            index, hist, tab, seg);
     else
-        hipLaunchKernelGGL(k_uq_scatter<false>, dim3(bx, n), dim3(KB), 0, s, bgr, ns, (long long)P,
+        hipLaunchKernelGGL(k_uq_scatter<false>, dim3(bx, n), dim3(KB), 0, s, bgr, img_tab, ns, (long long)P,
                            (long long)key_stride, index, hist, tab, seg);
     return hipGetLastError();
 }

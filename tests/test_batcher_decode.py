@@ -265,6 +265,12 @@ def test_batcher_pipelined_on_gpu_device_images_equal_run_batch():
     feats = ("colors", "shapes", "shadows")
     imgs = [synth.synth_numpy(i, 270, 480, seed=11) for i in range(24)]
     dev = [torch.from_numpy(im).to("cuda:0") for im in imgs]  # separately allocated
+    # images 16..23 start 3 bytes into their allocation: not 16-B aligned, so their launch
+    # gathers them (k_gather_images) instead of reading them in place through the table
+    for i in range(16, 24):
+        flat = torch.empty(imgs[i].size + 3, dtype=torch.uint8, device="cuda:0")
+        dev[i] = flat[3:].view(270, 480, 3)
+        dev[i].copy_(torch.from_numpy(imgs[i]))
     ref = run_batch(imgs, feats, seed=77, index_base=4000)
     with MicroBatcher(features=feats, max_batch=8, max_wait_ms=50, inflight=2, seed=77) as b:
         futs = [b.submit(t, index=4000 + i) for i, t in enumerate(dev)]
