@@ -856,12 +856,14 @@ int enqueue_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_
     if (want_shp || want_shd) {
         HIPCHK(ctx, W.d_shadow.ensure(2 * (size_t)n + shadow_tiles(n, h, w)));
         StencilParams sp = ctx->sp;
-        sp.img_tab = img_tab;
         if (want_shp) {
             HIPCHK(ctx, W.d_cls.ensure((size_t)n * P));
-            rc = stencil_params(ctx, W, n, h, w, s, &sp);
+            rc = stencil_params(ctx, W, n, h, w, s, &sp);  // (starts from ctx->sp)
             if (rc) return rc;
         }
+        // after stencil_params: the stencil reads an in-place batch through its table (with
+        // the packed-batch addressing, image i >= 1 would lie past image 0's allocation)
+        sp.img_tab = img_tab;
         TIMED(ctx, s, "k_stencil", (double)n * P * (3 + (want_shp ? 1 : 0)),
               launch_stencil(img, n, h, w, want_shp ? W.d_cls.p : nullptr, nullptr,
                              want_shd ? W.d_shadow.p : nullptr, want_shd ? W.d_shadow.p + n : nullptr,
