@@ -451,7 +451,10 @@ def main():
                     help="steps of an all-ui and an all-photo batch (SURVEY.md 8d per-class throughput; 4 steps "
                          "left the pipeline's fill and drain in a third of the timed region: ui 21-30k across "
                          "round-5 runs); 0 disables")
-    ap.add_argument("--batcher-inflight", type=int, default=0, help="launches the batcher keeps in flight (0: as value)")
+    ap.add_argument("--batcher-inflight", type=int, default=3,
+                    help="launches the batcher keeps in flight (MicroBatcher's default, 3: the request path's "
+                         "host work -- request futures, descriptors, result dicts -- shares the GIL with the "
+                         "serving thread, so it keeps one more launch queued than `value`'s loop)")
     ap.add_argument("--batcher-steps", type=int, default=10,
                     help="0 disables the served_batcher line (single-image requests through MicroBatcher)")
     ap.add_argument("--contours", choices=["auto", "host", "gpu"], default="auto",
@@ -706,7 +709,7 @@ def main():
     served = None
     if args.batcher_steps > 0 and pipelined:
         barrier()
-        served = served_batcher(imgs, feats, args.batcher_steps, args.seed, args.batcher_inflight or be.inflight, local)
+        served = served_batcher(imgs, feats, args.batcher_steps, args.seed, args.batcher_inflight, local)
         barrier()
 
     # (the e2e lines run on every rank before rank 0 reports: each rank pays its own

@@ -7,7 +7,9 @@ single worker thread (with its own device context) drains up to ``max_batch`` im
 whatever arrived within ``max_wait_ms`` of the first one, into one launch.
 
 The worker runs the serving loop the headline measures (bench.py): it keeps ``inflight``
-launches in flight through ``Backend.submit_images`` / ``Backend.collect``
+(default 3: its Python side shares the GIL with the event loop and the resolver, so one
+more launch stays queued than in the bench's loop) launches in flight through
+``Backend.submit_images`` / ``Backend.collect``
 (llfe_submit_images gathers the requests' separately allocated images on the device, so
 batch k + 1's kernels start in the tail of batch k's k-means), and a resolver thread
 turns each collected batch into the reference-shaped results (``pipeline.assemble_batch``)
@@ -109,7 +111,7 @@ def _resolve(futs, results):
 
 class MicroBatcher:
     def __init__(self, features: Sequence[str] = ("colors", "shapes", "shadows"), max_batch: int = 64,
-                 max_wait_ms: float = 2.0, run: Optional[Callable] = None, inflight: int = 2,
+                 max_wait_ms: float = 2.0, run: Optional[Callable] = None, inflight: int = 3,
                  seed: Optional[int] = None, n_colors: int = 5, freeze_gc: bool = True, backend=None,
                  device: Optional[int] = None, fill_wait_ms: float = 8.0):
         if max_batch < 1:
