@@ -10,8 +10,9 @@ The worker runs the serving loop the headline measures (bench.py): it keeps ``in
 (default 3: its Python side shares the GIL with the event loop and the resolver, so one
 more launch stays queued than in the bench's loop) launches in flight through
 ``Backend.submit_images`` / ``Backend.collect``
-(llfe_submit_images gathers the requests' separately allocated images on the device, so
-batch k + 1's kernels start in the tail of batch k's k-means), and a resolver thread
+(llfe_submit_images reads the requests' separately allocated device images in place through
+an address table, or gathers other layouts on the device; batch k + 1's kernels start in
+the tail of batch k's k-means), and a resolver thread
 turns each collected batch into the reference-shaped results (``pipeline.assemble_batch``)
 and resolves the requests' futures while the worker submits the next batch.  After its
 first batch the worker calls ``gc.collect(); gc.freeze()`` (``freeze_gc``): the serving
