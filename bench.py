@@ -455,8 +455,10 @@ def main():
                     help="launches the batcher keeps in flight (MicroBatcher's default, 3: the request path's "
                          "host work -- request futures, descriptors, result dicts -- shares the GIL with the "
                          "serving thread, so it keeps one more launch queued than `value`'s loop)")
-    ap.add_argument("--batcher-steps", type=int, default=10,
-                    help="0 disables the served_batcher line (single-image requests through MicroBatcher)")
+    ap.add_argument("--batcher-steps", type=int, default=None,
+                    help="launches of B requests the served_batcher line times (default: --steps, so its "
+                         "pipeline fill and drain are amortised like `value`'s); 0 disables the line "
+                         "(single-image requests through MicroBatcher)")
     ap.add_argument("--contours", choices=["auto", "host", "gpu"], default="auto",
                     help="where findContours + the shape loop run: the host pool from the copied-back mask "
                          "(overlaps k-means), the GPU (contours_gpu.hip), or auto (the library's choice: "
@@ -707,6 +709,8 @@ def main():
     # the product request path at the same load: single-image requests through the
     # MicroBatcher, beside `value`
     served = None
+    if args.batcher_steps is None:
+        args.batcher_steps = args.steps
     if args.batcher_steps > 0 and pipelined:
         barrier()
         served = served_batcher(imgs, feats, args.batcher_steps, args.seed, args.batcher_inflight, local)

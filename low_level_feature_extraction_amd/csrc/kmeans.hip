@@ -37,6 +37,9 @@ constexpr int kCellMinCubes = 8192;
 #ifndef LLFE_KM_PP_CALL
 #define LLFE_KM_PP_CALL (!LLFE_KM_SPLIT)  // pp_cubes as a call in the one-launch kernel (its register budget)
 #endif  // the sweeps test cells before cubes from this cube count on
+#ifndef LLFE_KM_SUPS
+#define LLFE_KM_SUPS 1  // Lloyd tests 4 x 16 x 16 super-cells before cells
+#endif
 #ifndef LLFE_KM_THREADS
 #define LLFE_KM_THREADS 512
 #endif
@@ -164,7 +167,10 @@ __device__ __forceinline__ T wave_sum(T v) {
 struct KmSmem {
     unsigned long long accA[kMaxK][KT];  // x | y << 32 per lane and cluster
     unsigned long long accB[kMaxK][KT];  // z | 1 << 32
-    unsigned long long red[32][20];      // [part][cluster x component] (lanes read along v)
+    union {
+        unsigned long long red[32][20];  // [part][cluster x component] (lanes read along v)
+        int cs[KW][256];                 // (Lloyd sweep) per-wave list of the cells of a chunk's failing super-cells
+    };
     unsigned long long wtot[KW][3];
     unsigned long long scan_w[KW];
     double dred[KW];
@@ -199,12 +205,15 @@ struct KmSmem {
     unsigned long long sel_pts;          // colours the selection scans read
     unsigned long long wchunk[3][KW];    // per trial: sum of D over each wave's chunk
     uint32_t stage[KW][kStage + 64];     // per-wave ring of boundary colours (+ a dummy row)
-    float thrL[2][kMaxK * kMaxK];        // Lloyd margin thresholds [cube / cell][owner k][j]
+    float thrL[3][kMaxK * kMaxK];        // Lloyd margin thresholds [cube / cell / super-cell][owner k][j]
     int cq[KW][256];                     // per-wave list of the cubes of a chunk's failing cells
     unsigned long long qtot;             // sum of |p|^2 over all colours (exact)
     int marg[kMaxK * kMaxK + 6 * kMaxK]; // k-means++ corner margins: centre pairs, trial vs centre (+/-)
     int margc[kMaxK * kMaxK + 6 * kMaxK];  // the same for the 4 x 8 x 8 cells
 };
+
+// two workgroups per CU (160 KB of LDS)
+static_assert(sizeof(KmSmem) <= 80 * 1024, "KmSmem must leave room for two workgroups per CU");
 
 __device__ __forceinline__ Cent load_centres(const float (*c)[3]) {
     Cent r;
@@ -1500,14 +1509,16 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
             // passes when d_j(q) - d_k(q) > T[k][j] for every j (T[k][k] = -inf), five
             // compares against the owner's row instead of the ten centre pairs' compares
             // combined by the owner masks.  Cube: 3 L1(c_j - c_k) + 1; 4 x 8 x 8 cell:
-            // 3 |dx| + 7 (|dy| + |dz|) + 1 (the half extents).
-            if (tid < 2 * kMaxK * kMaxK) {
+            // 3 |dx| + 7 (|dy| + |dz|) + 1; 4 x 16 x 16 super-cell: 3 |dx| + 15 (|dy| + |dz|) + 1
+            // (twice the half extents).
+            if (tid < 3 * kMaxK * kMaxK) {
                 const int kind = tid / (kMaxK * kMaxK), k = (tid / kMaxK) % kMaxK, j = tid % kMaxK;
                 const float dx = fabsf(sm.c[j][0] - sm.c[k][0]), dy = fabsf(sm.c[j][1] - sm.c[k][1]),
                             dz = fabsf(sm.c[j][2] - sm.c[k][2]);
                 sm.thrL[kind][k * kMaxK + j] = (j == k || j >= K || k >= K) ? -__builtin_inff()
                                                : kind == 0 ? 3.f * (dx + dy + dz) + 1.f
-                                                           : 3.f * dx + 7.f * (dy + dz) + 1.f;
+                                               : kind == 1 ? 3.f * dx + 7.f * (dy + dz) + 1.f
+                                                           : 3.f * dx + 15.f * (dy + dz) + 1.f;
             }
             __syncthreads();
             unsigned long long fails = 0;
@@ -1628,36 +1639,37 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
                 const int L = cubes.n_cells[img];
                 const CellEnt *ltab = cubes.cells + (size_t)img * cubes.cell_stride;
                 int *ql = sm.cq[wid];
-                int base = __builtin_amdgcn_readfirstlane(grab());
-                int ahead = grab();
-                CellEnt ln{0u, 0u, 0u, 0u};
-                if (base + lane < L) ln = ltab[base + lane];
-                while (base < L) {
-                    const bool lvalid = base + lane < L;
-                    const CellEnt e = ln;
-                    const int nb = __builtin_amdgcn_readfirstlane(ahead);
-                    if (nb + lane < L) ln = ltab[nb + lane];
-                    if (nb < L) ahead = grab();
+                auto mrank = [&](unsigned long long m) {
+                    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                };
+                // the margin test of a box with origin-derived centre (qx, qy, qz) against the
+                // thresholds of `kind`: the owner k (first minimum at q) and pass
+                auto box_test = [&](float qx, float qy, float qz, int kind, int &k) __attribute__((always_inline)) {
+                    const f2 px = f2{qx, qx}, py = f2{qy, qy}, pz = f2{qz, qz};
+                    f2 d[3];
+#pragma unroll
+                    for (int j = 0; j < 3; j++) {
+                        f2 dd = __builtin_elementwise_fma(px, lw_x[j], lc2[j]);
+                        dd = __builtin_elementwise_fma(py, lw_y[j], dd);
+                        d[j] = __builtin_elementwise_fma(pz, lw_z[j], dd);
+                    }
+                    const float dv[5] = {d[0].x, d[0].y, d[1].x, d[1].y, d[2].x};
+                    const float m1 = fminf(fminf(fminf(dv[0], dv[1]), fminf(dv[2], dv[3])), dv[4]);
+                    k = dv[0] == m1 ? 0 : (dv[1] == m1 ? 1 : (dv[2] == m1 ? 2 : (dv[3] == m1 ? 3 : 4)));
+                    const float *tk = &sm.thrL[kind][k * kMaxK];
+                    return (dv[0] - m1 > tk[0]) & (dv[1] - m1 > tk[1]) & (dv[2] - m1 > tk[2]) &
+                           (dv[3] - m1 > tk[3]) & (dv[4] - m1 > tk[4]);
+                };
+                // one 64-lane batch of cells: passing cells add their sums, the failing cells'
+                // cubes go to list slots [pre_c, pre_c + nc), pre_c = sum of nc over the failing
+                // lanes below (three ballots: the count and its two low bits), 64 at a time
+                // through the cube test
+                auto cell_body = [&](const CellEnt &e, const bool lvalid) __attribute__((always_inline)) {
                     bool pass = false;
                     int k = 0;
-                    if (lvalid) {
-                        const float qx = (float)((e.id >> 10) & 63u) * 4.f + 1.5f, qy = (float)((e.id >> 5) & 31u) * 8.f + 3.5f,
-                                    qz = (float)(e.id & 31u) * 8.f + 3.5f;
-                        const f2 px = f2{qx, qx}, py = f2{qy, qy}, pz = f2{qz, qz};
-                        f2 d[3];
-#pragma unroll
-                        for (int j = 0; j < 3; j++) {
-                            f2 dd = __builtin_elementwise_fma(px, lw_x[j], lc2[j]);
-                            dd = __builtin_elementwise_fma(py, lw_y[j], dd);
-                            d[j] = __builtin_elementwise_fma(pz, lw_z[j], dd);
-                        }
-                        const float dv[5] = {d[0].x, d[0].y, d[1].x, d[1].y, d[2].x};
-                        const float m1 = fminf(fminf(fminf(dv[0], dv[1]), fminf(dv[2], dv[3])), dv[4]);
-                        k = dv[0] == m1 ? 0 : (dv[1] == m1 ? 1 : (dv[2] == m1 ? 2 : (dv[3] == m1 ? 3 : 4)));
-                        const float *tk = &sm.thrL[1][k * kMaxK];
-                        pass = (dv[0] - m1 > tk[0]) & (dv[1] - m1 > tk[1]) & (dv[2] - m1 > tk[2]) &
-                               (dv[3] - m1 > tk[3]) & (dv[4] - m1 > tk[4]);
-                    }
+                    if (lvalid)
+                        pass = box_test((float)((e.id >> 10) & 63u) * 4.f + 1.5f, (float)((e.id >> 5) & 31u) * 8.f + 3.5f,
+                                        (float)(e.id & 31u) * 8.f + 3.5f, 1, k);
                     if (pass) {
                         // colour sums = n origin + sum u (origin (4R, 8G2, 8B2))
                         const uint32_t n = (e.id >> 18) & 511u;
@@ -1667,18 +1679,12 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
                         atomicAdd(&sm.accB[k][tid], (unsigned long long)(n * oz + (e.sums >> 21)) |
                                                         ((unsigned long long)n << 32));
                     }
-                    // the failing cells' cubes: cell c's nc = 1 + (bits 16..17) cubes go to list
-                    // slots [pre_c, pre_c + nc), pre_c = sum of nc over the failing lanes below
-                    // (three ballots: the count and its two low bits)
                     const bool cf = lvalid && !pass;
                     const uint32_t nc1 = (e.id >> 16) & 3u;
                     const unsigned long long F = __ballot(cf), B0 = __ballot(cf && (nc1 & 1u)),
                                              B1 = __ballot(cf && (nc1 & 2u));
                     if (F) {
-                        auto rank = [&](unsigned long long m) {
-                            return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                        };
-                        const uint32_t pre = rank(F) + rank(B0) + 2u * rank(B1);
+                        const uint32_t pre = mrank(F) + mrank(B0) + 2u * mrank(B1);
                         const int total = __popcll(F) + __popcll(B0) + 2 * __popcll(B1);
                         if (cf) {
 #pragma unroll
@@ -1695,9 +1701,80 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
                             if (v) ce = ctab[ql[b + lane]];
                             cube_body(ce, v);
                         }
-                        __builtin_amdgcn_wave_barrier();  // (the next chunk rewrites the list)
+                        __builtin_amdgcn_wave_barrier();  // (the next batch rewrites the list)
                     }
-                    base = nb;
+                };
+#if LLFE_KM_SUPS
+                if (cubes.sups) {
+                    // Super-cells first (SupEnt: the up to four cells of a 4 x 16 x 16 box, two
+                    // pairs in the cell table), the same test with centre
+                    // q = origin + (1.5, 7.5, 7.5); the cells of the failing super-cells of a chunk
+                    // are listed in the wave's cell list (sm.cs) and go through cell_body 64 at a time.
+                    const int S = cubes.n_sups[img];
+                    const SupEnt *stab = cubes.sups + (size_t)img * cubes.sup_stride;
+                    int *qs = sm.cs[wid];
+                    int base = __builtin_amdgcn_readfirstlane(grab());
+                    int ahead = grab();
+                    SupEnt sn{0u, 0u, 0u, 0u};
+                    if (base + lane < S) sn = stab[base + lane];
+                    while (base < S) {
+                        const bool svalid = base + lane < S;
+                        const SupEnt e = sn;
+                        const int nb = __builtin_amdgcn_readfirstlane(ahead);
+                        if (nb + lane < S) sn = stab[nb + lane];
+                        if (nb < S) ahead = grab();
+                        bool pass = false;
+                        int k = 0;
+                        if (svalid)
+                            pass = box_test((float)((e.id >> 8) & 63u) * 4.f + 1.5f, (float)((e.id >> 4) & 15u) * 16.f + 7.5f,
+                                            (float)(e.id & 15u) * 16.f + 7.5f, 2, k);
+                        if (pass) {
+                            const uint32_t n = (e.id >> 18) & 2047u;
+                            const uint32_t ox = ((e.id >> 8) & 63u) * 4u, oy = ((e.id >> 4) & 15u) * 16u, oz = (e.id & 15u) * 16u;
+                            atomicAdd(&sm.accA[k][tid], (unsigned long long)(n * ox + (e.srg & 4095u)) |
+                                                            ((unsigned long long)(n * oy + (e.srg >> 12)) << 32));
+                            atomicAdd(&sm.accB[k][tid], (unsigned long long)(n * oz + e.sb) | ((unsigned long long)n << 32));
+                        }
+                        const bool sf = svalid && !pass;
+                        const uint32_t c0 = (e.id >> 14) & 3u, ns1 = c0 + ((e.id >> 16) & 3u) - 1u;
+                        const unsigned long long F = __ballot(sf), B0 = __ballot(sf && (ns1 & 1u)),
+                                                 B1 = __ballot(sf && (ns1 & 2u));
+                        if (F) {
+                            const uint32_t pre = mrank(F) + mrank(B0) + 2u * mrank(B1);
+                            const int total = __popcll(F) + __popcll(B0) + 2 * __popcll(B1);
+                            if (sf) {
+#pragma unroll
+                                for (uint32_t jj = 0; jj < 4; jj++)
+                                    if (jj <= ns1)
+                                        qs[pre + jj] = (int)(jj < c0 ? (e.first & 0xFFFFu) + jj : (e.first >> 16) + jj - c0);
+                            }
+                            __builtin_amdgcn_wave_barrier();
+                            for (int b = 0; b < total; b += 64) {
+                                const bool v = b + lane < total;
+                                CellEnt ce{0u, 0u, 0u, 0u};
+                                if (v) ce = ltab[qs[b + lane]];
+                                cell_body(ce, v);
+                            }
+                            __builtin_amdgcn_wave_barrier();
+                        }
+                        base = nb;
+                    }
+                } else
+#endif
+                {
+                    int base = __builtin_amdgcn_readfirstlane(grab());
+                    int ahead = grab();
+                    CellEnt ln{0u, 0u, 0u, 0u};
+                    if (base + lane < L) ln = ltab[base + lane];
+                    while (base < L) {
+                        const bool lvalid = base + lane < L;
+                        const CellEnt e = ln;
+                        const int nb = __builtin_amdgcn_readfirstlane(ahead);
+                        if (nb + lane < L) ln = ltab[nb + lane];
+                        if (nb < L) ahead = grab();
+                        cell_body(e, lvalid);
+                        base = nb;
+                    }
                 }
             } else {
                 int base = __builtin_amdgcn_readfirstlane(grab());

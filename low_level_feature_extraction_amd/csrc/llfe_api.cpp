@@ -217,7 +217,8 @@ struct Work {
     DevBuf<uint32_t> d_raw, d_keys, d_kscratch, d_pmeta, d_tstrong, d_segtab;  // d_segtab: k_uq_scatter's run table
     DevBuf<CubeEnt> d_segcubes, d_cubes;
     DevBuf<CellEnt> d_segcells, d_cells;
-    DevBuf<int32_t> d_ncubes, d_ncells;
+    DevBuf<SupEnt> d_segsups, d_sups;
+    DevBuf<int32_t> d_ncubes, d_ncells, d_nsups;
     DevBuf<int64_t> d_nuniq;
     DevBuf<KmeansAttemptOut> d_att;
     int km_n = 0, km_colors = 0;  // images / n_colors of the last k-means launch (d_att)
@@ -350,8 +351,9 @@ int chunk_for(int h, int w) {
     const double P = (double)h * (double)w;
     const double cubes = std::min(P, (double)kMaxCubes), cells = std::min(cubes, (double)kParts * kCellsPerPart);
     const double per_image = 16.0 * P +  // keys, segments, class map, labels, masks
-                             (double)kParts * (kCubesPerPart * sizeof(CubeEnt) + kCellsPerPart * sizeof(CellEnt)) +
-                             cubes * sizeof(CubeEnt) + cells * sizeof(CellEnt);  // the gathered tables
+                             (double)kParts * (kCubesPerPart * sizeof(CubeEnt) + kCellsPerPart * sizeof(CellEnt) +
+                                               kSupsPerPart * sizeof(SupEnt)) +
+                             cubes * sizeof(CubeEnt) + 2.0 * cells * sizeof(CellEnt);  // the gathered tables
     const double n = gb * 1e9 / per_image;
     return (int)std::max(1.0, std::min(n, (double)kMaxKmeansBatch));
 }
@@ -668,12 +670,15 @@ int color_stage(llfe_ctx *ctx, Work &W, const uint8_t *img, const uint64_t *img_
     HIPCHK(ctx, W.d_segcells.ensure((size_t)n * kParts * kCellsPerPart));
     HIPCHK(ctx, W.d_cells.ensure((size_t)n * cell_stride));
     HIPCHK(ctx, W.d_ncells.ensure(n));
-    HIPCHK(ctx, W.d_pmeta.ensure((size_t)n * kParts * 4));
+    HIPCHK(ctx, W.d_segsups.ensure((size_t)n * kParts * kSupsPerPart));
+    HIPCHK(ctx, W.d_sups.ensure((size_t)n * cell_stride));
+    HIPCHK(ctx, W.d_nsups.ensure(n));
+    HIPCHK(ctx, W.d_pmeta.ensure((size_t)n * kParts * 5));
     HIPCHK(ctx, W.d_nuniq.ensure(n));
     HIPCHK(ctx, W.d_ncubes.ensure(n));
-    // (d_pmeta: hist, cl, uq, cc; k-means reads uq)
+    // (d_pmeta: hist, cl, uq, cc, cs; k-means reads uq)
     uint32_t *hist = W.d_pmeta.p, *cl = hist + (size_t)n * kParts, *uq = hist + (size_t)2 * n * kParts,
-             *cc = uq + (size_t)n * kParts;
+             *cc = uq + (size_t)n * kParts, *cs = cc + (size_t)n * kParts;
     HIPCHK(ctx, hipMemsetAsync(hist, 0, sizeof(uint32_t) * n * kParts, s));
     HIPCHK(ctx, W.d_segtab.ensure((size_t)n * uq_tab_words(P)));
     if (!noise) {
@@ -692,11 +697,11 @@ int color_stage(llfe_ctx *ctx, Work &W, const uint8_t *img, const uint64_t *img_
     // the partitions' sorted unique keys go to the (free) d_raw
     TIMED(ctx, s, "k_uq_part", (double)n * 4194304.0,
           launch_uq_part(W.d_keys.p, n, key_stride, P, hist, W.d_segtab.p, W.d_raw.p, W.d_segcubes.p,
-                         W.d_segcells.p, uq, cc, cl, s));
+                         W.d_segcells.p, W.d_segsups.p, uq, cc, cl, cs, s));
     TIMED(ctx, s, "k_uq_gather", 0,
-          launch_uq_gather(W.d_raw.p, n, key_stride, hist, uq, cc, cl, W.d_segcubes.p, W.d_segcells.p, W.d_keys.p,
-                           W.d_cubes.p, W.d_cells.p, cube_stride, cell_stride, W.d_nuniq.p, W.d_ncubes.p, W.d_ncells.p,
-                           contiguous_keys, s));
+          launch_uq_gather(W.d_raw.p, n, key_stride, hist, uq, cc, cl, cs, W.d_segcubes.p, W.d_segcells.p,
+                           W.d_segsups.p, W.d_keys.p, W.d_cubes.p, W.d_cells.p, W.d_sups.p, cube_stride, cell_stride,
+                           cell_stride, W.d_nuniq.p, W.d_ncubes.p, W.d_ncells.p, W.d_nsups.p, contiguous_keys, s));
     return LLFE_OK;
 }
 
@@ -909,7 +914,8 @@ int enqueue_chunk(llfe_ctx *ctx, const llfe_batch *b, uint32_t features, uint64_
         const KmeansCubes cubes{W.d_cubes.p, std::min<int64_t>(key_stride, kMaxCubes), W.d_ncubes.p,
                                 W.d_pmeta.p + (size_t)2 * n * kParts, W.d_cells.p, W.d_ncells.p,
                                 std::min<int64_t>(std::min<int64_t>(key_stride, kMaxCubes), (int64_t)kParts * kCellsPerPart),
-                                seg ? W.d_pmeta.p : nullptr};
+                                seg ? W.d_pmeta.p : nullptr, W.d_sups.p, W.d_nsups.p,
+                                std::min<int64_t>(std::min<int64_t>(key_stride, kMaxCubes), (int64_t)kParts * kCellsPerPart)};
         rc = kmeans_stage(ctx, W, seg ? W.d_raw.p : W.d_keys.p, key_stride, W.d_nuniq.p, n, n_colors, seed, index,
                           cubes, col_s);
         if (rc) return rc;
@@ -1791,7 +1797,7 @@ int llfe_kmeans(llfe_ctx *ctx, const uint32_t *keys, int64_t key_stride, const i
     Work &W = ctx->ws[0];
     HIPCHK(ctx, W.d_nuniq.ensure(n));
     HIPCHK(ctx, hipMemcpyAsync(W.d_nuniq.p, n_points, sizeof(int64_t) * n, hipMemcpyHostToDevice, s));
-    const KmeansCubes none{nullptr, 0, nullptr, nullptr, nullptr, nullptr, 0, nullptr};  // plain sweeps over caller-supplied keys
+    const KmeansCubes none{nullptr, 0, nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr, 0};  // plain sweeps over caller-supplied keys
     int rc = kmeans_stage(ctx, W, keys, key_stride, W.d_nuniq.p, n, n_colors, seed, ImgIndex{index_base, nullptr}, none, s);
     if (rc) return rc;
     HIPCHK(ctx, ctx->h_kout.ensure(n));

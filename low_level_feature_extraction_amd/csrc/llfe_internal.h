@@ -211,6 +211,18 @@ struct CellEnt {
     uint32_t s2;     // sum of |u|^2 (<= 27392)
 };
 static_assert(sizeof(CellEnt) == 16, "CellEnt is one 16-byte load");
+// 4 x 16 x 16 super-cells (round 6): the (up to) four cells (R, 2 G4 + j, 2 B4 + c) of one
+// partition; in the cell table (G2, B2) order they are two pairs, (j = 0, c = 0..1) at first0
+// and (j = 1, c = 0..1) at first1.  The Lloyd sweep tests them before their cells.
+constexpr int kSupsPerPart = 256;  // 16 x 16 super-cells per partition
+struct SupEnt {
+    uint32_t id;     // R << 8 | G4 << 4 | B4 in bits 0..13, cells of the j = 0 pair (0..2) in bits 14..15,
+                     // of the j = 1 pair in bits 16..17, colour count (<= 1024) in bits 18..28
+    uint32_t first;  // first0 | first1 << 16: the pairs' first cell indices in the image's cell table
+    uint32_t srg;    // sum over its colours u = colour - origin: u_r (<= 3072) | u_g << 12 (<= 15360)
+    uint32_t sb;     // sum of u_b (<= 15360)
+};
+static_assert(sizeof(SupEnt) == 16, "SupEnt is one 16-byte load");
 struct KmeansCubes {
     const CubeEnt *cubes;   // per image (cube_stride) entries, partition by partition (nullptr: no pruning)
     int64_t cube_stride;
@@ -224,6 +236,9 @@ struct KmeansCubes {
     // partitions' pixel counts: partition R's unique keys at [sum_{r<R} hist_r, + uq_R)),
     // not contiguously; part_uq gives the unique counts.
     const uint32_t *part_hist;
+    const SupEnt *sups;       // per image (sup_stride) super-cells in partition order (nullptr: none)
+    const int32_t *n_sups;
+    int64_t sup_stride;
 };
 // Unique colours (unique.hip), all per image with stride key_stride (u32 keys):
 //   keys:    pixels -> noised keys into `raw`, partition histogram `hist` (n x 64, zeroed)
@@ -247,14 +262,14 @@ hipError_t launch_uq_scatter(const uint8_t *bgr, const uint64_t *img_tab, const 
                              uint64_t seed, ImgIndex index, int64_t key_stride, uint32_t *hist, uint32_t *tab,
                              uint32_t *seg, hipStream_t s);
 hipError_t launch_uq_part(const uint32_t *seg, int n, int64_t key_stride, int64_t P, const uint32_t *hist,
-                          const uint32_t *tab, uint32_t *skeys, CubeEnt *seg_cubes, CellEnt *seg_cells, uint32_t *uq,
-                          uint32_t *cc, uint32_t *cl, hipStream_t s);
+                          const uint32_t *tab, uint32_t *skeys, CubeEnt *seg_cubes, CellEnt *seg_cells,
+                          SupEnt *seg_sups, uint32_t *uq, uint32_t *cc, uint32_t *cl, uint32_t *cs, hipStream_t s);
 hipError_t launch_uq_gather(const uint32_t *skeys, int n, int64_t key_stride, const uint32_t *hist, const uint32_t *uq,
-                            const uint32_t *cc, const uint32_t *cl, const CubeEnt *seg_cubes,
-                            const CellEnt *seg_cells, uint32_t *keys, CubeEnt *cubes, CellEnt *cells,
-                            int64_t cube_stride, int64_t cell_stride, int64_t *n_unique, int32_t *n_cubes,
-                            int32_t *n_cells,
-                            bool copy_keys, hipStream_t s);
+                            const uint32_t *cc, const uint32_t *cl, const uint32_t *cs, const CubeEnt *seg_cubes,
+                            const CellEnt *seg_cells, const SupEnt *seg_sups, uint32_t *keys, CubeEnt *cubes,
+                            CellEnt *cells, SupEnt *sups, int64_t cube_stride, int64_t cell_stride, int64_t sup_stride,
+                            int64_t *n_unique, int32_t *n_cubes, int32_t *n_cells, int32_t *n_sups, bool copy_keys,
+                            hipStream_t s);
 
 // per image: K = min(n_colors, U); attempts run as separate workgroups
 // (ordered largest U first), then a finalize kernel picks the best attempt.

@@ -313,15 +313,20 @@ __device__ __forceinline__ unsigned long long scan_u64_wg(unsigned long long v, 
     return r;
 }
 
-// grid (64, n).  Reads the partition's keys as its runs in the step segments (`tab`), writes
+// grid (64, n).  amdgpu_waves_per_eu(8): the super-cell sums (round 6) took the kernel from 62 to
+// 70 VGPRs, three workgroups per CU instead of four; held at 64 it spills 3 VGPRs in the unique-key
+// scans (a few scratch accesses per workgroup) and measured the faster of the two
+// (profiles/r6/kmeans_sups/var_time.txt: supb vs supa).
+// Reads the partition's keys as its runs in the step segments (`tab`), writes
 // the sorted unique keys to `skeys` at the partition's place in key order (capacity: its
 // hist count), and up to 4096 cube entries to `seg_cubes`.
-__global__ __launch_bounds__(UT) void k_uq_part(const uint32_t *__restrict__ seg, long long key_stride, long long P,
+__global__ __launch_bounds__(UT) __attribute__((amdgpu_waves_per_eu(8))) void k_uq_part(const uint32_t *__restrict__ seg, long long key_stride, long long P,
                                                 const uint32_t *__restrict__ hist, const uint32_t *__restrict__ tab,
                                                 uint32_t *__restrict__ skeys,
                                                 CubeEnt *__restrict__ seg_cubes, CellEnt *__restrict__ seg_cells,
+                                                SupEnt *__restrict__ seg_sups,
                                                 uint32_t *__restrict__ uq, uint32_t *__restrict__ cc,
-                                                uint32_t *__restrict__ cl) {
+                                                uint32_t *__restrict__ cl, uint32_t *__restrict__ cs) {
     __shared__ __attribute__((aligned(16))) uint32_t W[4 * 2048];  // rows r = 4R + i, word g << 3 | b >> 5
     __shared__ unsigned long long tmp[UT / 64];
     __shared__ uint32_t sbase, scount;
@@ -341,6 +346,7 @@ __global__ __launch_bounds__(UT) void k_uq_part(const uint32_t *__restrict__ seg
             uq[(size_t)img * NPART + R] = 0;
             cc[(size_t)img * NPART + R] = 0;
             cl[(size_t)img * NPART + R] = 0;
+            cs[(size_t)img * NPART + R] = 0;
         }
         return;
     }
@@ -426,17 +432,21 @@ __global__ __launch_bounds__(UT) void k_uq_part(const uint32_t *__restrict__ seg
         }
         if (t == 0) uq[(size_t)img * NPART + R] = sbase_q;
     }
-    // (b) the partition's 4x4x4 cubes and 4x8x8 cells.  In pass h thread t owns cell
-    // (G2, B2) = (c >> 5, c & 31), c = h UT + t, and its four cubes (G, B) = (2 G2 + j,
-    // 2 B2 + cc), written in cell order and within a cell in (j, cc) order, so a cell's cubes
-    // are consecutive; bit i*16 + jj*4 + bb of a cube = colour (4R + i, 4G + jj, 4B + bb).
-    // The cell's colours are the bytes (B2 & 3) of the 32 words W[i][8 G2 + g][B2 >> 2].
-    uint32_t cbase = 0, lbase = 0;
+    // (b) the partition's 4x4x4 cubes, 4x8x8 cells and 4x16x16 super-cells.  In pass h thread
+    // t owns cell (G2, B2) = (c >> 5, c & 31), c = h UT + t, and its four cubes (G, B) =
+    // (2 G2 + j, 2 B2 + cc), written in cell order and within a cell in (j, cc) order, so a
+    // cell's cubes are consecutive; bit i*16 + jj*4 + bb of a cube = colour (4R + i, 4G + jj,
+    // 4B + bb).  The cell's colours are the bytes (B2 & 3) of the 32 words W[i][8 G2 + g][B2 >> 2].
+    // A wave holds the cell rows G2 = 2 G4, 2 G4 + 1: super-cell (G4, B4) is lanes {2 B4,
+    // 2 B4 + 1} of both rows (lane quads {l, l ^ 1, l ^ 32, l ^ 33}, l = 2 B4).
+    uint32_t cbase = 0, lbase = 0, sbase_s = 0;
     CubeEnt *ce = seg_cubes + ((size_t)img * NPART + R) * 4096;
     CellEnt *le = seg_cells + ((size_t)img * NPART + R) * kCellsPerPart;
+    SupEnt *se = seg_sups + ((size_t)img * NPART + R) * kSupsPerPart;
 #pragma unroll 1
     for (int h = 0; h < kCellsPerPart / UT; h++) {
         const int cell = h * UT + t, G2 = cell >> 5, B2 = cell & 31;
+        const bool lead = (t & 33) == 0;  // the quad's (row 0, even B2) lane
         const int wsel = (G2 << 6) | (B2 >> 2), sh0 = (B2 & 3) * 8;
         unsigned long long mask[4];  // cube (j, c) = mask[2 j + c]
 #pragma unroll
@@ -453,13 +463,23 @@ __global__ __launch_bounds__(UT) void k_uq_part(const uint32_t *__restrict__ seg
         unsigned long long mine = 0;
 #pragma unroll
         for (int q = 0; q < 4; q++) mine += mask[q] ? 1ull : 0ull;
-        if (mine) mine |= 1ull << 32;  // one cell
+        // one cell; one super-cell on the quad's first thread when any of its cells is occupied
+        // (fields: cubes bits 0..31, cells 32..47, super-cells 48..63 -- per pass <= 2048 /
+        // 512 / 128, no carries)
+        const bool any_cell = mine != 0;
+        uint32_t mq = any_cell ? 1u : 0u;
+        mq |= __shfl_xor(mq, 1);
+        mq |= __shfl_xor(mq, 32);
+        if (any_cell) mine |= 1ull << 32;
+        if (lead && mq) mine |= 1ull << 48;
         unsigned long long tot;
         const unsigned long long pos = scan_u64_wg(mine, tmp, &tot);
         uint32_t ci = cbase + (uint32_t)pos;
-        const uint32_t li = lbase + (uint32_t)(pos >> 32), first = ci;
+        const uint32_t li = lbase + (uint32_t)((pos >> 32) & 0xFFFFu), first = ci;
+        const uint32_t si = sbase_s + (uint32_t)(pos >> 48);
         cbase += (uint32_t)tot;
-        lbase += (uint32_t)(tot >> 32);
+        lbase += (uint32_t)((tot >> 32) & 0xFFFFu);
+        sbase_s += (uint32_t)(tot >> 48);
         uint32_t ln = 0, lr = 0, lg = 0, lb = 0, l2 = 0;  // the cell's sums
 #pragma unroll
         for (int q = 0; q < 4; q++) {
@@ -507,10 +527,35 @@ __global__ __launch_bounds__(UT) void k_uq_part(const uint32_t *__restrict__ seg
             e.s2 = l2;
             le[li] = e;
         }
+        // the super-cell's count and sums over u = colour - (4R, 16 G4, 16 B4): the quad's cell
+        // sums shifted by their cells' offsets (0, 8 (G2 & 1), 8 (B2 & 1)), packed in pairs of
+        // 16-bit fields (count <= 1024 | occupied cells of the lane's row pair << 16, u_r <= 3072
+        // | u_b <= 15360 << 16; u_g <= 15360).  Its cells are the occupied ones among the row
+        // pairs' slots li (row 0, lane 2 B4) and li (row 1, lane 2 B4 + 32): first0 / first1.
+        uint32_t qnc = ln | (ln ? 1u << 16 : 0u), qrb = lr | ((lb + 8u * (uint32_t)(B2 & 1) * ln) << 16),
+                 qg = lg + 8u * (uint32_t)(G2 & 1) * ln;
+        qnc += __shfl_xor(qnc, 1);  // (row pair: counts and its cells)
+        const uint32_t c_row1 = __shfl_xor(qnc, 32) >> 16, first1 = __shfl_xor(li, 32);
+        qnc += __shfl_xor(qnc, 32) & 0xFFFFu;
+        qrb += __shfl_xor(qrb, 1);
+        qrb += __shfl_xor(qrb, 32);
+        qg += __shfl_xor(qg, 1);
+        qg += __shfl_xor(qg, 32);
+        if (lead && (qnc & 0xFFFFu)) {
+            const uint32_t c_row0 = qnc >> 16;
+            SupEnt e;
+            e.id = ((uint32_t)R << 8) | ((uint32_t)(G2 >> 1) << 4) | (uint32_t)(B2 >> 1) | (c_row0 << 14) |
+                   (c_row1 << 16) | ((qnc & 0xFFFFu) << 18);
+            e.first = li | (first1 << 16);
+            e.srg = (qrb & 0xFFFFu) | (qg << 12);
+            e.sb = qrb >> 16;
+            se[si] = e;
+        }
     }
     if (t == 0) {
         cc[(size_t)img * NPART + R] = cbase;
         cl[(size_t)img * NPART + R] = lbase;
+        cs[(size_t)img * NPART + R] = sbase_s;
     }
 }
 
@@ -523,37 +568,45 @@ constexpr int GT = 256;
 __global__ __launch_bounds__(GT) void k_uq_gather(const uint32_t *__restrict__ skeys, long long key_stride,
                                                   const uint32_t *__restrict__ hist, const uint32_t *__restrict__ uq,
                                                   const uint32_t *__restrict__ cc, const uint32_t *__restrict__ cl,
+                                                  const uint32_t *__restrict__ cs,
                                                   const CubeEnt *__restrict__ seg_cubes,
-                                                  const CellEnt *__restrict__ seg_cells, uint32_t *__restrict__ keys,
+                                                  const CellEnt *__restrict__ seg_cells,
+                                                  const SupEnt *__restrict__ seg_sups, uint32_t *__restrict__ keys,
                                                   CubeEnt *__restrict__ cubes, CellEnt *__restrict__ cells,
-                                                  long long cube_stride, long long cell_stride,
+                                                  SupEnt *__restrict__ sups,
+                                                  long long cube_stride, long long cell_stride, long long sup_stride,
                                                   long long *__restrict__ n_unique,
-                                                  int *__restrict__ n_cubes, int *__restrict__ n_cells, int copy_keys) {
-    __shared__ uint32_t sp, su, sc, sl, nu, nc, nl;
+                                                  int *__restrict__ n_cubes, int *__restrict__ n_cells,
+                                                  int *__restrict__ n_sups, int copy_keys) {
+    __shared__ uint32_t sp, su, sc, sl, ss, nu, nc, nl, ns;
     const int R = blockIdx.x, img = blockIdx.y, t = threadIdx.x;
     if (t < 64) {
-        uint32_t tot, ut, ct, lt;
+        uint32_t tot, ut, ct, lt, st;
         const uint32_t ps = part_base(hist + (size_t)img * NPART, t, &tot);
         const uint32_t ub = part_base(uq + (size_t)img * NPART, t, &ut);
         const uint32_t cb = part_base(cc + (size_t)img * NPART, t, &ct);
         const uint32_t lb = part_base(cl + (size_t)img * NPART, t, &lt);
+        const uint32_t sb = part_base(cs + (size_t)img * NPART, t, &st);
         if (t == R) {
             sp = ps;
             su = ub;
             sc = cb;
             sl = lb;
+            ss = sb;
             nu = uq[(size_t)img * NPART + R];
             nc = cc[(size_t)img * NPART + R];
             nl = cl[(size_t)img * NPART + R];
+            ns = cs[(size_t)img * NPART + R];
         }
         if (t == 0 && R == 0) {
             n_unique[img] = ut;
             n_cubes[img] = (int)ct;
             n_cells[img] = (int)lt;
+            n_sups[img] = (int)st;
         }
     }
     __syncthreads();
-    const uint32_t U = nu, C = nc, L = nl, cbase = sc;
+    const uint32_t U = nu, C = nc, L = nl, S = ns, cbase = sc, lbase = sl;
     const uint32_t *sk = skeys + (size_t)img * key_stride + sp;
     uint32_t *ok = keys + (size_t)img * key_stride + su;
     if (copy_keys)
@@ -567,6 +620,13 @@ __global__ __launch_bounds__(GT) void k_uq_gather(const uint32_t *__restrict__ s
         CellEnt e = slp[i];
         e.first += cbase;
         ol[i] = e;
+    }
+    const SupEnt *ssp = seg_sups + ((size_t)img * NPART + R) * kSupsPerPart;
+    SupEnt *os = sups + (size_t)img * sup_stride + ss;
+    for (uint32_t i = t; i < S; i += GT) {
+        SupEnt e = ssp[i];
+        e.first += lbase | (lbase << 16);  // (both cell indices; an image's cells are < 65536)
+        os[i] = e;
     }
 }
 
@@ -608,22 +668,23 @@ hipError_t launch_uq_scatter(const uint8_t *bgr, const uint64_t *img_tab, const 
 }
 
 hipError_t launch_uq_part(const uint32_t *seg, int n, int64_t key_stride, int64_t P, const uint32_t *hist,
-                          const uint32_t *tab, uint32_t *skeys, CubeEnt *seg_cubes, CellEnt *seg_cells, uint32_t *uq,
-                          uint32_t *cc, uint32_t *cl, hipStream_t s) {
+                          const uint32_t *tab, uint32_t *skeys, CubeEnt *seg_cubes, CellEnt *seg_cells,
+                          SupEnt *seg_sups, uint32_t *uq, uint32_t *cc, uint32_t *cl, uint32_t *cs, hipStream_t s) {
     hipLaunchKernelGGL(k_uq_part, dim3(NPART, n), dim3(UT), 0, s, seg, (long long)key_stride, (long long)P, hist, tab,
-                       skeys, seg_cubes, seg_cells, uq, cc, cl);
+                       skeys, seg_cubes, seg_cells, seg_sups, uq, cc, cl, cs);
     return hipGetLastError();
 }
 
 hipError_t launch_uq_gather(const uint32_t *skeys, int n, int64_t key_stride, const uint32_t *hist, const uint32_t *uq,
-                            const uint32_t *cc, const uint32_t *cl, const CubeEnt *seg_cubes,
-                            const CellEnt *seg_cells, uint32_t *keys, CubeEnt *cubes, CellEnt *cells,
-                            int64_t cube_stride, int64_t cell_stride, int64_t *n_unique, int32_t *n_cubes,
-                            int32_t *n_cells, bool copy_keys, hipStream_t s) {
-    hipLaunchKernelGGL(k_uq_gather, dim3(NPART, n), dim3(GT), 0, s, skeys, (long long)key_stride, hist, uq, cc, cl,
-                       seg_cubes, seg_cells, keys, cubes, cells, (long long)cube_stride, (long long)cell_stride,
-                       (long long *)n_unique,
-                       (int *)n_cubes, (int *)n_cells, copy_keys ? 1 : 0);
+                            const uint32_t *cc, const uint32_t *cl, const uint32_t *cs, const CubeEnt *seg_cubes,
+                            const CellEnt *seg_cells, const SupEnt *seg_sups, uint32_t *keys, CubeEnt *cubes,
+                            CellEnt *cells, SupEnt *sups, int64_t cube_stride, int64_t cell_stride, int64_t sup_stride,
+                            int64_t *n_unique, int32_t *n_cubes, int32_t *n_cells, int32_t *n_sups, bool copy_keys,
+                            hipStream_t s) {
+    hipLaunchKernelGGL(k_uq_gather, dim3(NPART, n), dim3(GT), 0, s, skeys, (long long)key_stride, hist, uq, cc, cl, cs,
+                       seg_cubes, seg_cells, seg_sups, keys, cubes, cells, sups, (long long)cube_stride,
+                       (long long)cell_stride, (long long)sup_stride, (long long *)n_unique, (int *)n_cubes,
+                       (int *)n_cells, (int *)n_sups, copy_keys ? 1 : 0);
     return hipGetLastError();
 }
 

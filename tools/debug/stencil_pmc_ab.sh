@@ -2,7 +2,9 @@
 # GPU box (round 6): SQ counters of the stencil on the 512 x 1080p mix (3 launches,
 # tools/debug/stencil_kind.py), static grid (LLFE_ST_QUEUE=0) vs work queue, one
 # rocprofv3 --pmc pass each (8 SQ + 1 GRBM counters), plus a kernel-trace pass for the
-# durations.  Summary: gpurun_out/stencil_pmc_ab/summary.txt
+# durations.  Summary: gpurun_out/stencil_pmc_ab/summary.txt (round 6's is kept in
+# profiles/r6/stencil_breakdown/).  The work-queue kernel was measured and removed
+# (DESIGN.md §3), so both passes now run the static grid.
 set -u -o pipefail
 O=gpurun_out/stencil_pmc_ab
 mkdir -p $O
