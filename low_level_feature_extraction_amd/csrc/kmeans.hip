@@ -27,7 +27,10 @@
 namespace llfe {
 namespace {
 
-constexpr int kCellMinCubes = 8192;
+#ifndef LLFE_KM_CELL_MIN
+#define LLFE_KM_CELL_MIN 8192
+#endif
+constexpr int kCellMinCubes = LLFE_KM_CELL_MIN;  // cube count from which the sweeps take cells / super-cells
 #ifndef LLFE_KM_SPLIT
 #define LLFE_KM_SPLIT 0  // the cube path in two launches (measured slower; kept as a build option)
 #endif
@@ -39,6 +42,9 @@ constexpr int kCellMinCubes = 8192;
 #endif  // the sweeps test cells before cubes from this cube count on
 #ifndef LLFE_KM_SUPS
 #define LLFE_KM_SUPS 1  // Lloyd tests 4 x 16 x 16 super-cells before cells
+#endif
+#ifndef LLFE_KM_PP_SUPS
+#define LLFE_KM_PP_SUPS 0  // k-means++ sweeps test 4 x 16 x 16 super-cells before cells (measured slower)
 #endif
 #ifndef LLFE_KM_THREADS
 #define LLFE_KM_THREADS 512
@@ -210,6 +216,7 @@ struct KmSmem {
     unsigned long long qtot;             // sum of |p|^2 over all colours (exact)
     int marg[kMaxK * kMaxK + 6 * kMaxK]; // k-means++ corner margins: centre pairs, trial vs centre (+/-)
     int margc[kMaxK * kMaxK + 6 * kMaxK];  // the same for the 4 x 8 x 8 cells
+    int margs[kMaxK * kMaxK + 6 * kMaxK];  // ... and the 4 x 16 x 16 super-cells
 };
 
 // two workgroups per CU (160 KB of LDS)
@@ -439,7 +446,7 @@ __device__ __forceinline__
 #endif
 void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, int K, uint64_t &rng,
                          const CubeEnt *__restrict__ ctab, int C, const CellEnt *__restrict__ ltab, int L,
-                         const uint32_t *__restrict__ part_uq, const uint32_t *__restrict__ hist,
+                         const SupEnt *__restrict__ stab, int S, const uint32_t *__restrict__ part_uq, const uint32_t *__restrict__ hist,
                          unsigned long long &bytes, uint32_t &pp_pts, uint32_t &pp_sel, uint64_t &t_sel) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t c0 = cvrng_next(rng) % (uint32_t)N;  // (every thread advances its rng copy)
@@ -770,6 +777,20 @@ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, int K, uint64
                                               14 * max(sg * (t[1] - sm.icc[k2][1]), 0) +
                                               14 * max(sg * (t[2] - sm.icc[k2][2]), 0);
             }
+            // ... and for a 4 x 16 x 16 super-cell: 2 (3, 15, 15) . max(+-(a - b), 0)
+            if (tid >= 128 && tid < 128 + kMaxK * kMaxK) {
+                const int q = tid - 128, m = q / kMaxK, k2 = q % kMaxK;
+                sm.margs[q] = 6 * max(sm.icc[m][0] - sm.icc[k2][0], 0) + 30 * max(sm.icc[m][1] - sm.icc[k2][1], 0) +
+                              30 * max(sm.icc[m][2] - sm.icc[k2][2], 0);
+            } else if (tid >= 128 + kMaxK * kMaxK && tid < 128 + kMaxK * kMaxK + 6 * kMaxK) {
+                const int q = tid - 128 - kMaxK * kMaxK, j = (q / kMaxK) % 3, k2 = q % kMaxK;
+                const int t[3] = {j == 0 ? tx[0] : (j == 1 ? tx[1] : tx[2]), j == 0 ? ty[0] : (j == 1 ? ty[1] : ty[2]),
+                                  j == 0 ? tz[0] : (j == 1 ? tz[1] : tz[2])};
+                const int sg = q < 3 * kMaxK ? 1 : -1;
+                sm.margs[kMaxK * kMaxK + q] = 6 * max(sg * (t[0] - sm.icc[k2][0]), 0) +
+                                              30 * max(sg * (t[1] - sm.icc[k2][1]), 0) +
+                                              30 * max(sg * (t[2] - sm.icc[k2][2]), 0);
+            }
             __syncthreads();
             const int *Mkk = sm.marg, *NA = sm.marg + kMaxK * kMaxK, *NB = sm.marg + kMaxK * kMaxK + 3 * kMaxK;
             // waves take 64-cube chunks from a shared LDS counter, read two chunks ahead
@@ -924,6 +945,129 @@ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, int K, uint64
                 // the cube path above, 64 at a time
                 const int *MKc = sm.margc, *NAc = sm.margc + kMaxK * kMaxK, *NBc = sm.margc + kMaxK * kMaxK + 3 * kMaxK;
                 int *ql = sm.cq[wid];
+                auto mrank = [&](unsigned long long m) {
+                    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                };
+                auto cell_vals = [&](const CellEnt &e, uint32_t &v0, uint32_t &v1, uint32_t &v2,
+                                     bool &fail) __attribute__((always_inline)) {
+                    box_vals((int)((e.id >> 10) & 63u) * 4, (int)((e.id >> 5) & 31u) * 8, (int)(e.id & 31u) * 8,
+                             (int)((e.id >> 18) & 511u), (int)(e.sums & 1023u), (int)((e.sums >> 10) & 2047u),
+                             (int)(e.sums >> 21), (int)e.s2, MKc, NAc, NBc, 3, 7, 7, v0, v1, v2, fail);
+                };
+                // the failing cells among the lanes of cf (one partition): their cubes, 64 at a time
+                auto cell_cubes = [&](const CellEnt &e, const bool cf) __attribute__((always_inline)) {
+                    const uint32_t nc1 = (e.id >> 16) & 3u;
+                    const unsigned long long F = __ballot(cf), B0 = __ballot(cf && (nc1 & 1u)),
+                                             B1 = __ballot(cf && (nc1 & 2u));
+                    if (F) {
+                        const uint32_t pre = mrank(F) + mrank(B0) + 2u * mrank(B1);
+                        const int total = __popcll(F) + __popcll(B0) + 2 * __popcll(B1);
+                        if (cf) {
+    #pragma unroll
+                            for (uint32_t jj = 0; jj < 4; jj++)
+                                if (jj <= nc1) ql[pre + jj] = (int)(e.first + jj);
+                        }
+                        __builtin_amdgcn_wave_barrier();
+                        for (int b = 0; b < total; b += 64) {
+                            const bool cv = b + lane < total;
+                            CubeEnt ce;
+                            ce.mask = 0;
+                            ce.id = 0;
+                            ce.sums = 0;
+                            if (cv) ce = ctab[ql[b + lane]];
+                            uint32_t c0 = 0, c1 = 0, c2 = 0;
+                            bool cfail = false;
+                            if (cv) cube_vals(ce, c0, c1, c2, cfail);
+                            if (cv && !cfail) {
+                                acc0 += c0;
+                                acc1 += c1;
+                                acc2 += c2;
+                            }
+                            const unsigned long long fm = __ballot(cv && cfail);
+                            if (fm) push_cubes(fm, ce);
+                        }
+                        __builtin_amdgcn_wave_barrier();  // (the list is rewritten next)
+                    }
+                };
+#if LLFE_KM_PP_SUPS
+                if (stab) {
+                    // super-cells first (round 6), the same closed forms with extents (3, 15, 15); the
+                    // cells of the undecided ones (one partition at a time) are listed in the wave's
+                    // cell list (sm.cs) and go through the cell path, 64 at a time
+                    const int *MKs = sm.margs, *NAs = sm.margs + kMaxK * kMaxK, *NBs = sm.margs + kMaxK * kMaxK + 3 * kMaxK;
+                    int *qs = sm.cs[wid];
+                    int run = __builtin_amdgcn_readfirstlane(grab());  // the current run's first super-cell
+                    int base = run;
+                    int ahead = grab();
+                    SupEnt en{0u, 0u, 0u, 0u};
+                    if (base + lane < S) en = stab[base + lane];
+                    while (base < S) {
+                        const bool valid = base + lane < S;
+                        const SupEnt e = en;
+                        int nb = base + 64;
+                        if (nb >= run + kRun || nb >= S) {  // (uniform) next run
+                            run = __builtin_amdgcn_readfirstlane(ahead);
+                            nb = run;
+                            if (nb < S) ahead = grab();
+                        }
+                        if (nb + lane < S) en = stab[nb + lane];
+                        const int P = valid ? (int)((e.id >> 8) & 63u) : kParts;
+                        uint32_t v0 = 0, v1 = 0, v2 = 0;
+                        bool fail = false;
+                        if (valid)
+                            box_vals((int)((e.id >> 8) & 63u) * 4, (int)((e.id >> 4) & 15u) * 16, (int)(e.id & 15u) * 16,
+                                     (int)((e.id >> 18) & 2047u), (int)(e.srg & 4095u), (int)(e.srg >> 12),
+                                     (int)(e.sb & 16383u), (int)((e.sb >> 14) | (((e.id >> 29) & 1u) << 18)), MKs, NAs,
+                                     NBs, 3, 15, 15, v0, v1, v2, fail);
+                        // lanes hold ascending super-cell ids: visit the batch's partitions in order
+                        int Pseg = __shfl(P, 0);
+                        for (;;) {
+                            next_part(Pseg);
+                            const bool mine = P == Pseg;
+                            if (mine && !fail) {
+                                acc0 += v0;
+                                acc1 += v1;
+                                acc2 += v2;
+                            }
+                            const bool sf = mine && fail;
+                            const uint32_t c0 = (e.id >> 14) & 3u, ns1 = c0 + ((e.id >> 16) & 3u) - 1u;
+                            const unsigned long long F = __ballot(sf), B0 = __ballot(sf && (ns1 & 1u)),
+                                                     B1 = __ballot(sf && (ns1 & 2u));
+                            if (F) {
+                                const uint32_t pre = mrank(F) + mrank(B0) + 2u * mrank(B1);
+                                const int total = __popcll(F) + __popcll(B0) + 2 * __popcll(B1);
+                                if (sf) {
+    #pragma unroll
+                                    for (uint32_t jj = 0; jj < 4; jj++)
+                                        if (jj <= ns1)
+                                            qs[pre + jj] = (int)(jj < c0 ? (e.first & 0xFFFFu) + jj : (e.first >> 16) + jj - c0);
+                                }
+                                __builtin_amdgcn_wave_barrier();
+                                for (int b = 0; b < total; b += 64) {
+                                    const bool cv = b + lane < total;
+                                    CellEnt ce{0u, 0u, 0u, 0u};
+                                    if (cv) ce = ltab[qs[b + lane]];
+                                    uint32_t c0v = 0, c1v = 0, c2v = 0;
+                                    bool cfail = false;
+                                    if (cv) cell_vals(ce, c0v, c1v, c2v, cfail);
+                                    if (cv && !cfail) {
+                                        acc0 += c0v;
+                                        acc1 += c1v;
+                                        acc2 += c2v;
+                                    }
+                                    cell_cubes(ce, cv && cfail);
+                                }
+                                __builtin_amdgcn_wave_barrier();  // (the list is rewritten next)
+                            }
+                            const unsigned long long rest = __ballot(P > Pseg && P < kParts);
+                            if (!rest) break;
+                            Pseg = __shfl(P, (int)__builtin_ctzll(rest));
+                        }
+                        base = nb;
+                    }
+                } else
+#endif
+                {
                 int run = __builtin_amdgcn_readfirstlane(grab());  // the current run's first cell
                 int base = run;
                 int ahead = grab();
@@ -942,10 +1086,7 @@ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, int K, uint64
                     const int P = valid ? (int)((e.id >> 10) & 63u) : kParts;
                     uint32_t v0 = 0, v1 = 0, v2 = 0;
                     bool fail = false;
-                    if (valid)
-                        box_vals((int)((e.id >> 10) & 63u) * 4, (int)((e.id >> 5) & 31u) * 8, (int)(e.id & 31u) * 8,
-                                 (int)((e.id >> 18) & 511u), (int)(e.sums & 1023u), (int)((e.sums >> 10) & 2047u),
-                                 (int)(e.sums >> 21), (int)e.s2, MKc, NAc, NBc, 3, 7, 7, v0, v1, v2, fail);
+                    if (valid) cell_vals(e, v0, v1, v2, fail);
                     // lanes hold ascending cell ids: visit the batch's partitions in order
                     int Pseg = __shfl(P, 0);
                     for (;;) {
@@ -956,48 +1097,13 @@ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, int K, uint64
                             acc1 += v1;
                             acc2 += v2;
                         }
-                        const bool cf = mine && fail;
-                        const uint32_t nc1 = (e.id >> 16) & 3u;
-                        const unsigned long long F = __ballot(cf), B0 = __ballot(cf && (nc1 & 1u)),
-                                                 B1 = __ballot(cf && (nc1 & 2u));
-                        if (F) {
-                            auto rank = [&](unsigned long long m) {
-                                return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                            };
-                            const uint32_t pre = rank(F) + rank(B0) + 2u * rank(B1);
-                            const int total = __popcll(F) + __popcll(B0) + 2 * __popcll(B1);
-                            if (cf) {
-        #pragma unroll
-                                for (uint32_t jj = 0; jj < 4; jj++)
-                                    if (jj <= nc1) ql[pre + jj] = (int)(e.first + jj);
-                            }
-                            __builtin_amdgcn_wave_barrier();
-                            for (int b = 0; b < total; b += 64) {
-                                const bool cv = b + lane < total;
-                                CubeEnt ce;
-                                ce.mask = 0;
-                                ce.id = 0;
-                                ce.sums = 0;
-                                if (cv) ce = ctab[ql[b + lane]];
-                                uint32_t c0 = 0, c1 = 0, c2 = 0;
-                                bool cfail = false;
-                                if (cv) cube_vals(ce, c0, c1, c2, cfail);
-                                if (cv && !cfail) {
-                                    acc0 += c0;
-                                    acc1 += c1;
-                                    acc2 += c2;
-                                }
-                                const unsigned long long fm = __ballot(cv && cfail);
-                                if (fm) push_cubes(fm, ce);
-                            }
-                            __builtin_amdgcn_wave_barrier();  // (the list is rewritten next)
-                        }
+                        cell_cubes(e, mine && fail);
                         const unsigned long long rest = __ballot(P > Pseg && P < kParts);
                         if (!rest) break;
                         Pseg = __shfl(P, (int)__builtin_ctzll(rest));
                     }
                     base = nb;
+                }
                 }
             } else {
                 int run = __builtin_amdgcn_readfirstlane(grab());  // the current run's first cube
@@ -1209,6 +1315,7 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
     // ------------------------------------------------ k-means++ (generateCentersPP)
     if (use_cubes) {
         pp_cubes(sm, pts, N, K, rng, ctab, C, cubes.cells + (size_t)img * cubes.cell_stride, cubes.n_cells[img],
+                 cubes.sups ? cubes.sups + (size_t)img * cubes.sup_stride : nullptr, cubes.sups ? cubes.n_sups[img] : 0,
                  cubes.part_uq + (size_t)img * kParts, cubes.part_hist ? cubes.part_hist + (size_t)img * kParts : nullptr,
                  bytes, pp_pts, pp_sel, t_sel);
     } else {
@@ -1733,7 +1840,7 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
                             const uint32_t ox = ((e.id >> 8) & 63u) * 4u, oy = ((e.id >> 4) & 15u) * 16u, oz = (e.id & 15u) * 16u;
                             atomicAdd(&sm.accA[k][tid], (unsigned long long)(n * ox + (e.srg & 4095u)) |
                                                             ((unsigned long long)(n * oy + (e.srg >> 12)) << 32));
-                            atomicAdd(&sm.accB[k][tid], (unsigned long long)(n * oz + e.sb) | ((unsigned long long)n << 32));
+                            atomicAdd(&sm.accB[k][tid], (unsigned long long)(n * oz + (e.sb & 16383u)) | ((unsigned long long)n << 32));
                         }
                         const bool sf = svalid && !pass;
                         const uint32_t c0 = (e.id >> 14) & 3u, ns1 = c0 + ((e.id >> 16) & 3u) - 1u;

@@ -217,10 +217,11 @@ static_assert(sizeof(CellEnt) == 16, "CellEnt is one 16-byte load");
 constexpr int kSupsPerPart = 256;  // 16 x 16 super-cells per partition
 struct SupEnt {
     uint32_t id;     // R << 8 | G4 << 4 | B4 in bits 0..13, cells of the j = 0 pair (0..2) in bits 14..15,
-                     // of the j = 1 pair in bits 16..17, colour count (<= 1024) in bits 18..28
+                     // of the j = 1 pair in bits 16..17, colour count (<= 1024) in bits 18..28, bit 18 of
+                     // s2 in bit 29
     uint32_t first;  // first0 | first1 << 16: the pairs' first cell indices in the image's cell table
     uint32_t srg;    // sum over its colours u = colour - origin: u_r (<= 3072) | u_g << 12 (<= 15360)
-    uint32_t sb;     // sum of u_b (<= 15360)
+    uint32_t sb;     // sum of u_b (<= 15360) | bits 0..17 of s2 << 14; s2 = sum of |u|^2 (<= 1024 x 459 < 2^19)
 };
 static_assert(sizeof(SupEnt) == 16, "SupEnt is one 16-byte load");
 struct KmeansCubes {

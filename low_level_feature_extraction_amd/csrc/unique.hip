@@ -534,6 +534,11 @@ __global__ __launch_bounds__(UT) __attribute__((amdgpu_waves_per_eu(8))) void k_
         // pairs' slots li (row 0, lane 2 B4) and li (row 1, lane 2 B4 + 32): first0 / first1.
         uint32_t qnc = ln | (ln ? 1u << 16 : 0u), qrb = lr | ((lb + 8u * (uint32_t)(B2 & 1) * ln) << 16),
                  qg = lg + 8u * (uint32_t)(G2 & 1) * ln;
+        // sum of |u|^2 about the super-cell origin: |u_cell + d|^2 summed, d = (0, 8 (G2 & 1), 8 (B2 & 1))
+        uint32_t q2 = l2 + 16u * ((uint32_t)(G2 & 1) * lg + (uint32_t)(B2 & 1) * lb) +
+                      64u * ln * (uint32_t)((G2 & 1) + (B2 & 1));
+        q2 += __shfl_xor(q2, 1);
+        q2 += __shfl_xor(q2, 32);
         qnc += __shfl_xor(qnc, 1);  // (row pair: counts and its cells)
         const uint32_t c_row1 = __shfl_xor(qnc, 32) >> 16, first1 = __shfl_xor(li, 32);
         qnc += __shfl_xor(qnc, 32) & 0xFFFFu;
@@ -547,8 +552,9 @@ __global__ __launch_bounds__(UT) __attribute__((amdgpu_waves_per_eu(8))) void k_
             e.id = ((uint32_t)R << 8) | ((uint32_t)(G2 >> 1) << 4) | (uint32_t)(B2 >> 1) | (c_row0 << 14) |
                    (c_row1 << 16) | ((qnc & 0xFFFFu) << 18);
             e.first = li | (first1 << 16);
+            e.id |= (q2 >> 18) << 29;
             e.srg = (qrb & 0xFFFFu) | (qg << 12);
-            e.sb = qrb >> 16;
+            e.sb = (qrb >> 16) | ((q2 & 0x3FFFFu) << 14);
             se[si] = e;
         }
     }
