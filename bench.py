@@ -245,7 +245,7 @@ def served_batcher(imgs_dev, feats, batches, seed, inflight, device):
             "launches": len(sizes), "mean_launch": round(sum(sizes) / max(len(sizes), 1), 1),
             "max_in_flight": bt.max_in_flight,
             "sample": f"{batches * B} single {imgs_dev.shape[2]}x{imgs_dev.shape[1]} device images from {producers} "
-                      f"concurrent asyncio producers through MicroBatcher.analyze (llfe_submit_images gather + "
+                      f"concurrent asyncio producers through MicroBatcher.analyze (llfe_submit_images, images read in place + "
                       f"the full GPU path, {inflight} launches in flight, results assembled per request)"}
 
 
