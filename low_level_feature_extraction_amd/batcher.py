@@ -111,7 +111,10 @@ def _resolve(futs, results):
 
 
 class MicroBatcher:
-    def __init__(self, features: Sequence[str] = ("colors", "shapes", "shadows"), max_batch: int = 64,
+    # max_batch: requests per launch at most (split further per image size by the device pass
+    # capacity, llfe_batch_capacity: 512 for 1080p); at light load launches stay small anyway
+    # (max_wait_ms), at high load a full pass amortises the k-means launch's tail
+    def __init__(self, features: Sequence[str] = ("colors", "shapes", "shadows"), max_batch: int = 512,
                  max_wait_ms: float = 2.0, run: Optional[Callable] = None, inflight: int = 3,
                  seed: Optional[int] = None, n_colors: int = 5, freeze_gc: bool = True, backend=None,
                  device: Optional[int] = None, fill_wait_ms: float = 8.0):
