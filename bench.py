@@ -679,6 +679,16 @@ def main():
     be.set_concurrency(True)
     be.set_profiling(False)
 
+    # the product request path at the same load: single-image requests through the
+    # MicroBatcher (SURVEY.md 8f row 3), beside `value`
+    served = None
+    if args.batcher_steps is None:
+        args.batcher_steps = args.steps
+    if args.batcher_steps > 0 and pipelined:
+        barrier()
+        served = served_batcher(imgs, feats, args.batcher_steps, args.seed, args.batcher_inflight, local)
+        barrier()
+
     # per-class throughput: the same step on an all-"ui" and an all-"photo"
     # batch of the same size (k-means cost scales with the unique-colour count U)
     per_class = None
@@ -705,16 +715,6 @@ def main():
                                "host_contour_busy": round(hc["busy_ms"] / 1e3 / (tc1 - tc0), 3),
                                "host_contour_ms_per_image": round(hc["busy_ms"] * hc["threads"] / max(hc["images"], 1), 3)}
             del cb
-
-    # the product request path at the same load: single-image requests through the
-    # MicroBatcher (SURVEY.md 8f row 3), beside `value`
-    served = None
-    if args.batcher_steps is None:
-        args.batcher_steps = args.steps
-    if args.batcher_steps > 0 and pipelined:
-        barrier()
-        served = served_batcher(imgs, feats, args.batcher_steps, args.seed, args.batcher_inflight, local)
-        barrier()
 
     # (the e2e lines run on every rank before rank 0 reports: each rank pays its own
     # host-side work, as a serving node would)
