@@ -295,6 +295,20 @@ __device__ __forceinline__ void rowpass4(uint32_t B, const float *__restrict__ k
 #ifndef LLFE_ST_LPT
 #define LLFE_ST_LPT 0
 #endif
+#ifndef LLFE_ST_QD
+#define LLFE_ST_QD 3  // input-row ring length: rows are loaded QD - 1 steps before use (divides 12)
+#endif
+#ifndef LLFE_ST_LDSQ
+#define LLFE_ST_LDSQ 0  // > 0: input rows through a per-wave LDS ring of this depth (divides 12), loaded
+                        // LDSQ - 1 steps ahead by direct-to-LDS loads (interior waves) or staged one
+                        // step in VGPRs (border / unaligned waves), instead of the Q VGPR ring
+#endif
+#ifndef LLFE_ST_HOTROW
+#define LLFE_ST_HOTROW 0  // (timing experiments only: every step loads the segment's first row, L2-hot)
+#endif
+#ifndef LLFE_ST_NOSTORE
+#define LLFE_ST_NOSTORE 0  // (timing experiments only: no class-map stores, wrong results)
+#endif
 #ifndef LLFE_ST_STORE_AUX
 #define LLFE_ST_STORE_AUX 2  // the class-map stores' cache policy (2: non-temporal)
 #endif
@@ -367,9 +381,26 @@ __device__ __forceinline__ void stencil_wave(int wid, const uint8_t *__restrict_
     // t >= H copy row t - 1; rows -5 .. -1 (the first segment) are filled with row 0 when it
     // is computed, at step 0, before anything reads them.
     constexpr int kU = 12;
-    const int t0 = ya - 5, t_end = yb + 5, ts = t0 - 6, tf = max(t0, 0);
+#if LLFE_ST_LDSQ
+    constexpr int QD = LLFE_ST_LDSQ;
+    // this wave's ring: QD rows of 64 lanes x 12 bytes (lane l's 4 BGR pixels at l * 12)
+    __shared__ __attribute__((aligned(16))) uint32_t qring[kWavesPerBlock][QD][192];
+    uint32_t(*const qr)[192] = qring[__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))];
+    // border waves load the window's raw row (x * 3 .. x * 3 + 11 per lane) through a buffer
+    // resource, so lanes left of column 0 / past the image's end read zeros instead of
+    // faulting, and take each pixel's REFLECT_101 column from the row in LDS (byte offsets
+    // within the window; every column a needed lane reflects to lies in it, others clamp)
+    const __amdgpu_buffer_rsrc_t irs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)img, (short)0, H * W * 3, 0x00020000);
+#else
+    constexpr int QD = LLFE_ST_QD;
+#endif
+    static_assert(kU % QD == 0, "the input ring's length must divide the unroll");
+    const int t0 = ya - 5, t_end = yb + 5, ts = t0 - 6 - (QD - 3), tf = max(t0, 0);
     const int tb0 = ts >= 0 ? ts - ts % kU : -(((-ts) + kU - 1) / kU) * kU;  // floor to a multiple of kU
-    Raw Q[3];
+#if !LLFE_ST_LDSQ
+    Raw Q[QD];
+#endif
     uint32_t G[6], bring[6], Mlo[3], Mhi[3];
     bool Mc[3];
     f32x2 ra[kU], rb[kU];
@@ -378,8 +409,15 @@ __device__ __forceinline__ void stencil_wave(int wid, const uint8_t *__restrict_
 #pragma unroll
     for (int k = 0; k < 6; k++) G[k] = bring[k] = 0;
 #pragma unroll
-    for (int k = 0; k < 3; k++) {
+    for (int k = 0; k < QD; k++) {
+#if LLFE_ST_LDSQ
+        qr[k][3 * lane] = qr[k][3 * lane + 1] = qr[k][3 * lane + 2] = 0u;
+#else
         Q[k] = Raw{0u, 0u, 0u};
+#endif
+    }
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
         Mlo[k] = Mhi[k] = 0;
         Mc[k] = false;
     }
@@ -397,10 +435,59 @@ __device__ __forceinline__ void stencil_wave(int wid, const uint8_t *__restrict_
             const int t = tb + k;
             if (t >= ts && t < t_end) {  // (no break: the loop must unroll so ring slots are registers)
             ST_MARK(load);
-            if (t + 2 < t_end) Q[(k + 2) % 3] = load_px(img, reflect101(t + 4, H), W, x, fast, coff);
-            if (t >= ts + 2) {
+#if LLFE_ST_LDSQ
+            if (t + QD - 1 < t_end) {
+                const int yl = reflect101(t + QD + 1, H);
+                uint32_t *const slot = &qr[(k + QD - 1) % QD][0];
+                if (fast) {
+                    __builtin_amdgcn_global_load_lds((const void *)(img + (size_t)yl * W * 3 + (uint32_t)(x * 3)),
+                                                     (void *)slot, 12, 0, 0);
+                } else if (vec) {
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(irs, (__attribute__((address_space(3))) void *)slot, 12,
+                                                             yl * W * 3 + x * 3, 0, 0, 0);
+                } else {  // unaligned rows: byte loads (REFLECT_101 columns), written now
+                    const Raw r = load_px(img, yl, W, x, false, coff);
+                    slot[3 * lane] = r.a;
+                    slot[3 * lane + 1] = r.b;
+                    slot[3 * lane + 2] = r.c;
+                }
+            }
+            if (t >= ts + QD - 1) {
                 ST_MARK(gray);
-                uint32_t g = gray4(Q[k % 3]);
+                // the direct-to-LDS row issued QD - 1 steps ago has landed once at most QD - 2
+                // younger vector-memory operations are outstanding (they complete in order;
+                // the compiler does not track these loads)
+                if (vec) __builtin_amdgcn_s_waitcnt(((QD - 2) & 15) | (7 << 4) | (15 << 8) | (((QD - 2) >> 4) << 14));
+                Raw cur;
+                if (edge && vec) {
+                    // (a needed lane's columns lie in the window; the others' offsets may fall
+                    // outside this wave's row: harmless reads of other rows or, out of the
+                    // workgroup's LDS, zeros)
+                    // (32-bit LDS addresses: with generic pointers the compiler hoisted a 64-bit
+                    // address per byte and slot out of the loop and spilled 100 VGPRs)
+                    const uint32_t rbase = (uint32_t)(uintptr_t)&qr[k % QD][0] - 3u * (uint32_t)xw0;
+                    uint32_t v[3] = {0u, 0u, 0u};
+#pragma unroll
+                    for (int j = 0; j < 4; j++)
+#pragma unroll
+                        for (int c = 0; c < 3; c++) {
+                            const int q = 3 * j + c;
+                            v[q >> 2] |= (uint32_t)(*(const __attribute__((address_space(3))) uint8_t *)(uintptr_t)(rbase + coff[j] + c))
+                                           << (8 * (q & 3));
+                        }
+                    cur = Raw{v[0], v[1], v[2]};
+                } else {
+                    const uint32_t *qs = &qr[k % QD][3 * lane];
+                    cur = Raw{qs[0], qs[1], qs[2]};
+                }
+                uint32_t g = gray4(cur);
+#else
+            if (t + QD - 1 < t_end)
+                Q[(k + QD - 1) % QD] = load_px(img, LLFE_ST_HOTROW ? ya : reflect101(t + QD + 1, H), W, x, fast, coff);
+            if (t >= ts + QD - 1) {
+                ST_MARK(gray);
+                uint32_t g = gray4(Q[k % QD]);
+#endif
                 ST_PIN(g);
                 G[(k + 2) % 6] = g;
             }
@@ -464,7 +551,8 @@ __device__ __forceinline__ void stencil_wave(int wid, const uint8_t *__restrict_
                     }
                     ST_PIN(o);
                     ST_MARK(store);
-                    if (out_fast) {
+                    if (LLFE_ST_NOSTORE) {
+                    } else if (out_fast) {
                         // buffer store: row offset yn * W in an SGPR, the lane's column x in a
                         // VGPR that never changes -- no per-lane 64-bit address per step
                         __builtin_amdgcn_raw_buffer_store_b32(o, crs, (uint32_t)x, yn * W, LLFE_ST_STORE_AUX);
