@@ -51,6 +51,20 @@ __global__ __launch_bounds__(64) void k_probe(const uint8_t *src, uint32_t *sink
     atomicAdd(bad + MODE, nbad);
 }
 
+// the raw layout: one dwordx3 DMA (global and buffer forms) into a zeroed 2 KB LDS buffer, dumped
+__global__ __launch_bounds__(64) void k_layout(const uint8_t *src, uint32_t *out, int n_bytes) {
+    __shared__ __attribute__((aligned(16))) uint32_t buf[2][512];
+    const int lane = threadIdx.x;
+    for (int i = lane; i < 1024; i += 64) (&buf[0][0])[i] = 0xEEEEEEEEu;
+    __syncthreads();
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)src, (short)0, n_bytes, 0x00020000);
+    __builtin_amdgcn_global_load_lds((const void *)(src + lane * 12), (void *)&buf[0][0], 12, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)&buf[1][0], 12, lane * 12, 0, 0, 0);
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+    __syncthreads();
+    for (int i = lane; i < 1024; i += 64) out[i] = (&buf[0][0])[i];
+}
+
 int main() {
     const int blocks = 4096;
     const size_t n = (size_t)blocks * R * 768;
@@ -66,6 +80,23 @@ int main() {
     hipMemset(bad, 0, 8);
     hipLaunchKernelGGL(k_probe<0>, dim3(blocks), dim3(64), 0, 0, d, sink, bad, (int)n);
     hipLaunchKernelGGL(k_probe<1>, dim3(blocks), dim3(64), 0, 0, d, sink, bad, (int)n);
+    uint32_t *lay;
+    hipMalloc(&lay, 4096);
+    hipLaunchKernelGGL(k_layout, dim3(1), dim3(64), 0, 0, d, lay, (int)n);
+    uint32_t hl[1024];
+    hipMemcpy(hl, lay, 4096, hipMemcpyDeviceToHost);
+    for (int form = 0; form < 2; form++) {
+        const uint32_t *L = hl + 512 * form, *S = (const uint32_t *)h;
+        int m12 = 0, m16 = 0, untouched = 0;
+        for (int l = 0; l < 64; l++)
+            for (int w = 0; w < 3; w++) {
+                m12 += L[3 * l + w] == S[3 * l + w];
+                m16 += L[4 * l + w] == S[3 * l + w];
+            }
+        for (int i = 0; i < 512; i++) untouched += L[i] == 0xEEEEEEEEu;
+        printf("%s dwordx3 -> LDS: words matching at lane*12: %d / 192, at lane*16: %d / 192, untouched words of 512: %d\n",
+               form ? "buffer" : "global", m12, m16, untouched);
+    }
     int hb[2];
     hipMemcpy(hb, bad, 8, hipMemcpyDeviceToHost);
     printf("glds dwordx3 ring: %d bad words; buffer ... lds ring: %d bad words (of %zu)\n", hb[0], hb[1], n / 4);
