@@ -15,12 +15,13 @@
 // needs -- blur5 +-2, Sobel / NMS +-1, Gauss11 +-5 on the blurred row -- comes from lanes
 // L-2 .. L+2 through DPP wave shifts, so 240 columns per wave are exact (1920 = 8 x
 // 240).  Vertical neighbours live in registers, in rings whose lengths divide the
-// 12-step unroll of the row loop (input rows 3, gray rows 6, blurred rows 6, CV_32F
-// row-pass results 12, magnitude rows 3), so every ring slot is a fixed register and no
-// step moves ring data.  One BGR row is loaded per step (3 dwords per lane, coalesced, two
-// steps ahead), each pixel is read from HBM once plus a 10/216-row halo (the
-// 16/256-column halo of neighbouring strips hits L2), and nothing goes through LDS: no
-// barriers, no halo recomputation beyond those margins.
+// 12-step unroll of the row loop (gray rows 6, blurred rows 6, CV_32F row-pass results 12,
+// magnitude rows 3), so every ring slot is a fixed register and no step moves ring data.
+// One BGR row is loaded per step, five steps ahead, straight into a per-wave LDS ring of 6
+// rows (round 6: 12-byte direct-to-LDS loads, a counted vmcnt wait before a row is read;
+// the round-5 kernel held 3 input rows in VGPRs, two steps ahead); each pixel is read from
+// HBM once plus a 10/216-row halo (the 16/256-column halo of neighbouring strips hits L2);
+// no barriers, no halo recomputation beyond those margins.
 //
 // Per step (blur row c = clamp(t, 0, H-1) enters; REPLICATE of the blurred image):
 //   gray row reflect101(c + 2) -> vertical then horizontal blur5 (exact integer, any
@@ -299,9 +300,10 @@ __device__ __forceinline__ void rowpass4(uint32_t B, const float *__restrict__ k
 #define LLFE_ST_QD 3  // input-row ring length: rows are loaded QD - 1 steps before use (divides 12)
 #endif
 #ifndef LLFE_ST_LDSQ
-#define LLFE_ST_LDSQ 0  // > 0: input rows through a per-wave LDS ring of this depth (divides 12), loaded
-                        // LDSQ - 1 steps ahead by direct-to-LDS loads (interior waves) or staged one
-                        // step in VGPRs (border / unaligned waves), instead of the Q VGPR ring
+#define LLFE_ST_LDSQ 6  // > 0: input rows through a per-wave LDS ring of this depth (divides 12), loaded
+                        // LDSQ - 1 steps ahead by direct-to-LDS loads (buffer loads with range checks
+                        // for border waves; byte loads for unaligned rows); 0: the Q VGPR ring
+                        // (rows two steps ahead; 2.60-2.65 vs 2.32-2.38 ms per 512 x 1080p, round 6)
 #endif
 #ifndef LLFE_ST_HOTROW
 #define LLFE_ST_HOTROW 0  // (timing experiments only: every step loads the segment's first row, L2-hot)
@@ -369,8 +371,8 @@ __device__ __forceinline__ void stencil_wave(int wid, const uint8_t *__restrict_
     // every ring's length divides 12, so each ring slot is a fixed register and no step
     // moves ring data -- round 4's 11-row unroll shifted its gray / input / magnitude rings
     // by register moves every step):
-    //   input rows  Q[3]   virtual row v = t + 4 issued at step t, consumed at step t + 2
-    //                      (two loads in flight), slot v % 3
+    //   input rows  LDS ring qr[6] (LLFE_ST_LDSQ; Q[3] in VGPRs without it): virtual row
+    //                      v = t + QD + 1 issued at step t, consumed at step t + QD - 1
     //   gray rows   G[6]   virtual row v = t + 2 converted at step t, slot v % 6 (gray row
     //                      reflect101(v): blur row t reads virtual rows t - 2 .. t + 2)
     //   blurred     bring[6]: row t, slot t % 6 (read back to row t - 5); CV_32F row pass
@@ -383,15 +385,29 @@ __device__ __forceinline__ void stencil_wave(int wid, const uint8_t *__restrict_
     constexpr int kU = 12;
 #if LLFE_ST_LDSQ
     constexpr int QD = LLFE_ST_LDSQ;
-    // this wave's ring: QD rows of 64 lanes x 12 bytes (lane l's 4 BGR pixels at l * 12)
-    __shared__ __attribute__((aligned(16))) uint32_t qring[kWavesPerBlock][QD][192];
-    uint32_t(*const qr)[192] = qring[__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))];
+    // this wave's ring: QD rows of 64 lanes x 16 bytes -- a 12-byte direct-to-LDS load puts lane
+    // l's bytes at l * 16, not l * 12 (measured, tools/debug/glds_probe.hip)
+    __shared__ __attribute__((aligned(16))) uint32_t qring[kWavesPerBlock][QD][256];
+    uint32_t(*const qr)[256] = qring[__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))];
     // border waves load the window's raw row (x * 3 .. x * 3 + 11 per lane) through a buffer
     // resource, so lanes left of column 0 / past the image's end read zeros instead of
     // faulting, and take each pixel's REFLECT_101 column from the row in LDS (byte offsets
     // within the window; every column a needed lane reflects to lies in it, others clamp)
+    // (32-bit buffer offsets: border waves of images of 2^31 bytes or more take the byte path)
+    const bool small_img = (long long)H * W * 3 < 0x7fffffffll;
     const __amdgpu_buffer_rsrc_t irs =
-        __builtin_amdgcn_make_buffer_rsrc((void *)img, (short)0, H * W * 3, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void *)img, (short)0, small_img ? H * W * 3 : 0, 0x00020000);
+    // LDS byte offset of each of the lane's REFLECT_101 columns in the ring row (column c of the
+    // window, d = c - xw0: lane d >> 2 at 16 B a lane, pixel d & 3 at 3 B a pixel); only border
+    // waves read them, out-of-window columns of lanes no output needs clamp to the row
+    // (held in coff, whose byte offsets only the unaligned-row path reads)
+    if (vec && small_img) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int d = min(max(reflect101(x + j, W) - xw0, 0), 255);
+            coff[j] = (uint32_t)((d >> 2) * 16 + (d & 3) * 3);
+        }
+    }
 #else
     constexpr int QD = LLFE_ST_QD;
 #endif
@@ -411,7 +427,7 @@ __device__ __forceinline__ void stencil_wave(int wid, const uint8_t *__restrict_
 #pragma unroll
     for (int k = 0; k < QD; k++) {
 #if LLFE_ST_LDSQ
-        qr[k][3 * lane] = qr[k][3 * lane + 1] = qr[k][3 * lane + 2] = 0u;
+        qr[k][4 * lane] = qr[k][4 * lane + 1] = qr[k][4 * lane + 2] = 0u;
 #else
         Q[k] = Raw{0u, 0u, 0u};
 #endif
@@ -442,14 +458,14 @@ __device__ __forceinline__ void stencil_wave(int wid, const uint8_t *__restrict_
                 if (fast) {
                     __builtin_amdgcn_global_load_lds((const void *)(img + (size_t)yl * W * 3 + (uint32_t)(x * 3)),
                                                      (void *)slot, 12, 0, 0);
-                } else if (vec) {
+                } else if (vec && small_img) {
                     __builtin_amdgcn_raw_ptr_buffer_load_lds(irs, (__attribute__((address_space(3))) void *)slot, 12,
                                                              yl * W * 3 + x * 3, 0, 0, 0);
                 } else {  // unaligned rows: byte loads (REFLECT_101 columns), written now
                     const Raw r = load_px(img, yl, W, x, false, coff);
-                    slot[3 * lane] = r.a;
-                    slot[3 * lane + 1] = r.b;
-                    slot[3 * lane + 2] = r.c;
+                    slot[4 * lane] = r.a;
+                    slot[4 * lane + 1] = r.b;
+                    slot[4 * lane + 2] = r.c;
                 }
             }
             if (t >= ts + QD - 1) {
@@ -459,13 +475,10 @@ __device__ __forceinline__ void stencil_wave(int wid, const uint8_t *__restrict_
                 // the compiler does not track these loads)
                 if (vec) __builtin_amdgcn_s_waitcnt(((QD - 2) & 15) | (7 << 4) | (15 << 8) | (((QD - 2) >> 4) << 14));
                 Raw cur;
-                if (edge && vec) {
-                    // (a needed lane's columns lie in the window; the others' offsets may fall
-                    // outside this wave's row: harmless reads of other rows or, out of the
-                    // workgroup's LDS, zeros)
+                if (edge && vec && small_img) {
                     // (32-bit LDS addresses: with generic pointers the compiler hoisted a 64-bit
                     // address per byte and slot out of the loop and spilled 100 VGPRs)
-                    const uint32_t rbase = (uint32_t)(uintptr_t)&qr[k % QD][0] - 3u * (uint32_t)xw0;
+                    const uint32_t rbase = (uint32_t)(uintptr_t)&qr[k % QD][0];
                     uint32_t v[3] = {0u, 0u, 0u};
 #pragma unroll
                     for (int j = 0; j < 4; j++)
@@ -477,7 +490,7 @@ __device__ __forceinline__ void stencil_wave(int wid, const uint8_t *__restrict_
                         }
                     cur = Raw{v[0], v[1], v[2]};
                 } else {
-                    const uint32_t *qs = &qr[k % QD][3 * lane];
+                    const uint32_t *qs = &qr[k % QD][4 * lane];
                     cur = Raw{qs[0], qs[1], qs[2]};
                 }
                 uint32_t g = gray4(cur);
