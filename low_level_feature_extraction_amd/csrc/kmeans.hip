@@ -46,6 +46,9 @@ constexpr int kCellMinCubes = LLFE_KM_CELL_MIN;  // cube count from which the sw
 #ifndef LLFE_KM_PP_SUPS
 #define LLFE_KM_PP_SUPS 0  // k-means++ sweeps test 4 x 16 x 16 super-cells before cells (measured slower)
 #endif
+#ifndef LLFE_KM_PP_SUPS_KK
+#define LLFE_KM_PP_SUPS_KK 0  // ... in the rounds with at most this many chosen centres (0: the first round)
+#endif
 #ifndef LLFE_KM_THREADS
 #define LLFE_KM_THREADS 512
 #endif
@@ -989,9 +992,10 @@ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, int K, uint64
                         __builtin_amdgcn_wave_barrier();  // (the list is rewritten next)
                     }
                 };
-#if LLFE_KM_PP_SUPS
-                if (stab) {
-                    // super-cells first (round 6), the same closed forms with extents (3, 15, 15); the
+                // (round 6) the first round (KK = 0: the sums of d(., c0), every box decided) walks
+                // the super-cells; the later rounds only with LLFE_KM_PP_SUPS (measured slower)
+                if (stab && (LLFE_KM_PP_SUPS || KK <= LLFE_KM_PP_SUPS_KK)) {
+                    // super-cells first, the same closed forms with extents (3, 15, 15); the
                     // cells of the undecided ones (one partition at a time) are listed in the wave's
                     // cell list (sm.cs) and go through the cell path, 64 at a time
                     const int *MKs = sm.margs, *NAs = sm.margs + kMaxK * kMaxK, *NBs = sm.margs + kMaxK * kMaxK + 3 * kMaxK;
@@ -1066,7 +1070,6 @@ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, int K, uint64
                         base = nb;
                     }
                 } else
-#endif
                 {
                 int run = __builtin_amdgcn_readfirstlane(grab());  // the current run's first cell
                 int base = run;
