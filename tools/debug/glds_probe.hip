@@ -2,7 +2,8 @@
 // LDS input ring uses them.  One wave per block streams R rows of 64 x 12 bytes through a
 // ring of D slots: the row for step t + D - 1 is issued at step t (global_load_lds_dwordx3, or
 // buffer_load_dwordx3 ... lds), a store is issued every step, and step t reads its row back
-// after s_waitcnt vmcnt(D - 2).  Mismatching words are counted per mode.
+// after s_waitcnt vmcnt(D - 2).  Mismatching words are counted per mode (ring lanes 16 bytes
+// apart: k_layout shows a 12-byte load lands at lane * 16).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -12,7 +13,7 @@ constexpr int D = 6, R = 64;
 
 template <int MODE>
 __global__ __launch_bounds__(64) void k_probe(const uint8_t *src, uint32_t *sink, int *bad, int n_bytes) {
-    __shared__ __attribute__((aligned(16))) uint32_t ring[D][192];
+    __shared__ __attribute__((aligned(16))) uint32_t ring[D][256];  // 16 bytes a lane (measured below)
     const int lane = threadIdx.x;
     const uint8_t *base = src + (size_t)blockIdx.x * R * 768;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)src, (short)0, n_bytes, 0x00020000);
@@ -35,7 +36,7 @@ __global__ __launch_bounds__(64) void k_probe(const uint8_t *src, uint32_t *sink
             if (t >= 0 && t < R) {
                 __builtin_amdgcn_s_waitcnt(((D - 2) & 15) | (7 << 4) | (15 << 8));
                 const int rs_ = ((t % D) + D) % D;
-                const uint32_t *q = &ring[rs_][3 * lane];
+                const uint32_t *q = &ring[rs_][4 * lane];
                 // expected bytes from the fill formula (no global loads of our own to wait for)
                 uint32_t e[3] = {0u, 0u, 0u};
                 const uint32_t i0 = blockIdx.x * R * 768u + (uint32_t)t * 768u + (uint32_t)lane * 12u;
