@@ -1226,6 +1226,22 @@ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, int K, uint64
 // keep the plain path's register-heavy prefetch out of the hot kernels.  (The body stays
 // in the kernel: as an inlined device function the Lloyd sweep lost its register budget
 // and spilled 20 VGPRs.)
+#ifndef LLFE_KM_XCD
+#define LLFE_KM_XCD 0  // measured slower: 14.45-14.48 -> 14.61-14.63 ms pipelined
+#endif
+// XCD-aware task order (round 6 experiment): workgroup b runs on XCD b mod 8 (in-order dispatch), and
+// the ten attempts of an image read the same cube / cell / super-cell tables and keys, so the
+// attempts of image slot i (LPT order) all go to XCD i mod 8 -- its r-th workgroup takes
+// attempt r mod 10 of its (r / 10)-th image -- and share that XCD's L2 instead of pulling the
+// tables into all eight.  The tasks of the last n mod 8 images keep their places.
+__device__ __forceinline__ int xcd_task(int b, int n_tasks) {
+    constexpr int X = 8;
+    const int t8 = n_tasks / (X * kAttempts) * (X * kAttempts);
+    if (!LLFE_KM_XCD || b >= t8) return b;
+    const int x = b % X, r = b / X;
+    return (x + X * (r / kAttempts)) * kAttempts + r % kAttempts;
+}
+
 template <bool kCubes, int kPhase, bool kQueue>
 __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__restrict__ keys, long long key_stride,
                                                    const long long *__restrict__ n_unique, int n_colors,
@@ -1238,7 +1254,7 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     KmSmem &sm = *reinterpret_cast<KmSmem *>(smem_raw);
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    int task = blockIdx.x;
+    int task = kQueue ? (int)blockIdx.x : xcd_task((int)blockIdx.x, n_tasks);
     if (kQueue) {
         if (tid == 0) sm.task = atomicAdd(queue, 1);
         __syncthreads();
