@@ -217,7 +217,7 @@ struct Work {
     DevBuf<uint32_t> d_raw, d_keys, d_kscratch, d_pmeta, d_tstrong, d_segtab;  // d_segtab: k_uq_scatter's run table
     DevBuf<CubeEnt> d_segcubes, d_cubes;
     DevBuf<CellEnt> d_segcells, d_cells;
-    DevBuf<SupEnt> d_segsups, d_sups;
+    DevBuf<SupEnt> d_sups;
     DevBuf<int32_t> d_ncubes, d_ncells, d_nsups;
     DevBuf<int64_t> d_nuniq;
     DevBuf<KmeansAttemptOut> d_att;
@@ -351,8 +351,7 @@ int chunk_for(int h, int w) {
     const double P = (double)h * (double)w;
     const double cubes = std::min(P, (double)kMaxCubes), cells = std::min(cubes, (double)kParts * kCellsPerPart);
     const double per_image = 16.0 * P +  // keys, segments, class map, labels, masks
-                             (double)kParts * (kCubesPerPart * sizeof(CubeEnt) + kCellsPerPart * sizeof(CellEnt) +
-                                               kSupsPerPart * sizeof(SupEnt)) +
+                             (double)kParts * (kCubesPerPart * sizeof(CubeEnt) + kCellsPerPart * sizeof(CellEnt)) +
                              cubes * sizeof(CubeEnt) + 2.0 * cells * sizeof(CellEnt);  // the gathered tables
     const double n = gb * 1e9 / per_image;
     return (int)std::max(1.0, std::min(n, (double)kMaxKmeansBatch));
@@ -670,7 +669,6 @@ int color_stage(llfe_ctx *ctx, Work &W, const uint8_t *img, const uint64_t *img_
     HIPCHK(ctx, W.d_segcells.ensure((size_t)n * kParts * kCellsPerPart));
     HIPCHK(ctx, W.d_cells.ensure((size_t)n * cell_stride));
     HIPCHK(ctx, W.d_ncells.ensure(n));
-    HIPCHK(ctx, W.d_segsups.ensure((size_t)n * kParts * kSupsPerPart));
     HIPCHK(ctx, W.d_sups.ensure((size_t)n * cell_stride));
     HIPCHK(ctx, W.d_nsups.ensure(n));
     HIPCHK(ctx, W.d_pmeta.ensure((size_t)n * kParts * 5));
@@ -697,10 +695,10 @@ int color_stage(llfe_ctx *ctx, Work &W, const uint8_t *img, const uint64_t *img_
     // the partitions' sorted unique keys go to the (free) d_raw
     TIMED(ctx, s, "k_uq_part", (double)n * 4194304.0,
           launch_uq_part(W.d_keys.p, n, key_stride, P, hist, W.d_segtab.p, W.d_raw.p, W.d_segcubes.p,
-                         W.d_segcells.p, W.d_segsups.p, uq, cc, cl, cs, s));
+                         W.d_segcells.p, uq, cc, cl, cs, s));
     TIMED(ctx, s, "k_uq_gather", 0,
           launch_uq_gather(W.d_raw.p, n, key_stride, hist, uq, cc, cl, cs, W.d_segcubes.p, W.d_segcells.p,
-                           W.d_segsups.p, W.d_keys.p, W.d_cubes.p, W.d_cells.p, W.d_sups.p, cube_stride, cell_stride,
+                           W.d_keys.p, W.d_cubes.p, W.d_cells.p, W.d_sups.p, cube_stride, cell_stride,
                            cell_stride, W.d_nuniq.p, W.d_ncubes.p, W.d_ncells.p, W.d_nsups.p, contiguous_keys, s));
     return LLFE_OK;
 }

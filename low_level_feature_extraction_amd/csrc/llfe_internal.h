@@ -264,10 +264,10 @@ hipError_t launch_uq_scatter(const uint8_t *bgr, const uint64_t *img_tab, const 
                              uint32_t *seg, hipStream_t s);
 hipError_t launch_uq_part(const uint32_t *seg, int n, int64_t key_stride, int64_t P, const uint32_t *hist,
                           const uint32_t *tab, uint32_t *skeys, CubeEnt *seg_cubes, CellEnt *seg_cells,
-                          SupEnt *seg_sups, uint32_t *uq, uint32_t *cc, uint32_t *cl, uint32_t *cs, hipStream_t s);
+                          uint32_t *uq, uint32_t *cc, uint32_t *cl, uint32_t *cs, hipStream_t s);
 hipError_t launch_uq_gather(const uint32_t *skeys, int n, int64_t key_stride, const uint32_t *hist, const uint32_t *uq,
                             const uint32_t *cc, const uint32_t *cl, const uint32_t *cs, const CubeEnt *seg_cubes,
-                            const CellEnt *seg_cells, const SupEnt *seg_sups, uint32_t *keys, CubeEnt *cubes,
+                            const CellEnt *seg_cells, uint32_t *keys, CubeEnt *cubes,
                             CellEnt *cells, SupEnt *sups, int64_t cube_stride, int64_t cell_stride, int64_t sup_stride,
                             int64_t *n_unique, int32_t *n_cubes, int32_t *n_cells, int32_t *n_sups, bool copy_keys,
                             hipStream_t s);

@@ -313,10 +313,8 @@ __device__ __forceinline__ unsigned long long scan_u64_wg(unsigned long long v, 
     return r;
 }
 
-// grid (64, n).  amdgpu_waves_per_eu(8): the super-cell sums (round 6) took the kernel from 62 to
-// 70 VGPRs, three workgroups per CU instead of four; held at 64 it spills 3 VGPRs in the unique-key
-// scans (a few scratch accesses per workgroup) and measured the faster of the two
-// (profiles/r6/kmeans_sups/var_time.txt: supb vs supa).
+// grid (64, n).  amdgpu_waves_per_eu(8): the super-cell count (round 6) took the kernel from 62
+// to 66 VGPRs (three workgroups per CU instead of four); held at 64 it needs no spill.
 // Reads the partition's keys as its runs in the step segments (`tab`), writes
 // the sorted unique keys to `skeys` at the partition's place in key order (capacity: its
 // hist count), and up to 4096 cube entries to `seg_cubes`.
@@ -324,7 +322,6 @@ __global__ __launch_bounds__(UT) __attribute__((amdgpu_waves_per_eu(8))) void k_
                                                 const uint32_t *__restrict__ hist, const uint32_t *__restrict__ tab,
                                                 uint32_t *__restrict__ skeys,
                                                 CubeEnt *__restrict__ seg_cubes, CellEnt *__restrict__ seg_cells,
-                                                SupEnt *__restrict__ seg_sups,
                                                 uint32_t *__restrict__ uq, uint32_t *__restrict__ cc,
                                                 uint32_t *__restrict__ cl, uint32_t *__restrict__ cs) {
     __shared__ __attribute__((aligned(16))) uint32_t W[4 * 2048];  // rows r = 4R + i, word g << 3 | b >> 5
@@ -432,7 +429,8 @@ __global__ __launch_bounds__(UT) __attribute__((amdgpu_waves_per_eu(8))) void k_
         }
         if (t == 0) uq[(size_t)img * NPART + R] = sbase_q;
     }
-    // (b) the partition's 4x4x4 cubes, 4x8x8 cells and 4x16x16 super-cells.  In pass h thread
+    // (b) the partition's 4x4x4 cubes and 4x8x8 cells, and its count of occupied 4x16x16
+    // super-cells (their entries are built by k_uq_gather from the cells).  In pass h thread
     // t owns cell (G2, B2) = (c >> 5, c & 31), c = h UT + t, and its four cubes (G, B) =
     // (2 G2 + j, 2 B2 + cc), written in cell order and within a cell in (j, cc) order, so a
     // cell's cubes are consecutive; bit i*16 + jj*4 + bb of a cube = colour (4R + i, 4G + jj,
@@ -442,7 +440,6 @@ __global__ __launch_bounds__(UT) __attribute__((amdgpu_waves_per_eu(8))) void k_
     uint32_t cbase = 0, lbase = 0, sbase_s = 0;
     CubeEnt *ce = seg_cubes + ((size_t)img * NPART + R) * 4096;
     CellEnt *le = seg_cells + ((size_t)img * NPART + R) * kCellsPerPart;
-    SupEnt *se = seg_sups + ((size_t)img * NPART + R) * kSupsPerPart;
 #pragma unroll 1
     for (int h = 0; h < kCellsPerPart / UT; h++) {
         const int cell = h * UT + t, G2 = cell >> 5, B2 = cell & 31;
@@ -476,7 +473,6 @@ __global__ __launch_bounds__(UT) __attribute__((amdgpu_waves_per_eu(8))) void k_
         const unsigned long long pos = scan_u64_wg(mine, tmp, &tot);
         uint32_t ci = cbase + (uint32_t)pos;
         const uint32_t li = lbase + (uint32_t)((pos >> 32) & 0xFFFFu), first = ci;
-        const uint32_t si = sbase_s + (uint32_t)(pos >> 48);
         cbase += (uint32_t)tot;
         lbase += (uint32_t)((tot >> 32) & 0xFFFFu);
         sbase_s += (uint32_t)(tot >> 48);
@@ -527,36 +523,6 @@ __global__ __launch_bounds__(UT) __attribute__((amdgpu_waves_per_eu(8))) void k_
             e.s2 = l2;
             le[li] = e;
         }
-        // the super-cell's count and sums over u = colour - (4R, 16 G4, 16 B4): the quad's cell
-        // sums shifted by their cells' offsets (0, 8 (G2 & 1), 8 (B2 & 1)), packed in pairs of
-        // 16-bit fields (count <= 1024 | occupied cells of the lane's row pair << 16, u_r <= 3072
-        // | u_b <= 15360 << 16; u_g <= 15360).  Its cells are the occupied ones among the row
-        // pairs' slots li (row 0, lane 2 B4) and li (row 1, lane 2 B4 + 32): first0 / first1.
-        uint32_t qnc = ln | (ln ? 1u << 16 : 0u), qrb = lr | ((lb + 8u * (uint32_t)(B2 & 1) * ln) << 16),
-                 qg = lg + 8u * (uint32_t)(G2 & 1) * ln;
-        // sum of |u|^2 about the super-cell origin: |u_cell + d|^2 summed, d = (0, 8 (G2 & 1), 8 (B2 & 1))
-        uint32_t q2 = l2 + 16u * ((uint32_t)(G2 & 1) * lg + (uint32_t)(B2 & 1) * lb) +
-                      64u * ln * (uint32_t)((G2 & 1) + (B2 & 1));
-        q2 += __shfl_xor(q2, 1);
-        q2 += __shfl_xor(q2, 32);
-        qnc += __shfl_xor(qnc, 1);  // (row pair: counts and its cells)
-        const uint32_t c_row1 = __shfl_xor(qnc, 32) >> 16, first1 = __shfl_xor(li, 32);
-        qnc += __shfl_xor(qnc, 32) & 0xFFFFu;
-        qrb += __shfl_xor(qrb, 1);
-        qrb += __shfl_xor(qrb, 32);
-        qg += __shfl_xor(qg, 1);
-        qg += __shfl_xor(qg, 32);
-        if (lead && (qnc & 0xFFFFu)) {
-            const uint32_t c_row0 = qnc >> 16;
-            SupEnt e;
-            e.id = ((uint32_t)R << 8) | ((uint32_t)(G2 >> 1) << 4) | (uint32_t)(B2 >> 1) | (c_row0 << 14) |
-                   (c_row1 << 16) | ((qnc & 0xFFFFu) << 18);
-            e.first = li | (first1 << 16);
-            e.id |= (q2 >> 18) << 29;
-            e.srg = (qrb & 0xFFFFu) | (qg << 12);
-            e.sb = (qrb >> 16) | ((q2 & 0x3FFFFu) << 14);
-            se[si] = e;
-        }
     }
     if (t == 0) {
         cc[(size_t)img * NPART + R] = cbase;
@@ -576,8 +542,7 @@ __global__ __launch_bounds__(GT) void k_uq_gather(const uint32_t *__restrict__ s
                                                   const uint32_t *__restrict__ cc, const uint32_t *__restrict__ cl,
                                                   const uint32_t *__restrict__ cs,
                                                   const CubeEnt *__restrict__ seg_cubes,
-                                                  const CellEnt *__restrict__ seg_cells,
-                                                  const SupEnt *__restrict__ seg_sups, uint32_t *__restrict__ keys,
+                                                  const CellEnt *__restrict__ seg_cells, uint32_t *__restrict__ keys,
                                                   CubeEnt *__restrict__ cubes, CellEnt *__restrict__ cells,
                                                   SupEnt *__restrict__ sups,
                                                   long long cube_stride, long long cell_stride, long long sup_stride,
@@ -627,12 +592,52 @@ __global__ __launch_bounds__(GT) void k_uq_gather(const uint32_t *__restrict__ s
         e.first += cbase;
         ol[i] = e;
     }
-    const SupEnt *ssp = seg_sups + ((size_t)img * NPART + R) * kSupsPerPart;
-    SupEnt *os = sups + (size_t)img * sup_stride + ss;
-    for (uint32_t i = t; i < S; i += GT) {
-        SupEnt e = ssp[i];
-        e.first += lbase | (lbase << 16);  // (both cell indices; an image's cells are < 65536)
-        os[i] = e;
+    // the partition's super-cells (round 6), thread t = super-cell (G4, B4) = (t >> 4, t & 15):
+    // its cells (2 G4 + j, 2 B4 + c) from a map of the partition's cells by (G2, B2), its count
+    // and sums over u = colour - (4R, 16 G4, 16 B4) from the cells' (cell offsets (0, 8j, 8c)),
+    // its slot from a workgroup scan in (G4, B4) order (k_uq_part counted them: S)
+    static_assert(GT == kSupsPerPart, "one thread per super-cell of a partition");
+    __shared__ short cmap[kCellsPerPart];
+    __shared__ uint32_t wsum[GT / 64];
+    for (int i = t; i < kCellsPerPart; i += GT) cmap[i] = -1;
+    __syncthreads();
+    for (uint32_t i = t; i < L; i += GT) cmap[slp[i].id & (kCellsPerPart - 1)] = (short)i;
+    __syncthreads();
+    const int G4 = t >> 4, B4 = t & 15;
+    int cix[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) cix[q] = cmap[((2 * G4 + (q >> 1)) << 5) | (2 * B4 + (q & 1))];
+    const bool occ = (cix[0] & cix[1] & cix[2] & cix[3]) >= 0;  // some cell present (the AND is -1 only when all are)
+    const unsigned long long bal = __ballot(occ);
+    const int lane = t & 63, wv = t >> 6;
+    if (lane == 0) wsum[wv] = (uint32_t)__popcll(bal);
+    __syncthreads();
+    uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+    for (int w = 0; w < wv; w++) rank += wsum[w];
+    if (occ && rank < S) {
+        uint32_t n = 0, sr = 0, sg = 0, sb = 0, s2 = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            if (cix[q] < 0) continue;
+            const CellEnt e = slp[cix[q]];
+            const uint32_t j8 = 8u * (uint32_t)(q >> 1), c8 = 8u * (uint32_t)(q & 1);
+            const uint32_t ln = (e.id >> 18) & 511u, lr = e.sums & 1023u, lg = (e.sums >> 10) & 2047u, lb = e.sums >> 21;
+            n += ln;
+            sr += lr;
+            sg += lg + j8 * ln;
+            sb += lb + c8 * ln;
+            s2 += e.s2 + 2u * (j8 * lg + c8 * lb) + ln * (j8 * j8 + c8 * c8);
+        }
+        const uint32_t c0 = (cix[0] >= 0) + (cix[1] >= 0), c1 = (cix[2] >= 0) + (cix[3] >= 0);
+        const uint32_t f0 = cix[0] >= 0 ? cix[0] : (cix[1] >= 0 ? cix[1] : 0);
+        const uint32_t f1 = cix[2] >= 0 ? cix[2] : (cix[3] >= 0 ? cix[3] : 0);
+        SupEnt e;
+        e.id = ((uint32_t)R << 8) | ((uint32_t)G4 << 4) | (uint32_t)B4 | (c0 << 14) | (c1 << 16) | (n << 18) |
+               ((s2 >> 18) << 29);
+        e.first = (lbase + f0) | ((lbase + f1) << 16);  // (an image's cells are < 65536)
+        e.srg = sr | (sg << 12);
+        e.sb = sb | ((s2 & 0x3FFFFu) << 14);
+        sups[(size_t)img * sup_stride + ss + rank] = e;
     }
 }
 
@@ -675,20 +680,20 @@ hipError_t launch_uq_scatter(const uint8_t *bgr, const uint64_t *img_tab, const 
 
 hipError_t launch_uq_part(const uint32_t *seg, int n, int64_t key_stride, int64_t P, const uint32_t *hist,
                           const uint32_t *tab, uint32_t *skeys, CubeEnt *seg_cubes, CellEnt *seg_cells,
-                          SupEnt *seg_sups, uint32_t *uq, uint32_t *cc, uint32_t *cl, uint32_t *cs, hipStream_t s) {
+                          uint32_t *uq, uint32_t *cc, uint32_t *cl, uint32_t *cs, hipStream_t s) {
     hipLaunchKernelGGL(k_uq_part, dim3(NPART, n), dim3(UT), 0, s, seg, (long long)key_stride, (long long)P, hist, tab,
-                       skeys, seg_cubes, seg_cells, seg_sups, uq, cc, cl, cs);
+                       skeys, seg_cubes, seg_cells, uq, cc, cl, cs);
     return hipGetLastError();
 }
 
 hipError_t launch_uq_gather(const uint32_t *skeys, int n, int64_t key_stride, const uint32_t *hist, const uint32_t *uq,
                             const uint32_t *cc, const uint32_t *cl, const uint32_t *cs, const CubeEnt *seg_cubes,
-                            const CellEnt *seg_cells, const SupEnt *seg_sups, uint32_t *keys, CubeEnt *cubes,
+                            const CellEnt *seg_cells, uint32_t *keys, CubeEnt *cubes,
                             CellEnt *cells, SupEnt *sups, int64_t cube_stride, int64_t cell_stride, int64_t sup_stride,
                             int64_t *n_unique, int32_t *n_cubes, int32_t *n_cells, int32_t *n_sups, bool copy_keys,
                             hipStream_t s) {
     hipLaunchKernelGGL(k_uq_gather, dim3(NPART, n), dim3(GT), 0, s, skeys, (long long)key_stride, hist, uq, cc, cl, cs,
-                       seg_cubes, seg_cells, seg_sups, keys, cubes, cells, sups, (long long)cube_stride,
+                       seg_cubes, seg_cells, keys, cubes, cells, sups, (long long)cube_stride,
                        (long long)cell_stride, (long long)sup_stride, (long long *)n_unique, (int *)n_cubes,
                        (int *)n_cells, (int *)n_sups, copy_keys ? 1 : 0);
     return hipGetLastError();
