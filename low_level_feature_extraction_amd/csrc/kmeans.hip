@@ -1226,6 +1226,10 @@ void pp_cubes(KmSmem &sm, const uint32_t *__restrict__ pts, int N, int K, uint64
 // keep the plain path's register-heavy prefetch out of the hot kernels.  (The body stays
 // in the kernel: as an inlined device function the Lloyd sweep lost its register budget
 // and spilled 20 VGPRs.)
+#ifndef LLFE_KM_HIDE
+#define LLFE_KM_HIDE 0  // Lloyd: label staged colours between a list gather's issue and its use
+                        // (bit-identical, measured no faster: 14.54-14.59 vs 14.56-14.62 ms)
+#endif
 #ifndef LLFE_KM_XCD
 #define LLFE_KM_XCD 0  // measured slower: 14.45-14.48 -> 14.61-14.63 ms pipelined
 #endif
@@ -1825,6 +1829,11 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
                             ce.id = 0;
                             ce.sums = 0;
                             if (v) ce = ctab[ql[b + lane]];
+#if LLFE_KM_HIDE
+                            // staged boundary colours need no ce: label them while the gather is
+                            // in flight (integer sums, any order gives the same totals)
+                            while (head - tail >= 64) label_stage(64);
+#endif
                             cube_body(ce, v);
                         }
                         __builtin_amdgcn_wave_barrier();  // (the next batch rewrites the list)
@@ -1879,6 +1888,9 @@ __global__ __launch_bounds__(KT, LLFE_KM_MINW) void k_kmeans(const uint32_t *__r
                                 const bool v = b + lane < total;
                                 CellEnt ce{0u, 0u, 0u, 0u};
                                 if (v) ce = ltab[qs[b + lane]];
+#if LLFE_KM_HIDE
+                                while (head - tail >= 64) label_stage(64);  // (as above)
+#endif
                                 cell_body(ce, v);
                             }
                             __builtin_amdgcn_wave_barrier();
