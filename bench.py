@@ -488,7 +488,8 @@ def main():
 
         if os.environ.get("LLFE_BENCH_SHARE_GPU") != "1":
             have = visible_gpus()
-            if have < args.gpus:
+            # (0: no kfd topology readable here -- leave the check to the ranks' own runtimes)
+            if 0 < have < args.gpus:
                 raise SystemExit(f"bench.py: --gpus {args.gpus} but {have} GPUs are visible")
 
         sys.exit(subprocess.call(launch_ranks(args.gpus, sys.argv[1:])))
