@@ -231,7 +231,9 @@ def served_batcher(imgs_dev, feats, batches, seed, inflight, device):
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
     finally:
-        bt.close()
+        bt.close()  # (the worker's context and its workspaces are released with it)
+    del dev
+    torch.cuda.empty_cache()  # the request images' memory back to the device for the next legs
     sizes = bt.batch_sizes[n0:]
     log = [e for e in bt.launch_log[n0:] if e[2] is not None]
     # the worker's clock per launch: blocked in collect (the GPU still on it), and from one

@@ -114,6 +114,16 @@ class Backend:
                 b = cls._instances[key] = Backend(device)
             return b
 
+    @classmethod
+    def release(cls, backend: "Backend"):
+        """Drop a thread's cached context (``get``) and free its device workspaces -- for a
+        thread that is about to end, e.g. MicroBatcher's worker at close()."""
+        with cls._ilock:
+            for key, b in list(cls._instances.items()):
+                if b is backend:
+                    del cls._instances[key]
+        backend.close()
+
     def close(self):
         if self.ctx:
             with self._lock:

@@ -427,6 +427,10 @@ class MicroBatcher:
             raise
         finally:
             resolver.shutdown(wait=True)
+            if self._backend is None:  # the worker's own context: its workspaces go with it
+                from .backend import Backend
+
+                Backend.release(be)
 
     @staticmethod
     def _capacity(be, h, w) -> int:
