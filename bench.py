@@ -191,7 +191,7 @@ def e2e_host(be, imgs_dev, feats, steps, seed, index_base):
                       f"H2D + full GPU path per batch, two batches in flight (llfe_submit_batch / llfe_collect_batch)"}
 
 
-def served_batcher(imgs_dev, feats, batches, seed, inflight, device):
+def served_batcher(imgs_dev, feats, batches, seed, inflight, device, backend=None):
     """The product request path at load (the reference serves one
     image per /analyze call, app/api/v1/endpoints/analyze.py:94-111): P concurrent asyncio
     producers each await ``MicroBatcher.analyze`` on its own single 1080p device image
@@ -211,7 +211,11 @@ def served_batcher(imgs_dev, feats, batches, seed, inflight, device):
     producers = (inflight + 1) * B  # enough outstanding requests to keep every slot full
     dev = [imgs_dev[i % B].clone() for i in range(producers)]  # one allocation per request image
     torch.cuda.synchronize()
-    bt = MicroBatcher(features=feats, max_batch=B, max_wait_ms=2.0, inflight=inflight, seed=seed, device=device)
+    # the worker drives the rank's own context (`backend`; the main thread only waits on the
+    # event loop meanwhile), so the leg adds no second set of device workspaces
+    depth0 = backend.inflight if backend is not None else None
+    bt = MicroBatcher(features=feats, max_batch=B, max_wait_ms=2.0, inflight=inflight, seed=seed, device=device,
+                      backend=backend)
 
     async def drive(n_requests):
         counter = itertools.count()
@@ -231,7 +235,9 @@ def served_batcher(imgs_dev, feats, batches, seed, inflight, device):
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
     finally:
-        bt.close()  # (the worker's context and its workspaces are released with it)
+        bt.close()
+        if backend is not None:
+            backend.inflight = depth0  # (the batcher set its own depth on the context)
     del dev
     torch.cuda.empty_cache()  # the request images' memory back to the device for the next legs
     sizes = bt.batch_sizes[n0:]
@@ -689,7 +695,7 @@ def main():
         args.batcher_steps = args.steps
     if args.batcher_steps > 0 and pipelined:
         barrier()
-        served = served_batcher(imgs, feats, args.batcher_steps, args.seed, args.batcher_inflight, local)
+        served = served_batcher(imgs, feats, args.batcher_steps, args.seed, args.batcher_inflight, local, backend=be)
         barrier()
 
     # per-class throughput: the same step on an all-"ui" and an all-"photo"
