@@ -282,6 +282,9 @@ __global__ __launch_bounds__(KB) void k_uq_scatter(const uint8_t *__restrict__ b
 }
 
 // ------------------------------------------------------------------ partitions
+#ifndef LLFE_UQ_DMA
+#define LLFE_UQ_DMA 0  // > 0: runs' first keys through an LDS double buffer, this many runs a group
+#endif
 // k_uq_part threads per (image, partition): 512 (four workgroups per CU by LDS) measured
 // 2.34 ms per 512 x 1080p against 2.41 for 1024 and 3.04 for 256
 constexpr int UT = 512;
@@ -364,6 +367,76 @@ __global__ __launch_bounds__(UT) __attribute__((amdgpu_waves_per_eu(8))) void k_
         const uint32_t wi = ((k >> 16) & 3u) * 2048 + ((k >> 5) & 2047u), bit = 1u << (k & 31u);
         if (k != 0xFFFFFFFFu && !(W[wi] & bit)) atomicOr(&W[wi], bit);
     };
+#if LLFE_UQ_DMA
+    // (round 6 experiment) the runs' first 64 keys go straight to a per-wave LDS double buffer by
+    // direct-to-LDS loads, one group of RGD runs ahead of the group being marked; a counted
+    // vmcnt wait (the group issued after it) before a group's keys are read back
+    constexpr int RGD = LLFE_UQ_DMA;
+    __shared__ __attribute__((aligned(16))) uint32_t rstage[UT / 64][2][RGD][64];
+    uint32_t(*const rs)[RGD][64] = rstage[__builtin_amdgcn_readfirstlane(wid)];
+    auto wait_vm = [&](int n) __attribute__((always_inline)) {
+        switch (n) {  // (s_waitcnt takes an immediate)
+#define UQ_W(N) case N: __builtin_amdgcn_s_waitcnt((N) | (7 << 4) | (15 << 8)); break;
+            UQ_W(0) UQ_W(1) UQ_W(2) UQ_W(3) UQ_W(4) UQ_W(5) UQ_W(6) UQ_W(7) UQ_W(8)
+#undef UQ_W
+            default: __builtin_amdgcn_s_waitcnt(0 | (7 << 4) | (15 << 8)); break;
+        }
+    };
+    for (long long base = 0; base < nsteps; base += (UT / 64) * 64) {
+        const long long sl = base + wid + (UT / 64) * lane;  // this lane's run
+        const uint32_t e = sl < nsteps ? tb[(size_t)sl * NPART] : 0u;
+        const unsigned long long live = __ballot(e != 0u);
+        auto next_group = [&](int j) {  // the first group from run j with a live run (64: none)
+            while (j < 64 && !((live >> j) & ((1ull << RGD) - 1))) j += RGD;
+            return j;
+        };
+        auto issue = [&](int j0, int buf) __attribute__((always_inline)) {
+            int nd = 0;
+#pragma unroll
+            for (int j = 0; j < RGD; j++) {
+                const uint32_t ej = __builtin_amdgcn_readlane(e, j0 + j);
+                if (ej >> 16) {  // (uniform)
+                    const size_t st = (size_t)(base + wid + (UT / 64) * (j0 + j));
+                    if ((uint32_t)lane < (ej >> 16))
+                        __builtin_amdgcn_global_load_lds((const void *)(sg + st * SK + (ej & 0xFFFFu) + lane),
+                                                         (void *)&rs[buf][j][0], 4, 0, 0);
+                    nd++;
+                }
+            }
+            return nd;
+        };
+        int j0 = next_group(0), buf = 0;
+        if (j0 < 64) issue(j0, 0);
+        while (j0 < 64) {
+            const int j1 = next_group(j0 + RGD);
+            const int n1 = j1 < 64 ? issue(j1, buf ^ 1) : 0;
+            wait_vm(n1);  // group j0's loads have landed (at most the n1 of group j1 outstanding)
+#pragma unroll
+            for (int j = 0; j < RGD; j++) {
+                const uint32_t ej = __builtin_amdgcn_readlane(e, j0 + j);
+                mark((uint32_t)lane < (ej >> 16) ? rs[buf][j][lane] : 0xFFFFFFFFu);
+            }
+#pragma unroll
+            for (int j = 0; j < RGD; j++) {
+                const uint32_t ej = __builtin_amdgcn_readlane(e, j0 + j), c = ej >> 16;
+                if (c <= 64) continue;  // (uniform)
+                const uint32_t *rp = sg + (size_t)(base + wid + (UT / 64) * (j0 + j)) * SK + (ej & 0xFFFFu);
+                for (uint32_t i0 = 64; i0 < c; i0 += 64 * RG) {
+                    uint32_t q[RG];
+#pragma unroll
+                    for (int i = 0; i < RG; i++) {
+                        const uint32_t ix = i0 + 64 * i + lane;
+                        q[i] = ix < c ? rp[ix] : 0xFFFFFFFFu;
+                    }
+#pragma unroll
+                    for (int i = 0; i < RG; i++) mark(q[i]);
+                }
+            }
+            j0 = j1;
+            buf ^= 1;
+        }
+    }
+#else
     for (long long base = 0; base < nsteps; base += (UT / 64) * 64) {
         const long long sl = base + wid + (UT / 64) * lane;  // this lane's run
         const uint32_t e = sl < nsteps ? tb[(size_t)sl * NPART] : 0u;
@@ -397,6 +470,7 @@ __global__ __launch_bounds__(UT) __attribute__((amdgpu_waves_per_eu(8))) void k_
             }
         }
     }
+#endif
     __syncthreads();
     // (a) unique keys in ascending order: thread t owns words q * UT + t (q < NQ), so a
     // store instruction's lanes write neighbouring runs of the output (a few cache lines)
