@@ -55,6 +55,9 @@ __host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     return z ^ (z >> 31);
 }
 
+#ifndef LLFE_UQ_VSTORE
+#define LLFE_UQ_VSTORE 0  // (experiment) the scatter's segment in 16-byte stores (2: non-temporal)
+#endif
 constexpr int KB = 256;  // threads per scatter block: a step is 4096 pixels (512 / 1024: the
                          // scatter 1.67 -> 2.19 / 2.55 ms for part 2.41 -> 2.13 / 2.04)
 constexpr int PPT = 16;   // pixels per thread per block step
@@ -276,7 +279,20 @@ __global__ __launch_bounds__(KB) void k_uq_scatter(const uint8_t *__restrict__ b
         __syncthreads();
         const int tot = (int)min((long long)SK, P - st * SK);
         uint32_t *o = out + st * SK;
+#if LLFE_UQ_VSTORE
+        {  // (experiment) 16-byte stores of the step's segment (2: non-temporal)
+            typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+            const int t4 = tot >> 2;
+            for (int i = t; i < t4; i += KB) {
+                const u32x4 v = ((const u32x4 *)stage)[i];
+                if (LLFE_UQ_VSTORE == 2) __builtin_nontemporal_store(v, (u32x4 *)o + i);
+                else ((u32x4 *)o)[i] = v;
+            }
+            for (int i = (t4 << 2) + t; i < tot; i += KB) o[i] = stage[i];
+        }
+#else
         for (int i = t; i < tot; i += KB) o[i] = stage[i];
+#endif
         __syncthreads();
     }
 }
