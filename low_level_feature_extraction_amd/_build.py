@@ -18,6 +18,10 @@ SOURCES = ["llfe_api.cpp", "contours.cpp", "png_decode.cpp", "jpeg_decode.cpp", 
            "cvresize.hip", "text.hip", "gather.hip"]
 HEADERS = ["llfe_internal.h", "contours.h", "kmeans_common.h"]
 ARCH = os.environ.get("LLFE_OFFLOAD_ARCH", "gfx950")
+# sources compiled with LLVM's iterative ILP scheduler (-amdgpu-sched-strategy=iterative-ilp):
+# bit-identical, the stencil at 120 VGPRs without its 3 spills; round 6, four interleaved A/B
+# pairs: headline +0.65 %, k_stencil 2.375 -> 2.336 ms isolated
+ILP_SCHED = set(filter(None, os.environ.get("LLFE_ILP_SCHED", "stencil_stream.hip,kmeans.hip").split(",")))
 
 
 def _hipcc() -> str:
@@ -54,6 +58,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
         else:
             lang = ["-x", "hip", f"--offload-arch={ARCH}"]
         extra = ["-fno-slp-vectorize"] if src == "stencil_stream.hip" else []  # keep the scalar fma chains scalar
+        if src in ILP_SCHED:
+            extra += ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
         cmd = [hipcc, *common, *lang, *extra, "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)

@@ -6,7 +6,7 @@ kernel waits for a row with a hand-placed, counted ``s_waitcnt vmcnt(4)`` before
 (at most four younger ring loads outstanding, vector-memory operations completing in order).
 A ring read scheduled above its wait would read a row that has not landed yet -- wrong
 results that come and go with memory timing.  This test pins, in the ISA of the kernel the
-bench runs (k_stencil_stream<true, true>, built as _build.py builds it), that every ring
+bench runs (k_stencil_stream<true, true>, built with _build.py's flags), that every ring
 read (one ``ds_read_b96`` of the lane's 16-byte slot) comes after a ``vmcnt(4)`` wait with
 no other ring read in between, once per unrolled row step, and that the rows arrive by
 direct-to-LDS loads
@@ -43,6 +43,9 @@ def test_stencil_ring_reads_wait_for_their_rows(tmp_path):
     cmd = [_hipcc(), "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize",
            f"-I{os.path.join(ROOT, 'include')}", "--offload-arch=gfx950", "--cuda-device-only", "-S", SRC,
            "-o", str(out)]
+    from low_level_feature_extraction_amd import _build
+    if "stencil_stream.hip" in _build.ILP_SCHED:
+        cmd[1:1] = ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
     subprocess.run(cmd, check=True, capture_output=True, timeout=600)
     f = _function(out.read_text(), r"k_stencil_streamILb1ELb1E")
     lines = f.splitlines()
