@@ -2,7 +2,8 @@
 // KMEANS_PP_CENTERS) for a batch of images on gfx950
 // (app/services/analyze/color_extractor.py:189-197).
 //
-// One 512-thread workgroup per (image, attempt), two per CU; workgroups are issued largest-U
+// One 256-thread workgroup per (image, attempt), four per CU (round 6; 512 threads / two per CU
+// before, LLFE_KM_THREADS); workgroups are issued largest-U
 // first (LPT) so the many short "ui" attempts back-fill behind the long "photo" ones.
 // The point set is the compacted unique-colour key list (4 B / point, ascending =
 // np.unique row order); wave w owns a contiguous range of 256-point steps and reads
@@ -50,7 +51,8 @@ constexpr int kCellMinCubes = LLFE_KM_CELL_MIN;  // cube count from which the sw
 #define LLFE_KM_PP_SUPS_KK 0  // ... in the rounds with at most this many chosen centres (0: the first round)
 #endif
 #ifndef LLFE_KM_THREADS
-#define LLFE_KM_THREADS 512
+#define LLFE_KM_THREADS 256  // (round 6) 256-thread workgroups, four per CU: the pipelined step 20.5 ->
+                             // 18.8 ms although an isolated launch is slower
 #endif
 constexpr int KT = LLFE_KM_THREADS;  // threads per (image, attempt)
 constexpr int KW = KT / 64;       // waves
@@ -147,7 +149,8 @@ constexpr int PF = 4;  // steps of 16-B key loads kept in flight per wave
 constexpr int kSelSteps = ((4 * 256 * 256 + 3 + STEP - 1) / STEP + KW - 1) / KW + 1;
 constexpr int SEL_U = 4;
 #ifndef LLFE_KM_UNROLL
-#define LLFE_KM_UNROLL 4
+#define LLFE_KM_UNROLL 2  // failing cubes per push trip (2: the 256-entry ring that fits four
+                          // 256-thread workgroups per CU)
 #endif
 #ifndef LLFE_KM_PPRUN
 #define LLFE_KM_PPRUN 4
@@ -222,8 +225,12 @@ struct KmSmem {
     int margs[kMaxK * kMaxK + 6 * kMaxK];  // ... and the 4 x 16 x 16 super-cells
 };
 
-// two workgroups per CU (160 KB of LDS)
-static_assert(sizeof(KmSmem) <= 80 * 1024, "KmSmem must leave room for two workgroups per CU");
+// 1024 / KT workgroups per CU (160 KB of LDS): two of 512 threads, four of 256
+static_assert(sizeof(KmSmem) * (1024 / KT) <= 160 * 1024, "KmSmem must leave room for 1024 / KT workgroups per CU");
+// the k-means++ selection's step sums alias the Lloyd accumulators (accA, then accB)
+static_assert(offsetof(KmSmem, accB) == sizeof(((KmSmem *)nullptr)->accA) &&
+                  3 * KW * kSelSteps * sizeof(uint32_t) <= 2 * sizeof(((KmSmem *)nullptr)->accA),
+              "selection step sums overflow the Lloyd accumulators (KT too small)");
 
 __device__ __forceinline__ Cent load_centres(const float (*c)[3]) {
     Cent r;
