@@ -459,13 +459,14 @@ def main():
                     help="steps of an all-ui and an all-photo batch (SURVEY.md 8d per-class throughput; 4 steps "
                          "left the pipeline's fill and drain in a third of the timed region: ui 21-30k across "
                          "round-5 runs); 0 disables")
-    ap.add_argument("--batcher-inflight", type=int, default=3,
-                    help="launches the batcher keeps in flight (MicroBatcher's default, 3: the request path's "
-                         "host work -- request futures, descriptors, result dicts -- shares the GIL with the "
-                         "serving thread, so it keeps one more launch queued than `value`'s loop)")
+    ap.add_argument("--batcher-inflight", type=int, default=2,
+                    help="launches the batcher keeps in flight (MicroBatcher's default, 2 like `value`'s loop; "
+                         "with four 256-thread k-means workgroups per CU a third launch in flight costs more "
+                         "than it hides: 0.935 vs 0.99 of `value`, profiles/r6/batcher/depth_ab_kt256.txt)")
     ap.add_argument("--batcher-steps", type=int, default=None,
-                    help="launches of B requests the served_batcher line times (default: --steps, so its "
-                         "pipeline fill and drain are amortised like `value`'s); 0 disables the line "
+                    help="launches of B requests the served_batcher line times (default: 2 x --steps: its "
+                         "fill and drain -- producers ramping up, the last launches' futures -- are longer "
+                         "than `value`'s; at 20 launches the ratio spread 0.88-0.97 between runs); 0 disables the line "
                          "(single-image requests through MicroBatcher)")
     ap.add_argument("--contours", choices=["auto", "host", "gpu"], default="auto",
                     help="where findContours + the shape loop run: the host pool from the copied-back mask "
@@ -692,7 +693,7 @@ def main():
     # MicroBatcher, beside `value`
     served = None
     if args.batcher_steps is None:
-        args.batcher_steps = args.steps
+        args.batcher_steps = 2 * args.steps
     if args.batcher_steps > 0 and pipelined:
         barrier()
         served = served_batcher(imgs, feats, args.batcher_steps, args.seed, args.batcher_inflight, local, backend=be)

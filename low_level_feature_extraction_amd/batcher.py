@@ -7,8 +7,8 @@ single worker thread (with its own device context) drains up to ``max_batch`` im
 whatever arrived within ``max_wait_ms`` of the first one, into one launch.
 
 The worker runs the serving loop the headline measures (bench.py): it keeps ``inflight``
-(default 3: its Python side shares the GIL with the event loop and the resolver, so one
-more launch stays queued than in the bench's loop) launches in flight through
+(default 2, like the bench's loop: with four 256-thread k-means workgroups per CU a third
+launch in flight slows the GPU more than it hides host work) launches in flight through
 ``Backend.submit_images`` / ``Backend.collect``
 (llfe_submit_images reads the requests' separately allocated device images in place through
 an address table, or gathers other layouts on the device; batch k + 1's kernels start in
@@ -115,7 +115,7 @@ class MicroBatcher:
     # capacity, llfe_batch_capacity: 512 for 1080p); at light load launches stay small anyway
     # (max_wait_ms), at high load a full pass amortises the k-means launch's tail
     def __init__(self, features: Sequence[str] = ("colors", "shapes", "shadows"), max_batch: int = 512,
-                 max_wait_ms: float = 2.0, run: Optional[Callable] = None, inflight: int = 3,
+                 max_wait_ms: float = 2.0, run: Optional[Callable] = None, inflight: int = 2,
                  seed: Optional[int] = None, n_colors: int = 5, freeze_gc: bool = True, backend=None,
                  device: Optional[int] = None, fill_wait_ms: float = 8.0):
         if max_batch < 1:
