@@ -57,7 +57,10 @@ __device__ __constant__ constexpr float kGauss11[11] = {LLFE_GAUSS11_F32};
 constexpr int kLanesOut = 60;               // lanes 2 .. 61 produce output
 constexpr int kStripW = 4 * kLanesOut;      // 240 output columns per wave
 constexpr int kHalo = 8;                    // columns left of the strip's first output
-constexpr int kWavesPerBlock = 4;
+#ifndef LLFE_ST_WPB
+#define LLFE_ST_WPB 4
+#endif
+constexpr int kWavesPerBlock = LLFE_ST_WPB;
 
 typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 typedef int16_t i16x2 __attribute__((ext_vector_type(2)));

@@ -303,7 +303,10 @@ __global__ __launch_bounds__(KB) void k_uq_scatter(const uint8_t *__restrict__ b
 #endif
 // k_uq_part threads per (image, partition): 512 (four workgroups per CU by LDS) measured
 // 2.34 ms per 512 x 1080p against 2.41 for 1024 and 3.04 for 256
-constexpr int UT = 512;
+#ifndef LLFE_UQ_UT
+#define LLFE_UQ_UT 512
+#endif
+constexpr int UT = LLFE_UQ_UT;
 
 __device__ __forceinline__ unsigned long long scan_u64_wg(unsigned long long v, unsigned long long *tmp,
                                                             unsigned long long *total) {
