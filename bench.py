@@ -750,12 +750,15 @@ def main():
             # PMC SQ_INSTS_VALU per launch (profiles/traffic_latest.json) over the launch's
             # VALU issue capacity (VALU_SLOTS_PER_S): how close the kernel is to its compute bound
             r["valu_busy"] = round(valu_insts[name] / (VALU_SLOTS_PER_S * avg_ms * 1e-3), 3)
-            # the limiter the counters show: VALU issue when it is > 70 % busy (frac stays
-            # the HBM fraction of the algorithmic bytes, against HBM peak)
-            if r["valu_busy"] > 0.7:
-                r["bound"] = "valu"
         if traffic.get(name) and avg_ms > 0:  # what the counters saw, beside the algorithmic rate
             r["hbm_gbs_pmc"] = round(traffic[name] / (avg_ms * 1e-3) / 1e9, 1)
+        if "valu_busy" in r:
+            # the limiter the counters show: the busier of VALU issue and the HBM bytes the
+            # counters saw (without a traffic count, VALU when it is > 70 % busy); frac stays
+            # the HBM fraction of the algorithmic bytes, against HBM peak
+            hbm_util = r["hbm_gbs_pmc"] / HBM_PEAK_GBS if "hbm_gbs_pmc" in r else 0.7
+            if r["valu_busy"] > hbm_util:
+                r["bound"] = "valu"
         return r
 
     kernels = {}
