@@ -17,6 +17,8 @@ LIB = os.path.join(PKG, "libllfe.so")
 SOURCES = ["llfe_api.cpp", "contours.cpp", "png_decode.cpp", "jpeg_decode.cpp", "stencil.hip", "stencil_stream.hip", "hysteresis.hip", "unique.hip", "kmeans.hip", "kmeans_big.hip", "resize.hip", "contours_gpu.hip",
            "cvresize.hip", "text.hip", "gather.hip"]
 HEADERS = ["llfe_internal.h", "contours.h", "kmeans_common.h"]
+# second builds of a source under another object name: (source, object stem, defines)
+RECOMPILE = [("kmeans.hip", "kmeans_wide", ["-DLLFE_KM_WIDE=1", "-DLLFE_KM_THREADS=512", "-DLLFE_KM_UNROLL=4"])]
 ARCH = os.environ.get("LLFE_OFFLOAD_ARCH", "gfx950")
 # sources compiled with LLVM's iterative ILP scheduler (-amdgpu-sched-strategy=iterative-ilp):
 # bit-identical, the stencil at 120 VGPRs without its 3 spills; round 6, four interleaved A/B
@@ -50,8 +52,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
     tmpdir = os.path.join(PKG, "build")
     os.makedirs(tmpdir, exist_ok=True)
     procs = []
-    for src in SOURCES:
-        obj = os.path.join(tmpdir, src + ".o")
+    for src, stem, defs in [(s, s, []) for s in SOURCES] + RECOMPILE:
+        obj = os.path.join(tmpdir, stem + ".o" if stem != src else src + ".o")
         objs.append(obj)
         if src in ("contours.cpp", "png_decode.cpp", "jpeg_decode.cpp"):  # pure host code
             lang = ["-x", "c++"]
@@ -60,7 +62,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         extra = ["-fno-slp-vectorize"] if src == "stencil_stream.hip" else []  # keep the scalar fma chains scalar
         if src in ILP_SCHED:
             extra += ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
-        cmd = [hipcc, *common, *lang, *extra, "-c", os.path.join(CSRC, src), "-o", obj]
+        cmd = [hipcc, *common, *lang, *extra, *defs, "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))

@@ -50,6 +50,11 @@ constexpr int kCellMinCubes = LLFE_KM_CELL_MIN;  // cube count from which the sw
 #ifndef LLFE_KM_PP_SUPS_KK
 #define LLFE_KM_PP_SUPS_KK 0  // ... in the rounds with at most this many chosen centres (0: the first round)
 #endif
+#ifndef LLFE_KM_WIDE
+#define LLFE_KM_WIDE 0  // 1: the second build of this file (_build.py: 512 threads, unroll 4) as
+                        // launch_kmeans_wide, which launch_kmeans hands batches whose attempts all
+                        // fit the GPU at once (small batches: an attempt on 8 waves finishes sooner)
+#endif
 #ifndef LLFE_KM_THREADS
 #define LLFE_KM_THREADS 256  // (round 6) 256-thread workgroups, four per CU: the pipelined step 20.5 ->
                              // 18.8 ms although an isolated launch is slower
@@ -2319,7 +2324,12 @@ __global__ void k_kmeans_finalize(const uint32_t *__restrict__ keys, long long k
 
 }  // namespace
 
-hipError_t launch_kmeans(const uint32_t *keys, int64_t key_stride, const int64_t *n_unique, int n, int n_colors,
+#if LLFE_KM_WIDE
+hipError_t launch_kmeans_wide(
+#else
+hipError_t launch_kmeans(
+#endif
+                         const uint32_t *keys, int64_t key_stride, const int64_t *n_unique, int n, int n_colors,
                          uint64_t seed, ImgIndex index, int32_t *order, uint32_t *scratch, int64_t scratch_stride,
                          KmeansAttemptOut *attempts, KmeansImageOut *out, const KmeansCubes &cubes,
                          hipStream_t s) {
@@ -2361,6 +2371,14 @@ hipError_t launch_kmeans(const uint32_t *keys, int64_t key_stride, const int64_t
             attr_set |= bit;
         }
     }
+#if !LLFE_KM_WIDE
+    // a batch whose attempts all fit at once gains nothing from the narrow workgroups' packing
+    // beside other kernels and runs each attempt at half width: the 512-thread build (round 6,
+    // 64 x 512^2 colours: 32.5k -> 41k images/s; 512 x 1080p: 27.2k narrow vs 24.9k wide)
+    if (cubes.cubes && n_colors <= kMaxK && !LLFE_KM_SPLIT && (int64_t)n * kAttempts <= slots_pp[dev])
+        return launch_kmeans_wide(keys, key_stride, n_unique, n, n_colors, seed, index, order, scratch,
+                                  scratch_stride, attempts, out, cubes, s);
+#endif
     hipLaunchKernelGGL(k_kmeans_order, dim3(1), dim3(OT), 0, s, (const long long *)n_unique, n, order);
     if (n_colors > kMaxK) {  // general K: plain sweeps over the keys (kmeans_big.hip)
         const hipError_t e = launch_kmeans_big(keys, key_stride, n_unique, n, n_colors, seed, index, order,
@@ -2391,6 +2409,8 @@ hipError_t launch_kmeans(const uint32_t *keys, int64_t key_stride, const int64_t
     return hipGetLastError();
 }
 
+#if !LLFE_KM_WIDE
 int64_t kmeans_scratch_stride(int64_t key_stride) { return 4 * ((key_stride + STEP - 1) / STEP) + 4; }
+#endif
 
 }  // namespace llfe

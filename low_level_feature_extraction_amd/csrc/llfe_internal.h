@@ -280,6 +280,12 @@ hipError_t launch_kmeans(const uint32_t *keys, int64_t key_stride, const int64_t
                          uint64_t seed, ImgIndex index, int32_t *order, uint32_t *scratch, int64_t scratch_stride,
                          KmeansAttemptOut *attempts, KmeansImageOut *out, const KmeansCubes &cubes,
                          hipStream_t s);
+// the same in 512-thread workgroups, two per CU (kmeans.hip built a second time with
+// LLFE_KM_WIDE): launch_kmeans calls it when every attempt of the batch fits the GPU at once
+hipError_t launch_kmeans_wide(const uint32_t *keys, int64_t key_stride, const int64_t *n_unique, int n, int n_colors,
+                              uint64_t seed, ImgIndex index, int32_t *order, uint32_t *scratch, int64_t scratch_stride,
+                              KmeansAttemptOut *attempts, KmeansImageOut *out, const KmeansCubes &cubes,
+                              hipStream_t s);
 // K in (kMaxK, kMaxColors]: the general-K attempts (kmeans_big.hip) in the order of
 // k_kmeans_order, into the same attempt records (launch_kmeans calls it)
 hipError_t launch_kmeans_big(const uint32_t *keys, int64_t key_stride, const int64_t *n_unique, int n, int n_colors,
