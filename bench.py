@@ -478,10 +478,11 @@ def main():
                          "kernel timings then come from the same steps run one batch at a time); "
                          "off: one llfe_process_batch per step")
     ap.add_argument("--inflight", choices=["auto", "2", "3"], default="auto",
-                    help="batches the pipelined loop keeps in flight: auto = 3 for steps of at most "
-                         "256 x 1080p pixels (short steps, where host jitter between collect and the next "
-                         "submit would otherwise idle the GPU: configs[1]/[2] measured +10-25 %%, "
-                         "profiles/r4/inflight/), else 2 (the headline: no difference, one workspace less)")
+                    help="batches the pipelined loop keeps in flight: auto = 3 for batches of at most 102 "
+                         "images (k-means' attempts all resident at once, its 512-thread build; 64 x 512^2: "
+                         "41.6k vs 32.5k), else 2 (the 256-thread k-means packs beside the next batch's "
+                         "kernels and a third batch only contends: 256 x 1080p colours+shapes 26.8k vs 22.1k, "
+                         "512 x 1080p 27.3k vs 25.4k; profiles/r6/kmeans_wg/depth_small.txt)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch the ranks, initialise the process group and run the control-plane collectives "
                          "(barrier, MAX over ranks), print the line's identity fields with value null; no workload")
@@ -560,8 +561,7 @@ def main():
     from low_level_feature_extraction_amd.backend import Backend
 
     be = Backend.get(local)
-    depth = (3 if args.batch * args.height * args.width <= 256 * 1080 * 1920 else 2) if args.inflight == "auto" \
-        else int(args.inflight)
+    depth = (3 if args.batch * 10 <= 1024 else 2) if args.inflight == "auto" else int(args.inflight)
     if args.pipeline == "on":
         be.inflight = depth
     if args.contours != "auto":
